@@ -1,0 +1,61 @@
+# Top-level build: the gfx950 HIP library (the product), the host library + CLIs above it, and
+# the oracle (test infrastructure).  hipcc cross-compiles for gfx950 without a GPU present.
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+LIBDIR   := imageencoder_amd/lib
+CSRC     := imageencoder_amd/csrc
+OBJDIR   := build
+# -ffp-contract=off: the exact FP64 path must not be fused into FMAs (reference op order);
+# the FP32 fast path uses explicit fmaf and is unaffected.
+HIPFLAGS := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -ffp-contract=off \
+            -Wall -Wno-unused-function
+KERNELS  := ie_encode
+OBJS     := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(KERNELS) ie_capi))
+
+.PHONY: all lib oracle ref host clean asmcheck
+all: lib host oracle
+
+lib: $(LIBDIR)/libie_hip.so
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.cuh include/ie_hip.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/ie_capi.o: $(CSRC)/ie_capi.cpp $(CSRC)/ie_device.h include/ie_hip.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libie_hip.so: $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+
+# ---- host library mirroring the reference interface + encoder/decoder CLIs
+HOSTSRC  := $(wildcard $(CSRC)/host/*.cpp)
+HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC)/host -Wall
+host: $(LIBDIR)/encoder $(LIBDIR)/decoder
+
+$(LIBDIR)/libie_host.a: $(HOSTSRC) $(wildcard $(CSRC)/host/*.hpp) include/ie_hip.h
+	@mkdir -p $(OBJDIR)/host $(LIBDIR)
+	for f in $(HOSTSRC); do $(CXX) $(HOSTFLAGS) -c $$f -o $(OBJDIR)/host/$$(basename $$f .cpp).o || exit 1; done
+	ar rcs $@ $(patsubst $(CSRC)/host/%.cpp,$(OBJDIR)/host/%.o,$(HOSTSRC))
+
+$(LIBDIR)/encoder: $(CSRC)/cli/main.cpp $(LIBDIR)/libie_host.a $(LIBDIR)/libie_hip.so
+	$(CXX) $(HOSTFLAGS) -DENCODER $< -L$(LIBDIR) -lie_host -lie_hip -Wl,-rpath,'$$ORIGIN' -o $@
+$(LIBDIR)/decoder: $(CSRC)/cli/main.cpp $(LIBDIR)/libie_host.a $(LIBDIR)/libie_hip.so
+	$(CXX) $(HOSTFLAGS) -DDECODER $< -L$(LIBDIR) -lie_host -lie_hip -Wl,-rpath,'$$ORIGIN' -o $@
+
+oracle:
+	$(MAKE) -C oracle oracle
+
+ref:
+	$(MAKE) -C oracle ref
+
+# Check the exact FP64 path really is unfused: dump the gfx950 ISA of the encode kernels.
+asmcheck:
+	@mkdir -p $(OBJDIR)/asm
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $(CSRC)/ie_encode.hip -o $(OBJDIR)/asm/ie_encode.s
+	@python3 tools/asmcheck.py $(OBJDIR)/asm/ie_encode.s
+
+clean:
+	rm -rf $(OBJDIR) $(LIBDIR)

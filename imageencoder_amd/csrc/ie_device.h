@@ -1,0 +1,93 @@
+// imageencoder_amd/csrc/ie_device.h -- structures shared by the host context (ie_capi.cpp) and
+// the gfx950 kernels (ie_encode.hip, ie_huffman.hip, ie_decode.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ie {
+
+constexpr int kTPB = 256;  // threads per workgroup: 4 waves of 64
+
+// Per-quant-matrix tables, built once on the host by ie_set_quant (ie_capi.cpp).
+struct EncTables {
+    // FP32 fast path (separable DCT, see encode_fast in ie_encode.hip)
+    float cf[64];   // cf[u*N+i] = float(c[u][i])
+    float g[64];    // float(S[uv] / q[uv])
+    float thr[64];  // near-tie half-width on |t|: |frac(|t|)-0.5| <= thr -> FP64 re-evaluation; <0: t exact
+    // FP64 reference order (algo.cpp:309-331, Block.cpp:149-152)
+    double S[64];   // C(u)*C(v)
+    double qd[64];  // double(q[uv])
+    double c[64];   // c[u*N+i] (std::cos, algo.cpp:318-319)
+    double P[64 * 64];  // P[uv*NN + ij] = c[u][i]*c[v][j]
+    // inverse (algo.cpp:343-363): R[uv*NN + ij] = ((C(u)*C(v))*c[u][i])*c[v][j]
+    double R[64 * 64];
+};
+
+// One encode launch.  Tiles (workgroups) never straddle frames; a "chain" is the sequence of
+// tiles whose bit offsets accumulate: the whole batch (concatenated stream) or one frame
+// (independent images, segmented = 1).
+struct EncArgs {
+    const uint8_t* y;
+    uint64_t stride, frame_pitch;
+    int w, h, nframes;
+    int bx, by;              // blocks per row / column
+    int gpr;                 // thread groups per block row = ceil(bx / BPT)
+    int groups_per_frame;    // gpr * by
+    int tiles_per_frame;     // ceil(groups_per_frame / kTPB)
+    int ntiles;
+    int rle;
+    int segmented;
+    int vec_ok;              // rows may be read with 16-/8-byte loads
+    uint32_t* out;           // 4-byte aligned, word w = stream bytes [4w, 4w+4)
+    uint64_t out_pitch_words;
+    uint64_t start_bit;
+    uint64_t* st_agg;        // [ntiles] {tag:8 | aggregate:24 | tail32:32}
+    uint64_t* st_inc;        // [ntiles] {tag:8 | inclusive:56}
+    unsigned long long* ticket;
+    unsigned long long ticket_base;
+    uint32_t tag;            // epoch tag 1..255
+    uint64_t* frame_start;   // [nframes] absolute start bit of each frame's payload
+    uint64_t* chain_end;     // [nchains] absolute end bit
+    unsigned* err;           // [0] look-back timeouts, [1] fallback coefficient count
+    const EncTables* tab;
+    int16_t* coef;           // optional: quantised coefficients, natural order, [nframes*bx*by][N*N]
+};
+
+void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s);
+
+struct PackArgs {            // Huffman re-encode / bit copy: one variable-length code per byte
+    const uint8_t* in;
+    uint64_t n;              // input bytes
+    const uint32_t* code;    // [256]
+    const uint8_t* len;      // [256]
+    int ntiles;
+    uint32_t* out;
+    uint64_t start_bit;
+    uint64_t* st_agg;
+    uint64_t* st_inc;
+    unsigned long long* ticket;
+    unsigned long long ticket_base;
+    uint32_t tag;
+    uint64_t* chain_end;
+    unsigned* err;
+};
+constexpr int kPackBytesPerThread = 16;
+void launch_pack(const PackArgs& a, hipStream_t s);
+void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, hipStream_t s);
+
+struct DecArgs {
+    const uint8_t* in;       // encoded bytes
+    uint64_t len;
+    uint64_t start_bit;
+    const uint64_t* block_bit;  // [nblocks] start bit of every block record (from the index pass)
+    int w, h, nframes, bx, by, rle;
+    uint8_t* out;
+    uint64_t stride, frame_pitch;
+    const EncTables* tab;
+};
+void launch_decode(const DecArgs& a, int n, hipStream_t s);
+int launch_decode_index(const uint8_t* in, uint64_t len, uint64_t start_bit, uint64_t nblocks, int n,
+                        int rle, uint64_t* block_bit, uint64_t* end_bit, void* scratch, size_t scratch_bytes,
+                        hipStream_t s);
+
+}  // namespace ie

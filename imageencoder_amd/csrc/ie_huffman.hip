@@ -1,0 +1,144 @@
+// imageencoder_amd/csrc/ie_huffman.hip -- device side of the Huffman post-pass (config 5).
+//
+// algo::Huffman<uint8_t>::encode (Huffman.cpp:233-344) is split three ways:
+//   hist_kernel   byte histogram + first occurrence of every value (the insertion order of the
+//                 reference's std::unordered_map, Huffman.cpp:237-243);
+//   (host)        tree / dictionary build, replayed with the reference's own libstdc++
+//                 containers (imageencoder_amd/csrc/host/Huffman.cpp);
+//   pack_kernel   re-encode every byte with its code, MSB-first (Huffman.cpp:314-319): the same
+//                 tile scan + LDS image + decoupled look-back + funnel store as the block encoder.
+// pack_kernel with the identity code (len 8) is also the shifted byte copy of the "no gain"
+// path ('0' + input, Huffman.cpp:329-341).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ie_common.cuh"
+#include "ie_device.h"
+
+namespace ie {
+
+constexpr int kHistTile = kTPB * 16;  // bytes per workgroup pass
+
+__global__ __launch_bounds__(kTPB) void hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t* hist,
+                                                     unsigned long long* first) {
+    __shared__ uint32_t h[256];
+    __shared__ unsigned long long f[256];
+    const int tid = threadIdx.x;
+    h[tid] = 0;
+    f[tid] = ~0ull;
+    __syncthreads();
+    for (uint64_t base = uint64_t(blockIdx.x) * kHistTile; base < n; base += uint64_t(gridDim.x) * kHistTile) {
+        const uint64_t p = base + uint64_t(tid) * 16;
+        uint8_t b[16];
+        if (p + 16 <= n && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
+            const uint4 v = *reinterpret_cast<const uint4*>(in + p);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 16; e++) b[e] = uint8_t(w[e >> 2] >> (8 * (e & 3)));
+        } else {
+#pragma unroll
+            for (int e = 0; e < 16; e++) b[e] = (p + e < n) ? in[p + e] : 0;
+        }
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            if (p + e < n) {
+                atomicAdd(&h[b[e]], 1u);
+                if (f[b[e]] > p + e) atomicMin(&f[b[e]], (unsigned long long)(p + e));
+            }
+        }
+    }
+    __syncthreads();
+    if (h[tid]) {
+        atomicAdd(&hist[tid], h[tid]);
+        atomicMin(&first[tid], f[tid]);
+    }
+}
+
+void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, hipStream_t s) {
+    const uint64_t tiles = (n + kHistTile - 1) / kHistTile;
+    const int grid = int(tiles < 2048 ? (tiles ? tiles : 1) : 2048);
+    hipLaunchKernelGGL(hist_kernel, dim3(grid), dim3(kTPB), 0, s, in, n, hist, first);
+}
+
+// One tile = kTPB threads x kPackBytesPerThread input bytes, codes of up to 32 bits.
+constexpr int kPackWords = kTPB * kPackBytesPerThread + 2;  // 32 bits per byte worst case
+
+__global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
+    __shared__ uint32_t smem[kPackWords + 16];
+    __shared__ uint32_t s_code[256];
+    __shared__ uint8_t s_len[256];
+    uint32_t* img = smem;
+    uint32_t* misc = smem + kPackWords;
+    const int tid = threadIdx.x;
+    if (tid == 0) misc[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+    s_code[tid] = a.code[tid];
+    s_len[tid] = a.len[tid];
+    __syncthreads();
+    const int t = int(misc[4]);
+    if (t >= a.ntiles) return;
+
+    const uint64_t p = uint64_t(t) * (kTPB * kPackBytesPerThread) + uint64_t(tid) * kPackBytesPerThread;
+    uint8_t b[kPackBytesPerThread];
+    int nb = 0;
+    if (p < a.n) nb = int(min<uint64_t>(kPackBytesPerThread, a.n - p));
+    if (nb == kPackBytesPerThread && ((reinterpret_cast<uintptr_t>(a.in) & 15) == 0)) {
+        const uint4 v = *reinterpret_cast<const uint4*>(a.in + p);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 16; e++) b[e] = uint8_t(w[e >> 2] >> (8 * (e & 3)));
+    } else {
+#pragma unroll
+        for (int e = 0; e < kPackBytesPerThread; e++) b[e] = (e < nb) ? a.in[p + e] : 0;
+    }
+    uint32_t mybits = 0;
+#pragma unroll
+    for (int e = 0; e < kPackBytesPerThread; e++) mybits += (e < nb) ? s_len[b[e]] : 0u;
+
+    uint32_t A;
+    const uint32_t off = block_excl_scan(mybits, misc, &A);
+    const uint32_t nw = (A + 31) >> 5;
+    for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
+    __syncthreads();
+    if (mybits) {
+        BitSink sink(img, off);
+#pragma unroll
+        for (int e = 0; e < kPackBytesPerThread; e++)
+            if (e < nb) sink.put(s_len[b[e]], s_code[b[e]]);
+        sink.finish();
+    }
+    __syncthreads();
+
+    const bool last = (t == a.ntiles - 1);
+    const uint32_t my_tail = (tid == 0) ? image_tail32(img, A) : 0u;
+    if (tid == 0 && A >= 32) st_state(&a.st_agg[t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | my_tail);
+    if (tid < 64) {
+        uint64_t excl = 0;
+        uint32_t ptail = 0;
+        if (t == 0) {
+            const uint32_t s = uint32_t(a.start_bit & 31);
+            ptail = s ? (bswap32(a.out[a.start_bit >> 5]) >> (32 - s)) : 0u;
+        } else {
+            excl = lookback(a.st_agg, a.st_inc, t, 0, a.tag, &ptail, a.err);
+        }
+        if (tid == 0) {
+            if (A < 32) {
+                const uint32_t tl = (A ? (ptail << A) : ptail) | my_tail;
+                st_state(&a.st_agg[t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
+            }
+            st_state(&a.st_inc[t], (uint64_t(a.tag) << 56) | ((excl + A) & kMask56));
+            misc[5] = uint32_t(excl);
+            misc[6] = uint32_t(excl >> 32);
+            misc[7] = ptail;
+            if (last) a.chain_end[0] = a.start_bit + excl + A;
+        }
+    }
+    __syncthreads();
+    const uint64_t excl = uint64_t(misc[5]) | (uint64_t(misc[6]) << 32);
+    store_image(a.out, img, A, a.start_bit + excl, misc[7], last);
+}
+
+void launch_pack(const PackArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(pack_kernel, dim3(a.ntiles), dim3(kTPB), 0, s, a);
+}
+
+}  // namespace ie

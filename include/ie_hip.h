@@ -1,0 +1,130 @@
+/* include/ie_hip.h -- the drop-in boundary: a C-ABI over the MI355X (gfx950) block codec.
+ *
+ * libie_hip.so replaces the LOOP BODY of the reference's frame encoders, i.e. everything between
+ * "blocks exist" and "payload bits are in the writer":
+ *
+ *   dc::ImageEncoder::process      ImageEncoder.cpp:96-147  (DCT+quant, RLE build, serial emission)
+ *   dc::Frame::process (I-frame)   Frame.cpp:129-159 + Frame::streamEncoded Frame.cpp:31-45
+ *   algo::Huffman<>::encode        Huffman.cpp:233-344      (histogram + re-encode; the tree build
+ *                                                            stays on the host, see ie_huffman_*)
+ *   dc::ImageDecoder::process      ImageDecoder.cpp:55-122  (parse + IDCT + clamp; ie_decode_*)
+ *
+ * A per-block C call would cross the host/device boundary 518 400 times per 4K frame, so the
+ * boundary is frame-batch level; dc::Block<> keeps its API in the host library (include/ie_host.hpp).
+ *
+ * Conventions
+ *   - Every function returns IE_OK (0) or a negative IE_E* code; ie_last_error() describes it.
+ *     No C++ exception crosses this boundary.
+ *   - Pixel and stream pointers may be host or device (hipMalloc) memory; the library detects
+ *     which (hipPointerGetAttributes).  With device pointers and NULL result pointers every call is
+ *     asynchronous on the context's stream.
+ *   - Streams are MSB-first (bit k = bit 7-k%8 of byte k/8, BitStream.cpp:61-77).  The library
+ *     only ORs bits in from `start_bit` on and never changes earlier bits, so a caller can write
+ *     the settings header with its own BitStreamWriter and hand over start_bit = header length.
+ *     Bits from start_bit on must be zero (the reference's writer buffer is zero-initialised,
+ *     utils.hpp:443-446).  Device output buffers are written in whole 32-bit words: size them
+ *     with ie_stream_bound().
+ *   - One context per device, not internally locked; one stream per context.
+ */
+#ifndef IE_HIP_H
+#define IE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ie_ctx ie_ctx;
+
+enum {
+    IE_OK = 0,
+    IE_EINVAL = -1,    /* bad argument: N not 4|8, W%N or H%N != 0, W/H > 32767 (15-bit DIM_BITS) */
+    IE_ECAP = -2,      /* output capacity too small */
+    IE_EHIP = -3,      /* HIP runtime error */
+    IE_ENOQUANT = -4,  /* ie_set_quant not called */
+    IE_EFORMAT = -5,   /* malformed encoded stream */
+    IE_EDEVICE = -6,   /* device-side protocol error (look-back timeout) */
+};
+
+enum {
+    IE_MODE_FAST = 0,  /* separable FP32 DCT + exact FP64 re-evaluation of near-tie coefficients */
+    IE_MODE_EXACT = 1, /* every coefficient in the reference's FP64 operation order */
+};
+
+/* Context lifetime.  device = HIP device ordinal. */
+int ie_create(int device, ie_ctx** out);
+int ie_destroy(ie_ctx* ctx);
+const char* ie_last_error(const ie_ctx* ctx);
+/* Run on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores
+ * the context's own stream. */
+int ie_set_stream(ie_ctx* ctx, void* hip_stream);
+int ie_sync(ie_ctx* ctx);
+
+/* Quantisation matrix, n x n row-major uint16 (MatrixReader<N>::read, MatrixReader.cpp:65-134;
+ * used as double[] via getData, :195-198).  n = 4 or 8 (the reference's compile-time
+ * dc::BlockSize, Block.hpp:13, becomes a runtime parameter).  The host builds the DCT cos table
+ * with std::cos in the reference's exact expression (algo.cpp:312,318-319).  q[k] must be > 0. */
+int ie_set_quant(ie_ctx* ctx, const uint16_t* q, int n);
+
+/* Upper bound in bytes of an output buffer for nframes frames of w x h encoded from start_bit
+ * (4 + 17*16 bits per 4x4 block, 4 + 65*16 per 8x8 block, rounded up to whole 32-bit words). */
+size_t ie_stream_bound(int w, int h, int n, int nframes, uint64_t start_bit);
+
+/* Encode nframes frames as ONE bit-contiguous stream of block records (the gop=1 video payload
+ * of Frame.cpp:31-45 / VideoEncoder.cpp:83-91; nframes = 1 is ImageEncoder's payload).
+ *   y            frame f row r starts at y + f*frame_pitch + r*stride
+ *   use_rle      Block::streamEncoded's use_rle (Block.cpp:372-413)
+ *   mode         IE_MODE_FAST or IE_MODE_EXACT (identical output)
+ *   out          stream buffer; records are appended from bit start_bit
+ *   frame_bits   optional [nframes]: payload bits of each frame
+ *   end_bit      optional: bit position after the last record
+ * Replaces ImageEncoder.cpp:96-147 and the frame loop of VideoEncoder.cpp:83-91. */
+int ie_encode_frames(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch,
+                     int nframes, int use_rle, int mode, uint8_t* out, size_t out_cap,
+                     uint64_t start_bit, uint64_t* frame_bits, uint64_t* end_bit);
+
+/* Encode nframes INDEPENDENT images in one launch (an image-server batch): image f's records
+ * go to out + f*out_pitch from bit start_bit (each image carries its own header region).
+ * end_bits optional [nframes].  out_pitch must be a multiple of 4 bytes. */
+int ie_encode_images(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch,
+                     int nframes, int use_rle, int mode, uint8_t* out, size_t out_pitch,
+                     uint64_t start_bit, uint64_t* end_bits);
+
+/* Quantised DCT coefficients only (Block::processDCTDivQ, Block.cpp:139-153): coef receives
+ * nframes * (w/n) * (h/n) blocks of n*n int16 in natural (row-major) order, block raster order.
+ * coef may be host or device memory.  Diagnostic / analysis entry point. */
+int ie_quantize_frames(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch,
+                       int nframes, int mode, int16_t* coef);
+
+/* Fallback statistics of the last FAST-mode encode: coefficients re-evaluated in FP64. */
+int ie_last_fallbacks(ie_ctx* ctx, uint64_t* count);
+
+/* ---- Huffman post-pass (config 5; Huffman.cpp:233-344) ----------------------------------
+ * hist[b] = occurrences of byte value b; first_pos[b] = index of its first occurrence
+ * (UINT64_MAX if absent).  The first-occurrence order is the insertion order of the reference's
+ * std::unordered_map (Huffman.cpp:237-243), which the host needs to replay the tree build. */
+int ie_huffman_hist(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint32_t* hist, uint64_t* first_pos);
+
+/* Re-encode n bytes with a code table (code[b] right-aligned in len[b] bits, len <= 32),
+ * appending from start_bit of out (Huffman.cpp:314-319).  end_bit optional. */
+int ie_huffman_pack(ie_ctx* ctx, const uint8_t* bytes, size_t n, const uint32_t* code, const uint8_t* len,
+                    uint8_t* out, size_t out_cap, uint64_t start_bit, uint64_t* end_bit);
+
+/* Copy n bytes shifted right by `shift` bits (0..7) into out starting at bit start_bit (the
+ * "no gain" path of Huffman.cpp:329-341 writes '0' + the input). */
+int ie_bitcopy(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint8_t* out, size_t out_cap, uint64_t start_bit);
+
+/* ---- Inverse path (ImageDecoder.cpp:55-122, Block.cpp:100-107,163-177,442-472) ------------
+ * Decode nframes frames of block records starting at bit start_bit of `in` (len bytes) into
+ * pixels (frame f row r at out + f*frame_pitch + r*stride).  Uses the quant matrix of
+ * ie_set_quant.  end_bit optional. */
+int ie_decode_frames(ie_ctx* ctx, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h,
+                     int nframes, int use_rle, uint8_t* out, size_t stride, size_t frame_pitch,
+                     uint64_t* end_bit);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

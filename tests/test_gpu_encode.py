@@ -1,0 +1,180 @@
+"""GPU parity: the HIP encoder (through the C-ABI) against the reference's golden streams and the
+CPU oracle.  Bit-exact is the only bar (integer/byte output).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from imageencoder_amd import MODE_EXACT, MODE_FAST, synth
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from imageencoder_amd import Codec
+    return Codec(0)
+
+
+def _md5(b: bytes) -> str:
+    return hashlib.md5(b).hexdigest()
+
+
+def _gpu_file(codec, oracle, c, raw: bytes, mode: int) -> bytes:
+    """Whole reference file: the oracle writes the settings header (host side), the GPU
+    appends every block record after it."""
+    from imageencoder_amd import stream_bound
+    n, w, h = c["n"], c["w"], c["h"]
+    q = O.read_matrix(c["matrix"], n)
+    codec.set_quant(q, n)
+    if c["video"]:
+        pitch = w * h * 3 // 2
+        frames = len(raw) // pitch
+        hdr, hb = oracle.header(n, q, c["rle"], w, h, video=True, frames=frames, gop=1, merange=16)
+        y = np.frombuffer(raw, dtype=np.uint8)
+    else:
+        frames, pitch = 1, w * h
+        hdr, hb = oracle.header(n, q, c["rle"], w, h)
+        y = np.frombuffer(raw, dtype=np.uint8)
+    out = np.zeros(stream_bound(w, h, n, frames, hb), dtype=np.uint8)
+    m = min(len(hdr), len(out))
+    out[:m] = hdr[:m]  # header bits, zero from bit hb on
+    fb, end = codec.encode_frames(y, w, h, out, start_bit=hb, frame_pitch=pitch, nframes=frames,
+                                  rle=bool(c["rle"]), mode=mode)
+    assert int(fb.sum()) == end - hb
+    return out[: (end + 7) // 8].tobytes()
+
+
+def _golden(nonhuff_only=True, big=False):
+    cs = []
+    for c in O.manifest():
+        if nonhuff_only and c["huffman"]:
+            continue
+        is_big = c["w"] * c["h"] >= 1920 * 1080
+        if is_big == big:
+            cs.append(c)
+    return cs
+
+
+@pytest.mark.parametrize("mode", [MODE_FAST, MODE_EXACT], ids=["fast", "exact"])
+@pytest.mark.parametrize("n,matrix", [(4, "matrix.txt"), (8, "matrix8_1.txt")])
+@pytest.mark.parametrize("kind", ["ex0", "ex6", "U", "M"])
+def test_quantized_coefficients(codec, oracle, kind, n, matrix, mode):
+    """Block::processDCTDivQ alone: every quantised coefficient vs the oracle."""
+    if kind.startswith("ex"):
+        raw = open(f"{O.GOLDEN}/{kind}.raw", "rb").read()
+        w, h = (8, 8) if kind == "ex0" else (512, 256)
+        y = np.frombuffer(raw, dtype=np.uint8).reshape(h, w)
+    else:
+        y = synth.frame(kind, 320, 240, seed=5)
+    q = O.read_matrix(matrix, n)
+    codec.set_quant(q, n)
+    got = codec.quantize_frames(y, y.shape[1], y.shape[0], mode=mode)
+    exp = oracle.quantize(y, n, q)
+    bad = np.argwhere(got != exp)
+    assert bad.size == 0, (bad[:8].tolist(), got[tuple(bad[0])], exp[tuple(bad[0])])
+
+
+@pytest.mark.parametrize("mode", [MODE_FAST, MODE_EXACT], ids=["fast", "exact"])
+@pytest.mark.parametrize("case", _golden(), ids=lambda c: c["name"])
+def test_golden_small(codec, oracle, case, mode):
+    enc = _gpu_file(codec, oracle, case, O.case_input(case), mode)
+    exp = O.case_expected(case)
+    if exp is not None:
+        assert enc == exp
+    assert len(enc) == case["size"] and _md5(enc) == case["md5"]
+
+
+@pytest.mark.parametrize("case", _golden(big=True), ids=lambda c: c["name"])
+def test_golden_fullsize(codec, oracle, case):
+    enc = _gpu_file(codec, oracle, case, O.case_input(case), MODE_FAST)
+    assert len(enc) == case["size"] and _md5(enc) == case["md5"]
+
+
+@pytest.mark.parametrize("n,matrix", [(4, "matrix.txt"), (8, "matrix8_1.txt"), (4, "matrix4_2.txt"),
+                                      (8, "matrix8_2.txt")])
+@pytest.mark.parametrize("start_bit", [0, 1, 31, 165, 549])
+def test_random_frames_vs_oracle(codec, oracle, n, matrix, start_bit):
+    """Seeded random sizes (ragged widths included), several frames concatenated, arbitrary
+    start bits, RLE on and off -- GPU vs oracle, bit for bit."""
+    rng = np.random.default_rng(1234 + n * 100 + start_bit)
+    q = O.read_matrix(matrix, n)
+    codec.set_quant(q, n)
+    for trial in range(3):
+        w = n * int(rng.integers(1, 90))
+        h = n * int(rng.integers(1, 40))
+        f = int(rng.integers(1, 4))
+        rle = bool(trial % 2 == 0)
+        kind = "U" if trial % 3 else "M"
+        y = synth.frames(kind, w, h, f, seed=int(rng.integers(1 << 30)))
+        from imageencoder_amd import stream_bound
+        out = np.zeros(stream_bound(w, h, n, f, start_bit), dtype=np.uint8)
+        fb, end = codec.encode_frames(y, w, h, out, start_bit=start_bit, nframes=f, rle=rle)
+        exp, eend, efb = oracle.encode_blocks(y, n, q, rle, start_bit)
+        assert end == eend and np.array_equal(fb, efb)
+        nb = (end + 7) // 8
+        assert out[:nb].tobytes() == exp[:nb].tobytes()
+
+
+def test_device_pointers_and_images_batch(codec, oracle):
+    """Device-resident input/output (torch tensors) and the independent-image batch mode."""
+    import torch
+    from imageencoder_amd import stream_bound
+    n, q = 4, O.read_matrix("matrix.txt", 4)
+    codec.set_quant(q, n)
+    w, h, f, sb = 640, 360, 6, 165
+    y = synth.frames("M", w, h, f, seed=77)
+    dy = torch.from_numpy(y).cuda()
+    pitch = (stream_bound(w, h, n, 1, sb) + 255) // 256 * 256
+    dout = torch.zeros(pitch * f, dtype=torch.uint8, device="cuda")
+    ends = codec.encode_images(dy, w, h, dout, out_pitch=pitch, nframes=f, start_bit=sb)
+    host = dout.cpu().numpy()
+    for i in range(f):
+        exp, eend, _ = oracle.encode_blocks(y[i], n, q, True, sb)
+        assert int(ends[i]) == eend
+        nb = (eend + 7) // 8
+        seg = host[i * pitch: i * pitch + nb]
+        assert seg[sb // 8 + 1:].tobytes() == exp[sb // 8 + 1: nb].tobytes()
+    # concatenated stream, device in / device out
+    dcat = torch.zeros(stream_bound(w, h, n, f, sb), dtype=torch.uint8, device="cuda")
+    fb, end = codec.encode_frames(dy, w, h, dcat, start_bit=sb, nframes=f)
+    exp, eend, efb = oracle.encode_blocks(y, n, q, True, sb)
+    assert end == eend and np.array_equal(fb, efb)
+    nb = (end + 7) // 8
+    assert dcat.cpu().numpy()[sb // 8 + 1: nb].tobytes() == exp[sb // 8 + 1: nb].tobytes()
+
+
+@pytest.mark.parametrize("n,matrix", [(4, "matrix.txt"), (8, "matrix8_1.txt")])
+def test_fast_equals_exact_large(codec, n, matrix):
+    """FAST (FP32 + FP64 near-tie re-evaluation) must equal EXACT (all FP64) bit for bit on
+    many blocks: 8 distinct 1080p frames of each generator (>= 1M 4x4 blocks)."""
+    import torch
+    from imageencoder_amd import stream_bound
+    q = O.read_matrix(matrix, n)
+    codec.set_quant(q, n)
+    w, h, f = 1920, 1080, 8
+    for kind in ("U", "M"):
+        y = torch.from_numpy(synth.frames(kind, w, h, f, seed=4242)).cuda()
+        a = torch.zeros(stream_bound(w, h, n, f), dtype=torch.uint8, device="cuda")
+        b = torch.zeros_like(a)
+        fa, ea = codec.encode_frames(y, w, h, a, nframes=f, mode=MODE_FAST)
+        fb, eb = codec.encode_frames(y, w, h, b, nframes=f, mode=MODE_EXACT)
+        assert ea == eb and np.array_equal(fa, fb)
+        assert torch.equal(a[: (ea + 7) // 8], b[: (eb + 7) // 8])
+
+
+def test_random_noise_stress(codec, oracle):
+    """Uniform random bytes from numpy's generator (not the splitmix frames) against the oracle."""
+    from imageencoder_amd import stream_bound
+    rng = np.random.default_rng(99)
+    for n, matrix in ((4, "matrix.txt"), (8, "matrix8_1.txt")):
+        q = O.read_matrix(matrix, n)
+        codec.set_quant(q, n)
+        y = rng.integers(0, 256, size=(4, 512, 768), dtype=np.uint8)
+        out = np.zeros(stream_bound(768, 512, n, 4), dtype=np.uint8)
+        fb, end = codec.encode_frames(y, 768, 512, out, nframes=4)
+        exp, eend, efb = oracle.encode_blocks(y, n, q, True, 0)
+        assert end == eend and np.array_equal(fb, efb)
+        assert out[: (end + 7) // 8].tobytes() == exp[: (end + 7) // 8].tobytes()
