@@ -34,7 +34,8 @@ struct ie_ctx {
     uint64_t* d_frame_start = nullptr;  // [cap_frames]
     uint64_t* d_chain_end = nullptr;    // [cap_frames]
     size_t cap_frames = 0;
-    unsigned* d_err = nullptr;          // [0] look-back timeouts, [1] fallbacks
+    unsigned* d_err = nullptr;          // [0] look-back timeouts, [2..65] fallback counters
+    bool use_ticket = false;            // order tiles with an atomic ticket (after a timeout)
 
     // staging for host-resident inputs / outputs
     uint8_t* d_in = nullptr;
@@ -47,9 +48,30 @@ struct ie_ctx {
     size_t cap_coef = 0;
 
     uint64_t last_fallbacks = 0;
+
+    // Huffman tables / histogram
+    uint32_t* d_code = nullptr;        // [256] codes, then [256/4] packed lengths (one block)
+    uint32_t* h_code = nullptr;        // pinned mirror
+    uint32_t* d_hist = nullptr;        // [256]
+    // decoder scratch
+    uint8_t* d_dec = nullptr;          // staged stream + padding
+    size_t cap_dec = 0;
+    uint64_t* d_walk = nullptr;        // entry, exA, exB, base: 4 x cap_chunks
+    size_t cap_walk = 0;
+    uint32_t* d_count = nullptr;
+    size_t cap_count = 0;
+    uint64_t* d_bb = nullptr;          // block start bits
+    size_t cap_bb = 0;
+    uint64_t* d_misc = nullptr;        // [0] end bit, [1] changed flag
+    uint8_t* d_pix = nullptr;
+    size_t cap_pix = 0;
+    int last_rounds = 0;
+    unsigned long long* d_first = nullptr;  // [256]
 };
 
 namespace {
+
+constexpr int kErrWords = 66;
 
 int fail(ie_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -87,14 +109,57 @@ int ensure(ie_ctx* c, T*& p, size_t& cap, size_t need_elems) {
     return IE_OK;
 }
 
+
+// ---- rigorous error bound of the FP32 fast path -----------------------------------------
+// Trk = an exact real linear form of the block's pixels x (|x| <= 128) plus a bound E on the
+// FP32 rounding error accumulated so far.  TrkOp mirrors every operation of ie_dct.h: the real
+// coefficients follow the FP32 constants exactly; each rounded operation adds u*|result| with
+// |result| <= 128*sum|coef| + E.  Sums/differences of integers below 2^24 round exactly (integ).
+struct Trk {
+    double a[64];
+    double E;
+    bool integ;
+};
+
+struct TrkOp {
+    int nn;
+    static constexpr double u = 1.0 / 16777216.0;  // 2^-24
+    double mag(const Trk& t) const {
+        double m = 0;
+        for (int k = 0; k < nn; k++) m += std::fabs(t.a[k]);
+        return 128.0 * m;
+    }
+    static bool is_int(double c) { return c == std::rint(c); }
+    Trk lin(const Trk& x, double cx, const Trk* y, double cy, double Ein, bool integ) const {
+        Trk r;
+        for (int k = 0; k < nn; k++) r.a[k] = cx * x.a[k] + (y ? cy * y->a[k] : 0.0);
+        for (int k = nn; k < 64; k++) r.a[k] = 0.0;
+        const double m = mag(r);
+        r.integ = integ && m < 16777216.0;
+        r.E = Ein + (r.integ ? 0.0 : u * (m + Ein));
+        return r;
+    }
+    Trk add(const Trk& x, const Trk& y) const { return lin(x, 1, &y, 1, x.E + y.E, x.integ && y.integ); }
+    Trk sub(const Trk& x, const Trk& y) const { return lin(x, 1, &y, -1, x.E + y.E, x.integ && y.integ); }
+    Trk mul(const Trk& x, float c) const {
+        return lin(x, double(c), nullptr, 0, std::fabs(double(c)) * x.E, x.integ && is_int(c));
+    }
+    Trk fma(const Trk& x, float c, const Trk& y) const {
+        return lin(x, double(c), &y, 1, std::fabs(double(c)) * x.E + y.E, x.integ && y.integ && is_int(c));
+    }
+};
+
 inline double Cf(int i) { return i == 0 ? 0.5 : M_SQRT1_2; }  // algo.cpp:294-297
 
-// Build the per-matrix tables.  The cos values are the reference's own expression evaluated
-// with the host libm (algo.cpp:312,318-319); P, S and R are the double products it forms.
-// thr[k] bounds |t32 - T| where t32 is the kernel's FP32 quotient for coefficient k and T the
-// reference's FP64 quotient: a forward error bound of the separable FMA chains of
-// encode_kernel (row pass over j, column pass over i, one scale), for |x| <= 128, doubled.
-void build_tables(int n, const uint16_t* q, ie::EncTables* T) {
+// Build the per-matrix tables.  The cos values are the reference's own expression evaluated with
+// the host libm (algo.cpp:312,318-319); P, S and R are the double products it forms.  For the
+// FP32 path, the tracked run of dct2d gives per coefficient k the real linear map alpha_k the
+// FP32 code implements and its rounding bound E_k; with alpha*_k the reference's map
+// (S*P/q) the FP32 quotient is within
+//     thr_k = 2 * ( E_k + 128 * sum|alpha_k - alpha*_k| + 1e-9 )
+// of the reference's FP64 quotient (1e-9 covers the reference's own FP64 rounding, <= 1e-10).
+// Returns false if alpha deviates from alpha* beyond FP32 constant rounding (a butterfly bug).
+bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
     const int nn = n * n;
     std::memset(T, 0, sizeof(*T));
     const double factor = M_PI_2 / double(n);
@@ -105,6 +170,8 @@ void build_tables(int n, const uint16_t* q, ie::EncTables* T) {
             const int k = u * n + v;
             T->S[k] = Cf(u) * Cf(v);
             T->qd[k] = double(q[k]);
+            int e2 = 0;
+            T->rq[k] = (std::frexp(double(q[k]), &e2) == 0.5) ? 1.0 / double(q[k]) : 0.0;
             for (int i = 0; i < n; i++)
                 for (int j = 0; j < n; j++) {
                     T->P[k * nn + i * n + j] = T->c[u * n + i] * T->c[v * n + j];
@@ -112,54 +179,45 @@ void build_tables(int n, const uint16_t* q, ie::EncTables* T) {
                 }
         }
     for (int k = 0; k < nn; k++) T->cf[k] = float(T->c[k]);
+    for (int k = 0; k <= 8; k++) T->dct.K[k] = float(std::cos(double(k) * M_PI / 16.0));
 
-    const double uf = std::ldexp(1.0, -24), X = 128.0;
-    double My[8], Ey[8];
-    bool exy[8];
-    for (int v = 0; v < n; v++) {
-        double M = 0, E = 0;
-        bool ex = true;
-        for (int j = 0; j < n; j++) {
-            const double cd = T->c[v * n + j], dc = std::fabs(double(T->cf[v * n + j]) - cd);
-            ex = ex && (cd == 1.0);
-            M += std::fabs(cd) * X;
-            E += dc * X;
-            if (!ex) E += uf * (M + E);
-        }
-        My[v] = M;
-        Ey[v] = ex ? 0.0 : E;
-        exy[v] = ex;
+    // tracked run of the kernel's transform
+    std::vector<Trk> b(nn);
+    for (int k = 0; k < nn; k++) {
+        for (int m = 0; m < 64; m++) b[k].a[m] = (m == k) ? 1.0 : 0.0;
+        b[k].E = 0.0;
+        b[k].integ = true;
     }
-    for (int u = 0; u < n; u++)
-        for (int v = 0; v < n; v++) {
-            const int k = u * n + v;
-            double M = 0, E = 0;
-            bool ex = exy[v];
-            for (int i = 0; i < n; i++) {
-                const double cd = T->c[u * n + i], cfv = T->cf[u * n + i];
-                ex = ex && (cd == 1.0);
-                M += std::fabs(cd) * My[v];
-                E += std::fabs(cfv) * Ey[v] + std::fabs(cfv - cd) * My[v];
-                if (!ex) E += uf * (M + E);
-            }
-            const double sq = T->S[k] / T->qd[k];
-            const float g = float(sq);
-            T->g[k] = g;
-            const double dg = std::fabs(double(g) - sq) + 1e-15 * sq;
-            double bound = std::fabs(double(g)) * E + M * dg + uf * std::fabs(double(g)) * (M + E);
-            // the reference's own FP64 rounding (<= NN terms of |P x| <= 128, relative 2^-53 each)
-            bound += 1e-9;
-            // exact when every step is: integer sums (rows/cols of ones), a power-of-two scale and
-            // divisor, so both the reference and the FP32 path compute the quotient exactly
-            int e2 = 0;
-            const double m2 = std::frexp(sq, &e2);
-            const bool pow2 = (m2 == 0.5);
-            if (ex && pow2 && double(g) == sq) {
-                T->thr[k] = -1.0f;
-            } else {
-                T->thr[k] = float(2.0 * bound);
-            }
+    TrkOp op{nn};
+    if (n == 4) ie::dct2d<4>(b.data(), T->dct, op);
+    else ie::dct2d<8>(b.data(), T->dct, op);
+    bool ok = true;
+    for (int k = 0; k < nn; k++) {
+        const double sq = T->S[k] / T->qd[k];
+        const float g = float(sq);
+        T->g[k] = g;
+        const Trk t = op.mul(b[k], g);
+        double dev = 0.0, amax = 0.0;
+        for (int m = 0; m < nn; m++) {
+            const double ref = sq * T->P[k * nn + m];
+            dev += std::fabs(t.a[m] - ref);
+            amax = std::max(amax, std::fabs(ref));
         }
+        if (dev > 1e-5 * (amax + 1e-30) * nn) ok = false;  // FP32 constants differ by ~1e-7 relative
+        const double bound = t.E + 128.0 * dev + 1e-9;
+        // coefficient 0: an integer sum scaled by a power of two is exact in FP32, and the
+        // reference computes it exactly too (c[0][*] = 1, C(0)^2 = 1/4, q a power of two)
+        int e2 = 0;
+        const bool pow2 = std::frexp(sq, &e2) == 0.5;
+        if (k == 0 && b[0].integ && b[0].E == 0.0 && pow2 && double(g) == sq) {
+            T->thr[k] = -1.0f;
+            T->lim[k] = 1.0f;  // never flagged
+        } else {
+            T->thr[k] = float(2.0 * bound);
+            T->lim[k] = float(0.5 - 2.0 * bound);
+        }
+    }
+    return ok;
 }
 
 int prepare_state(ie_ctx* c, int ntiles, int nframes) {
@@ -190,7 +248,19 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
         HIPCHK(c, hipMalloc(&c->d_chain_end, cap * sizeof(uint64_t)));
         c->cap_frames = cap;
     }
-    HIPCHK(c, hipMemsetAsync(c->d_err, 0, 2 * sizeof(unsigned), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_err, 0, kErrWords * sizeof(unsigned), c->stream));
+    return IE_OK;
+}
+
+// [0] look-back timeouts; sum of [2..65] = FP64 re-evaluations.  Synchronises the stream.
+int read_errors(ie_ctx* c, unsigned* timeouts, uint64_t* fallbacks) {
+    unsigned e[kErrWords];
+    HIPCHK(c, hipMemcpyAsync(e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint64_t f = 0;
+    for (int i = 2; i < kErrWords; i++) f += e[i];
+    if (timeouts) *timeouts = e[0];
+    if (fallbacks) *fallbacks = f;
     return IE_OK;
 }
 
@@ -295,9 +365,8 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.out = dout;
     a.out_pitch_words = segmented ? out_pitch / 4 : 0;
     a.start_bit = start_bit;
-    a.st_agg = c->d_state;
-    a.st_inc = c->d_state + c->cap_tiles;
-    a.ticket = c->d_ticket;
+    a.st = c->d_state;
+    a.ticket = c->use_ticket ? c->d_ticket : nullptr;
     a.ticket_base = c->ticket_base;
     a.tag = c->tag;
     a.frame_start = c->d_frame_start;
@@ -307,18 +376,21 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.coef = coef;
     ie::launch_encode(a, c->n, mode == IE_MODE_EXACT, c->stream);
     HIPCHK(c, hipGetLastError());
-    c->ticket_base += uint64_t(g.ntiles);
+    if (c->use_ticket) c->ticket_base += uint64_t(g.ntiles);
 
     const bool want = frame_bits || end_bits || !out_dev;
     if (!want) return IE_OK;
     std::vector<uint64_t> fs(nframes), ce(nchains);
-    unsigned errs[2];
     HIPCHK(c, hipMemcpyAsync(fs.data(), c->d_frame_start, nframes * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(ce.data(), c->d_chain_end, nchains * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(errs, c->d_err, sizeof(errs), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->last_fallbacks = errs[1];
-    if (errs[0]) return fail(c, IE_EDEVICE, "tile look-back timed out");
+    unsigned timeouts = 0;
+    if ((r = read_errors(c, &timeouts, &c->last_fallbacks))) return r;
+    if (timeouts) {
+        if (c->use_ticket) return fail(c, IE_EDEVICE, "tile look-back timed out");
+        c->use_ticket = true;  // dispatch order did not hold: order the tiles explicitly and redo
+        return encode(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_cap, out_pitch, start_bit,
+                      segmented, frame_bits, end_bits, coef);
+    }
     if (!out_dev) {
         for (int ch = 0; ch < nchains; ch++) {
             const size_t b0 = size_t(ch) * out_pitch + size_t(start_bit / 8);
@@ -337,6 +409,83 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     if (end_bits) {
         for (int ch = 0; ch < nchains; ch++) end_bits[ch] = ce[ch];
     }
+    return IE_OK;
+}
+
+// Variable-length re-encode of n bytes (Huffman.cpp:314-319) into one stream from start_bit.
+int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const uint8_t* len, uint8_t* out,
+         size_t out_cap, uint64_t start_bit, uint64_t* end_bit) {
+    HIPCHK(c, hipSetDevice(c->device));
+    int r;
+    unsigned maxlen = 0;
+    for (int b = 0; b < 256; b++) {
+        if (len[b] > 32) return fail(c, IE_EINVAL, "code length above 32 bits");
+        maxlen = std::max<unsigned>(maxlen, len[b]);
+    }
+    const uint64_t end_bound = start_bit + uint64_t(maxlen) * n;
+    const size_t need_bytes = size_t((end_bound + 31) / 32) * 4;
+    if (out_cap < need_bytes) return fail(c, IE_ECAP, "output capacity below start_bit + max_len * n bits");
+    // code table through pinned memory (the caller's arrays may be gone when the copy runs)
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::memcpy(c->h_code, code, 256 * sizeof(uint32_t));
+    std::memcpy(reinterpret_cast<uint8_t*>(c->h_code + 256), len, 256);
+    HIPCHK(c, hipMemcpyAsync(c->d_code, c->h_code, 2 * 256 * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    const uint8_t* din = bytes;
+    if (n && !is_device_ptr(bytes)) {
+        if ((r = ensure(c, c->d_in, c->cap_in, n))) return r;
+        HIPCHK(c, hipMemcpyAsync(c->d_in, bytes, n, hipMemcpyHostToDevice, c->stream));
+        din = c->d_in;
+    }
+    const bool out_dev = is_device_ptr(out);
+    const uint64_t w0 = start_bit / 32;
+    uint32_t* dout;
+    if (out_dev) {
+        if (reinterpret_cast<uintptr_t>(out) % 4) return fail(c, IE_EINVAL, "device output must be 4-byte aligned");
+        dout = reinterpret_cast<uint32_t*>(out);
+    } else {
+        if ((r = ensure(c, c->d_out, c->cap_out, need_bytes - size_t(w0) * 4))) return r;
+        uint8_t word[4] = {0, 0, 0, 0};
+        for (int e = 0; e < 4 && size_t(w0) * 4 + e < out_cap; e++) word[e] = out[size_t(w0) * 4 + e];
+        HIPCHK(c, hipMemcpyAsync(c->d_out, word, 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        dout = reinterpret_cast<uint32_t*>(c->d_out) - w0;
+    }
+    uint64_t end = start_bit;
+    if (n) {
+        const int ntiles = int((n + ie::kTPB * ie::kPackBytesPerThread - 1) / (ie::kTPB * ie::kPackBytesPerThread));
+        if ((r = prepare_state(c, ntiles, 1))) return r;
+        ie::PackArgs a{};
+        a.in = din;
+        a.n = n;
+        a.code = c->d_code;
+        a.len = reinterpret_cast<const uint8_t*>(c->d_code + 256);
+        a.ntiles = ntiles;
+        a.out = dout;
+        a.start_bit = start_bit;
+        a.st = c->d_state;
+        a.ticket = c->use_ticket ? c->d_ticket : nullptr;
+        a.ticket_base = c->ticket_base;
+        a.tag = c->tag;
+        a.chain_end = c->d_chain_end;
+        a.err = c->d_err;
+        ie::launch_pack(a, c->stream);
+        HIPCHK(c, hipGetLastError());
+        if (c->use_ticket) c->ticket_base += uint64_t(ntiles);
+        if (!end_bit && out_dev) return IE_OK;
+        HIPCHK(c, hipMemcpyAsync(&end, c->d_chain_end, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        unsigned timeouts = 0;
+        if ((r = read_errors(c, &timeouts, nullptr))) return r;
+        if (timeouts) {
+            if (c->use_ticket) return fail(c, IE_EDEVICE, "tile look-back timed out");
+            c->use_ticket = true;
+            return pack(c, bytes, n, code, len, out, out_cap, start_bit, end_bit);
+        }
+    }
+    if (!out_dev && end > start_bit) {
+        const size_t b0 = size_t(start_bit / 8), b1 = size_t((end + 7) / 8);
+        HIPCHK(c, hipMemcpy(out + b0, c->d_out + (b0 - size_t(w0) * 4), b1 - b0, hipMemcpyDeviceToHost));
+    }
+    if (end_bit) *end_bit = end;
     return IE_OK;
 }
 
@@ -360,7 +509,12 @@ int ie_create(int device, ie_ctx** out) {
     if (r == IE_OK) chk(hipHostMalloc(&c->h_tab, sizeof(ie::EncTables)), "hipHostMalloc(tables)");
     if (r == IE_OK) chk(hipMalloc(&c->d_ticket, sizeof(unsigned long long)), "hipMalloc(ticket)");
     if (r == IE_OK) chk(hipMemset(c->d_ticket, 0, sizeof(unsigned long long)), "hipMemset(ticket)");
-    if (r == IE_OK) chk(hipMalloc(&c->d_err, 4 * sizeof(unsigned)), "hipMalloc(err)");
+    if (r == IE_OK) chk(hipMalloc(&c->d_err, kErrWords * sizeof(unsigned)), "hipMalloc(err)");
+    if (r == IE_OK) chk(hipMalloc(&c->d_code, 2 * 256 * sizeof(uint32_t)), "hipMalloc(code)");
+    if (r == IE_OK) chk(hipHostMalloc(&c->h_code, 2 * 256 * sizeof(uint32_t)), "hipHostMalloc(code)");
+    if (r == IE_OK) chk(hipMalloc(&c->d_hist, 256 * sizeof(uint32_t)), "hipMalloc(hist)");
+    if (r == IE_OK) chk(hipMalloc(&c->d_misc, 4 * sizeof(uint64_t)), "hipMalloc(misc)");
+    if (r == IE_OK) chk(hipMalloc(&c->d_first, 256 * sizeof(unsigned long long)), "hipMalloc(first)");
     if (r != IE_OK) {
         std::fprintf(stderr, "ie_create: %s\n", c->err.c_str());
         ie_destroy(c);
@@ -385,6 +539,16 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_in);
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_scratch);
+    (void)hipFree(c->d_code);
+    (void)hipHostFree(c->h_code);
+    (void)hipFree(c->d_hist);
+    (void)hipFree(c->d_first);
+    (void)hipFree(c->d_dec);
+    (void)hipFree(c->d_walk);
+    (void)hipFree(c->d_count);
+    (void)hipFree(c->d_bb);
+    (void)hipFree(c->d_misc);
+    (void)hipFree(c->d_pix);
     (void)hipFree(c->d_coef);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -412,7 +576,7 @@ int ie_set_quant(ie_ctx* c, const uint16_t* q, int n) {
         if (q[k] == 0) return fail(c, IE_EINVAL, "quantisation matrix entries must be > 0");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));  // tables may be in use by a running launch
-    build_tables(n, q, c->h_tab);
+    if (!build_tables(n, q, c->h_tab)) return fail(c, IE_EINVAL, "FP32 transform does not match the reference map");
     HIPCHK(c, hipMemcpy(c->d_tab, c->h_tab, sizeof(ie::EncTables), hipMemcpyHostToDevice));
     c->n = n;
     std::memcpy(c->q, q, sizeof(uint16_t) * n * n);
@@ -463,12 +627,110 @@ int ie_quantize_frames(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride,
 
 int ie_last_fallbacks(ie_ctx* c, uint64_t* count) {
     if (!c || !count) return IE_EINVAL;
-    unsigned errs[2];
-    HIPCHK(c, hipMemcpyAsync(errs, c->d_err, sizeof(errs), hipMemcpyDeviceToHost, c->stream));
+    unsigned timeouts = 0;
+    int r = read_errors(c, &timeouts, &c->last_fallbacks);
+    if (r) return r;
+    *count = c->last_fallbacks;
+    if (timeouts) return fail(c, IE_EDEVICE, "tile look-back timed out");
+    return IE_OK;
+}
+
+int ie_huffman_hist(ie_ctx* c, const uint8_t* bytes, size_t n, uint32_t* hist, uint64_t* first_pos) {
+    if (!c || (!bytes && n) || !hist || !first_pos) return IE_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    int r;
+    const uint8_t* din = bytes;
+    if (n && !is_device_ptr(bytes)) {
+        if ((r = ensure(c, c->d_in, c->cap_in, n))) return r;
+        HIPCHK(c, hipMemcpyAsync(c->d_in, bytes, n, hipMemcpyHostToDevice, c->stream));
+        din = c->d_in;
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 256 * sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_first, 0xFF, 256 * sizeof(unsigned long long), c->stream));
+    if (n) ie::launch_hist(din, n, c->d_hist, c->d_first, c->stream);
+    HIPCHK(c, hipGetLastError());
+    const hipMemcpyKind k1 = is_device_ptr(hist) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    const hipMemcpyKind k2 = is_device_ptr(first_pos) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    HIPCHK(c, hipMemcpyAsync(hist, c->d_hist, 256 * sizeof(uint32_t), k1, c->stream));
+    HIPCHK(c, hipMemcpyAsync(first_pos, c->d_first, 256 * sizeof(uint64_t), k2, c->stream));
+    if (k1 == hipMemcpyDeviceToHost || k2 == hipMemcpyDeviceToHost) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return IE_OK;
+}
+
+int ie_huffman_pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const uint8_t* len,
+                    uint8_t* out, size_t out_cap, uint64_t start_bit, uint64_t* end_bit) {
+    if (!c || (!bytes && n) || !code || !len || !out) return IE_EINVAL;
+    return pack(c, bytes, n, code, len, out, out_cap, start_bit, end_bit);
+}
+
+int ie_bitcopy(ie_ctx* c, const uint8_t* bytes, size_t n, uint8_t* out, size_t out_cap, uint64_t start_bit) {
+    if (!c || (!bytes && n) || !out) return IE_EINVAL;
+    uint32_t code[256];
+    uint8_t len[256];
+    for (int b = 0; b < 256; b++) {
+        code[b] = uint32_t(b);
+        len[b] = 8;
+    }
+    uint64_t end = 0;
+    return pack(c, bytes, n, code, len, out, out_cap, start_bit, &end);
+}
+
+int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,
+                     int use_rle, uint8_t* out, size_t stride, size_t frame_pitch, uint64_t* end_bit) {
+    if (!c || !in || !out) return IE_EINVAL;
+    int r = check_dims(c, w, h, nframes);
+    if (r) return r;
+    if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
+    if (nframes > 1 && frame_pitch < stride * size_t(h - 1) + size_t(w))
+        return fail(c, IE_EINVAL, "frame_pitch smaller than a frame");
+    if (start_bit > uint64_t(len) * 8) return fail(c, IE_EINVAL, "start_bit beyond the stream");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int n = c->n;
+    // stream: staged (device copy or H2D) with two zero words of padding for the bit reader
+    const size_t padded = (len + 3) / 4 * 4 + 16;
+    if ((r = ensure(c, c->d_dec, c->cap_dec, padded))) return r;
+    HIPCHK(c, hipMemsetAsync(c->d_dec + (len / 4) * 4, 0, padded - (len / 4) * 4, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_dec, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                             c->stream));
+    const uint64_t nbits = uint64_t(len) * 8;
+    const uint64_t chunk_bits = 4096;
+    const size_t nchunks = size_t((nbits - start_bit) / chunk_bits + 1);
+    if ((r = ensure(c, c->d_walk, c->cap_walk, 4 * nchunks))) return r;
+    if ((r = ensure(c, c->d_count, c->cap_count, nchunks))) return r;
+    const uint64_t nblocks = uint64_t(nframes) * (w / n) * (h / n);
+    if ((r = ensure(c, c->d_bb, c->cap_bb, size_t(nblocks)))) return r;
+    const size_t pix_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
+    const bool out_dev = is_device_ptr(out);
+    uint8_t* dpix = out;
+    if (!out_dev) {
+        if ((r = ensure(c, c->d_pix, c->cap_pix, pix_bytes))) return r;
+        dpix = c->d_pix;
+    }
+    ie::DecArgs da{};
+    da.nframes = nframes;
+    da.bx = w / n;
+    da.by = h / n;
+    da.rle = use_rle ? 1 : 0;
+    da.out = dpix;
+    da.stride = stride;
+    da.frame_pitch = frame_pitch;
+    da.tab = c->d_tab;
+    uint64_t* wk = c->d_walk;
+    const size_t cap = c->cap_walk / 4;
+    HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 4 * sizeof(uint64_t), c->stream));
+    const int rounds = ie::decode_frames_device(reinterpret_cast<const uint32_t*>(c->d_dec), nbits, start_bit, da, n,
+                                                chunk_bits, wk, wk + cap, wk + 2 * cap, c->d_count, wk + 3 * cap,
+                                                c->d_bb, reinterpret_cast<unsigned*>(c->d_misc + 1), c->d_misc,
+                                                c->stream, int(nchunks) + 2);
+    if (rounds < 0) return fail(c, IE_EHIP, "decode index walk failed");
+    HIPCHK(c, hipGetLastError());
+    c->last_rounds = rounds;
+    uint64_t end = 0;
+    HIPCHK(c, hipMemcpyAsync(&end, c->d_misc, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->last_fallbacks = errs[1];
-    *count = errs[1];
-    if (errs[0]) return fail(c, IE_EDEVICE, "tile look-back timed out");
+    if (end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
+    if (!out_dev) HIPCHK(c, hipMemcpy(out, dpix, pix_bytes, hipMemcpyDeviceToHost));
+    if (end_bit) *end_bit = end;
     return IE_OK;
 }
 

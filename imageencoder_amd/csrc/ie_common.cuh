@@ -107,73 +107,121 @@ __device__ __forceinline__ void st_state(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Decoupled look-back, executed by ONE full wave.  Tile t of a chain starting at tile c0 reads
-// its predecessors' 8-byte {tag, value} granules (each written by a single agent-scope store,
-// so no fences are needed: the payload travels inside the atomic word).  Returns the exclusive
-// prefix (chain-relative bits); *pred_tail receives the last 32 bits of the chain before t.
-__device__ uint64_t lookback(const uint64_t* st_agg, const uint64_t* st_inc, int t, int c0, uint32_t tag,
-                            uint32_t* pred_tail, unsigned* err) {
-    const int l = lane_id();
-    // the immediate predecessor's tail bits (published together with its aggregate)
-    uint32_t tail = 0;
-    {
-        unsigned spins = 0;
-        uint64_t g = 0;
-        for (;;) {
-            g = (l == 0) ? ld_state(&st_agg[t - 1]) : 0ull;
-            g = __shfl(g, 0, 64);
-            if (uint32_t(g >> 56) == tag) break;
+// Decoupled look-back executed by the WHOLE workgroup (all kTPB threads must call it).
+// Tile t sits at position chain_pos of its chain; its d-th predecessor (d = 0, 1, ...) is tile
+// t - step*(d+1).  Every tile publishes two 8-byte granules st[2t] = {tag:8, aggregate:24,
+// tail32:32} and st[2t+1] = {tag:8, inclusive:56}, each with ONE agent-scope store, so the
+// payload travels inside the atomic word and no fence is needed.  One round trip reads 4*kTPB
+// predecessor states; the exclusive prefix is the sum of aggregates up to the nearest
+// inclusive value.  Returns the exclusive prefix (chain-relative bits); *pred_tail receives the
+// last 32 bits of the chain before t (the immediate predecessor's tail granule).
+// sh: >= 8 words of LDS scratch.
+__device__ uint64_t lookback_wg(uint64_t* st, int t, int chain_pos, int step, uint32_t tag, uint32_t* pred_tail,
+                                unsigned* err, uint32_t* sh) {
+    constexpr int Q = 4;                  // predecessors per thread per round
+    constexpr int WIN = kTPB * Q;
+    constexpr int NONE = 0x7FFFFFFF;
+    const int tid = threadIdx.x, wid = tid >> 6;
+    int* s_min = reinterpret_cast<int*>(sh);      // [0] nearest inclusive distance
+    int* s_x = reinterpret_cast<int*>(sh + 1);    // [1] a not-ready state before it
+    uint64_t* s_sum = reinterpret_cast<uint64_t*>(sh + 2);  // [2..9] per-wave sums
+    uint64_t excl = 0;
+    int d0 = 0;
+    unsigned spins = 0;
+    if (tid == 0) {
+        *s_min = NONE;
+        *s_x = 0;
+    }
+    __syncthreads();
+    for (;;) {
+        int status[Q];
+        uint64_t agg[Q], inc[Q];
+        int myP = NONE;
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const int d = d0 + tid * Q + q;
+            agg[q] = inc[q] = 0;
+            if (chain_pos - 1 - d < 0) {
+                status[q] = 2;  // before the chain start: a virtual inclusive prefix of 0
+            } else {
+                const int idx = t - step * (d + 1);
+                const uint64_t gi = ld_state(&st[2 * idx + 1]);
+                if (uint32_t(gi >> 56) == tag) {
+                    status[q] = 2;
+                    inc[q] = gi & kMask56;
+                } else {
+                    const uint64_t ga = ld_state(&st[2 * idx]);
+                    if (uint32_t(ga >> 56) == tag) {
+                        status[q] = 1;
+                        agg[q] = (ga >> 32) & 0xFFFFFFull;
+                    } else {
+                        status[q] = 0;
+                    }
+                }
+            }
+            if (status[q] == 2 && myP == NONE) myP = d;
+        }
+        if (myP != NONE) atomicMin(s_min, myP);
+        __syncthreads();
+        const int dP = *s_min;
+        uint64_t contrib = 0;
+        bool x = false;
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const int d = d0 + tid * Q + q;
+            if (d < dP) {
+                x |= (status[q] == 0);
+                contrib += agg[q];
+            } else if (d == dP) {
+                contrib += inc[q];
+            }
+        }
+        if (x) atomicOr(s_x, 1);
+        contrib = wave_sum64(contrib);
+        if ((tid & 63) == 0) s_sum[wid] = contrib;
+        __syncthreads();
+        const bool retry = *s_x != 0;
+        uint64_t tot = 0;
+#pragma unroll
+        for (int w = 0; w < kTPB / 64; w++) tot += s_sum[w];
+        __syncthreads();
+        if (tid == 0) {
+            *s_min = NONE;
+            *s_x = 0;
+        }
+        if (retry) {
             if (++spins > kSpinLimit) {
-                if (l == 0) atomicAdd(&err[0], 1u);
+                if (tid == 0) atomicAdd(&err[0], 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            __syncthreads();
+            continue;
+        }
+        excl += tot;
+        __syncthreads();
+        if (dP != NONE) break;
+        d0 += WIN;
+    }
+    // the immediate predecessor's tail (published with or before its inclusive value)
+    uint32_t tail = 0;
+    if (tid == 0) {
+        const int idx = t - step;
+        unsigned sp = 0;
+        for (;;) {
+            const uint64_t ga = ld_state(&st[2 * idx]);
+            if (uint32_t(ga >> 56) == tag) {
+                tail = uint32_t(ga);
+                break;
+            }
+            if (++sp > kSpinLimit) {
+                atomicAdd(&err[0], 1u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        tail = uint32_t(g);
     }
-    *pred_tail = tail;
-
-    uint64_t excl = 0;
-    int j = t - 1;
-    unsigned spins = 0;
-    for (;;) {
-        const int idx = j - l;
-        int status;     // 2 = inclusive, 1 = aggregate, 0 = not ready
-        uint64_t val = 0;
-        if (idx < c0) {
-            status = 2;  // before the chain start: a virtual inclusive prefix of 0
-        } else {
-            const uint64_t pi = ld_state(&st_inc[idx]);
-            if (uint32_t(pi >> 56) == tag) {
-                status = 2;
-                val = pi & kMask56;
-            } else {
-                const uint64_t pa = ld_state(&st_agg[idx]);
-                if (uint32_t(pa >> 56) == tag) {
-                    status = 1;
-                    val = (pa >> 32) & 0xFFFFFFull;
-                } else {
-                    status = 0;
-                }
-            }
-        }
-        const uint64_t pmask = __ballot(status == 2);
-        const uint64_t xmask = __ballot(status == 0);
-        const int firstP = pmask ? __ffsll((unsigned long long)pmask) - 1 : 64;
-        const uint64_t before = (firstP >= 64) ? ~0ull : ((1ull << firstP) - 1);
-        if (xmask & before) {
-            if (++spins > kSpinLimit) {
-                if (l == 0) atomicAdd(&err[0], 1u);
-                return excl;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        const uint64_t contrib = (l < firstP || l == firstP) ? val : 0ull;
-        excl += wave_sum64(l <= firstP ? contrib : 0ull);
-        if (firstP < 64) break;
-        j -= 64;
-    }
+    *pred_tail = tail;  // meaningful in thread 0 (the only reader)
     return excl;
 }
 

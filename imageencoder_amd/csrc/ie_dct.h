@@ -1,0 +1,93 @@
+// imageencoder_amd/csrc/ie_dct.h -- the FP32 fast-path forward DCT, written ONCE over a generic
+// arithmetic type T so that the very same operation sequence runs
+//   - on the device with T = float (encode_kernel), and
+//   - on the host with T = ie::Trk, which tracks every value as an exact linear form of the 64
+//     input pixels plus a rigorous bound on the accumulated FP32 rounding error.
+// The host run yields, per coefficient, the real linear map the FP32 code implements (checked
+// against the reference's c[u][i]*c[v][j]*C(u)C(v)/q) and a worst-case error bound; the kernel
+// re-evaluates in FP64 every coefficient whose quotient falls within that bound of a rounding
+// tie, so the FAST path returns the reference's integers exactly.
+//
+// Reference DCT (algo.cpp:309-331): D[u][v] = C(u)C(v) sum_ij c[u][i] c[v][j] x[i][j] with
+// c[u][i] = cos((2i+1) u pi / 2N).  It is separable, so rows then columns of an N-point DCT-II
+// (unscaled) compute it; the N-point DCTs use the even/odd butterfly of the cos symmetries
+// c[u][N-1-i] = (-1)^u c[u][i].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ie {
+
+// FP32 constants of the butterflies: k-th entry = cos(k pi / 16) rounded to float, k = 0..8
+// (4-point DCT uses cos(pi/8)=K[2], cos(pi/4)=K[4], cos(3pi/8)=K[6]).
+struct DctConsts {
+    float K[9];
+};
+
+template <class T, class Op>
+__host__ __device__ inline void dct4(const T* x, T* y, const DctConsts& k, const Op& op) {
+    // y0 = (x0+x3)+(x1+x2);  y2 = c(pi/4)*((x0+x3)-(x1+x2))
+    // y1 = c(pi/8)*(x0-x3) + c(3pi/8)*(x1-x2);  y3 = c(3pi/8)*(x0-x3) - c(pi/8)*(x1-x2)
+    const T s0 = op.add(x[0], x[3]), s1 = op.add(x[1], x[2]);
+    const T d0 = op.sub(x[0], x[3]), d1 = op.sub(x[1], x[2]);
+    y[0] = op.add(s0, s1);
+    y[2] = op.mul(op.sub(s0, s1), k.K[4]);
+    y[1] = op.fma(d1, k.K[6], op.mul(d0, k.K[2]));
+    y[3] = op.fma(d1, -k.K[2], op.mul(d0, k.K[6]));
+}
+
+template <class T, class Op>
+__host__ __device__ inline void dct8(const T* x, T* y, const DctConsts& k, const Op& op) {
+    // even half: 4-point DCT (pi/8 constants) of s_i = x_i + x_{7-i}
+    T s[4], d[4], e[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        s[i] = op.add(x[i], x[7 - i]);
+        d[i] = op.sub(x[i], x[7 - i]);
+    }
+    dct4(s, e, k, op);
+    y[0] = e[0];
+    y[2] = e[1];
+    y[4] = e[2];
+    y[6] = e[3];
+    // odd half: y[2m+1] = sum_i d_i cos((2i+1)(2m+1) pi / 16), entries +-cos(k pi/16), k odd
+    // m=0: c1 c3 c5 c7;  m=1: c3 -c7 -c1 -c5;  m=2: c5 -c1 c7 c3;  m=3: c7 -c5 c3 -c1
+    y[1] = op.fma(d[3], k.K[7], op.fma(d[2], k.K[5], op.fma(d[1], k.K[3], op.mul(d[0], k.K[1]))));
+    y[3] = op.fma(d[3], -k.K[5], op.fma(d[2], -k.K[1], op.fma(d[1], -k.K[7], op.mul(d[0], k.K[3]))));
+    y[5] = op.fma(d[3], k.K[3], op.fma(d[2], k.K[7], op.fma(d[1], -k.K[1], op.mul(d[0], k.K[5]))));
+    y[7] = op.fma(d[3], -k.K[1], op.fma(d[2], k.K[3], op.fma(d[1], -k.K[5], op.mul(d[0], k.K[7]))));
+}
+
+// 2-D transform of an N x N block in place: rows (over j) then columns (over i).
+// x[i*N+j] in, D[u*N+v] out (unscaled: the C(u)C(v)/q factor is applied by the caller).
+template <int N, class T, class Op>
+__host__ __device__ inline void dct2d(T* b, const DctConsts& k, const Op& op) {
+    T t[N], o[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+#pragma unroll
+        for (int j = 0; j < N; j++) t[j] = b[i * N + j];
+        if constexpr (N == 4) dct4(t, o, k, op);
+        else dct8(t, o, k, op);
+#pragma unroll
+        for (int v = 0; v < N; v++) b[i * N + v] = o[v];
+    }
+#pragma unroll
+    for (int v = 0; v < N; v++) {
+#pragma unroll
+        for (int i = 0; i < N; i++) t[i] = b[i * N + v];
+        if constexpr (N == 4) dct4(t, o, k, op);
+        else dct8(t, o, k, op);
+#pragma unroll
+        for (int u = 0; u < N; u++) b[u * N + v] = o[u];
+    }
+}
+
+struct FloatOp {
+    __device__ __forceinline__ float add(float a, float b) const { return a + b; }
+    __device__ __forceinline__ float sub(float a, float b) const { return a - b; }
+    __device__ __forceinline__ float mul(float a, float c) const { return a * c; }
+    __device__ __forceinline__ float fma(float a, float c, float b) const { return __builtin_fmaf(a, c, b); }
+};
+
+}  // namespace ie

@@ -1,0 +1,255 @@
+// imageencoder_amd/csrc/ie_decode.hip -- the inverse path on gfx950 (ImageDecoder.cpp:55-122).
+//
+// The reference parses block records serially (Block::loadFromStream, Block.cpp:442-472) because
+// a record's length is only known once its header is read.  Here the parse is made parallel:
+//   walk_kernel   the stream is cut into fixed chunks of bits; one lane walks each chunk from an
+//                 entry position, record by record (length = 4 + bl*(rle + Lw) or 4 + bl*N*N),
+//                 and reports where it leaves the chunk.  The first walk starts every chunk at its
+//                 first bit (speculative); a record header that cannot occur in a real stream
+//                 (bl = 0, Lw > N*N) makes the walk slide one bit, so wrong walks quickly fall onto
+//                 the true record boundaries.  Fix-up rounds re-walk every chunk whose entry differs
+//                 from its predecessor's exit until nothing changes; then chunk 0's exact entry
+//                 (start_bit) makes every chunk exact by induction.
+//   index_kernel  the final walks write the start bit of every record (block index = exclusive scan
+//                 of per-chunk record counts).
+//   decode_kernel one lane per block: read bl / Lw / values, sign-extend (utils.hpp:265-269), place
+//                 them in zig-zag order, dequantise (Block.cpp:163-169), inverse DCT in the
+//                 reference's FP64 order (algo.cpp:343-363), +128, clamp and truncate to uint8
+//                 (Block.cpp:100-107).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ie_common.cuh"
+#include "ie_device.h"
+
+namespace ie {
+
+namespace {
+constexpr int kZZ4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+constexpr int kZZ8[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                          12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                          35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                          58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+}  // namespace
+
+struct WalkArgs {
+    const uint32_t* words;  // stream as stored (big-endian bytes), zero-padded by >= 2 words
+    uint64_t nbits;         // stream length in bits
+    uint64_t start_bit;
+    uint64_t chunk_bits;
+    int nchunks;
+    int nn;                 // N*N
+    int rle;
+    uint64_t* entry;        // [nchunks]
+    const uint64_t* exit_in;
+    uint64_t* exit_out;
+    uint32_t* count;
+    unsigned* changed;
+    int first;              // speculative first pass
+};
+
+// bits [p, p+l) of the stream, l <= 32
+__device__ __forceinline__ uint32_t getbits(const uint32_t* W, uint64_t p, int l) {
+    if (l == 0) return 0;
+    const uint64_t w = p >> 5;
+    const uint64_t v = (uint64_t(bswap32(W[w])) << 32) | bswap32(W[w + 1]);
+    return uint32_t((v << (p & 31)) >> (64 - l));
+}
+
+__device__ __forceinline__ void walk(const WalkArgs& a, uint64_t pos, uint64_t end, uint64_t* exit_pos,
+                                     uint32_t* cnt, uint64_t* out_idx_base, uint64_t* block_bit, uint64_t nblocks) {
+    uint32_t c = 0;
+    while (pos < end && pos < a.nbits) {
+        const uint32_t head = getbits(a.words, pos, 20);
+        const int bl = int(head >> 16);
+        int lw;
+        bool ok;
+        if (a.rle) {
+            lw = bl ? int((head << 16 >> 16) >> (16 - bl)) : 0;
+            ok = bl >= 1 && lw <= a.nn;
+        } else {
+            lw = a.nn;
+            ok = bl >= 1;
+        }
+        if (!ok) {  // cannot be a record start: slide (never happens on the true path)
+            pos += 1;
+            continue;
+        }
+        if (block_bit) {
+            const uint64_t idx = *out_idx_base + c;
+            if (idx < nblocks) block_bit[idx] = pos;
+        }
+        c++;
+        pos += 4 + uint64_t(bl) * uint64_t(lw + a.rle);
+    }
+    *exit_pos = pos;
+    *cnt = c;
+}
+
+__global__ void walk_kernel(WalkArgs a) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.nchunks) return;
+    const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
+    const uint64_t cend = cstart + a.chunk_bits;
+    uint64_t e;
+    if (a.first) {
+        e = cstart;
+    } else {
+        if (k == 0) {
+            a.exit_out[0] = a.exit_in[0];
+            return;
+        }
+        e = a.exit_in[k - 1];
+        if (e == a.entry[k]) {
+            a.exit_out[k] = a.exit_in[k];
+            return;
+        }
+        atomicOr(a.changed, 1u);
+    }
+    a.entry[k] = e;
+    uint64_t x;
+    uint32_t c;
+    uint64_t dummy = 0;
+    walk(a, e, cend, &x, &c, &dummy, nullptr, 0);
+    a.exit_out[k] = x;
+    a.count[k] = c;
+}
+
+__global__ void index_kernel(WalkArgs a, const uint64_t* base, uint64_t* block_bit, uint64_t nblocks) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.nchunks) return;
+    const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
+    uint64_t x, b = base[k];
+    uint32_t c;
+    walk(a, a.entry[k], cstart + a.chunk_bits, &x, &c, &b, block_bit, nblocks);
+}
+
+// exclusive scan of per-chunk counts (single workgroup, sequential over strips)
+__global__ void scan_counts_kernel(const uint32_t* count, uint64_t* base, int n) {
+    __shared__ uint32_t scratch[8];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int s = 0; s < n; s += kTPB) {
+        const int i = s + threadIdx.x;
+        const uint32_t v = (i < n) ? count[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan(v, scratch, &tot);
+        if (i < n) base[i] = carry + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) carry += tot;
+        __syncthreads();
+    }
+}
+
+// Inverse of one block: parse, dequantise, IDCT in the reference order, clamp/truncate.
+template <int N>
+__global__ __launch_bounds__(kTPB) void decode_kernel(DecArgs a, const uint32_t* W, uint64_t* end_out) {
+    constexpr int NN = N * N;
+    const uint64_t nblocks = uint64_t(a.nframes) * a.bx * a.by;
+    const uint64_t b = uint64_t(blockIdx.x) * kTPB + threadIdx.x;
+    if (b >= nblocks) return;
+    const EncTables* __restrict__ tab = a.tab;
+    uint64_t pos = a.block_bit[b];
+    const int bl = int(getbits(W, pos, 4));
+    pos += 4;
+    int length = NN;
+    if (a.rle) {
+        length = int(getbits(W, pos, bl));
+        pos += bl;
+    }
+    if (length > NN) length = NN;  // cannot happen for a well-formed stream
+    double Y[NN];
+#pragma unroll
+    for (int k = 0; k < NN; k++) Y[k] = 0.0;
+    const int* zz = (N == 4) ? kZZ4 : kZZ8;
+    for (int k = 0; k < length; k++) {
+        const uint32_t raw = getbits(W, pos, bl);
+        pos += bl;
+        const int sh = 16 - bl;
+        const int16_t v = int16_t(int16_t(uint16_t(raw << sh)) >> sh);
+        Y[zz[k]] = double(v);
+    }
+    if (b == nblocks - 1 && end_out) *end_out = pos;
+    // Block::processIDCTMulQ: Y *= q, then temp[ij] += R[uv][ij] * Y[uv] over uv ascending.
+    // Zero Y terms add +-0 and leave every partial sum unchanged, so they are skipped.
+    double t[NN];
+#pragma unroll
+    for (int k = 0; k < NN; k++) t[k] = 0.0;
+#pragma unroll
+    for (int uv = 0; uv < NN; uv++) {
+        const double y = Y[uv] * tab->qd[uv];
+        if (y != 0.0) {
+            const double* R = &tab->R[uv * NN];
+#pragma unroll
+            for (int ij = 0; ij < NN; ij++) t[ij] = t[ij] + R[ij] * y;
+        }
+    }
+    const uint64_t bpf = uint64_t(a.bx) * a.by;
+    const uint64_t f = b / bpf, r = b - f * bpf;
+    const int byi = int(r / a.bx), bxi = int(r - uint64_t(byi) * a.bx);
+    uint8_t* o = a.out + f * a.frame_pitch + uint64_t(byi) * N * a.stride + uint64_t(bxi) * N;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            double x = t[i * N + j] + 128.0;
+            x = x < 0.0 ? 0.0 : (x > 255.0 ? 255.0 : x);
+            o[uint64_t(i) * a.stride + j] = uint8_t(x);
+        }
+    }
+}
+
+// Host-driven decode sequence (ie_capi.cpp::decode calls this).
+int decode_frames_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& da, int n,
+                         uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,
+                         uint64_t* base, uint64_t* block_bit, unsigned* changed, uint64_t* end_out, hipStream_t s,
+                         int max_rounds) {
+    const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
+    const int nchunks = int(span / chunk_bits + 1);
+    WalkArgs wa{};
+    wa.words = W;
+    wa.nbits = nbits;
+    wa.start_bit = start_bit;
+    wa.chunk_bits = chunk_bits;
+    wa.nchunks = nchunks;
+    wa.nn = n * n;
+    wa.rle = da.rle;
+    wa.entry = entry;
+    wa.count = count;
+    wa.changed = changed;
+    const dim3 g((nchunks + kTPB - 1) / kTPB), blk(kTPB);
+    wa.first = 1;
+    wa.exit_in = exA;
+    wa.exit_out = exA;
+    hipLaunchKernelGGL(walk_kernel, g, blk, 0, s, wa);
+    uint64_t* cur = exA;
+    uint64_t* nxt = exB;
+    int rounds = 0;
+    for (; rounds < max_rounds; rounds++) {
+        unsigned h = 0;
+        if (hipMemsetAsync(changed, 0, sizeof(unsigned), s) != hipSuccess) return -1;
+        wa.first = 0;
+        wa.exit_in = cur;
+        wa.exit_out = nxt;
+        hipLaunchKernelGGL(walk_kernel, g, blk, 0, s, wa);
+        if (hipMemcpyAsync(&h, changed, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+        if (hipStreamSynchronize(s) != hipSuccess) return -1;
+        uint64_t* t = cur;
+        cur = nxt;
+        nxt = t;
+        if (!h) break;
+    }
+    if (rounds == max_rounds) return -2;
+    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
+    hipLaunchKernelGGL(index_kernel, g, blk, 0, s, wa, base, block_bit, uint64_t(da.nframes) * da.bx * da.by);
+    DecArgs d = da;
+    d.block_bit = block_bit;
+    const uint64_t nblocks = uint64_t(da.nframes) * da.bx * da.by;
+    const dim3 gd(unsigned((nblocks + kTPB - 1) / kTPB));
+    if (n == 4) hipLaunchKernelGGL((decode_kernel<4>), gd, blk, 0, s, d, W, end_out);
+    else hipLaunchKernelGGL((decode_kernel<8>), gd, blk, 0, s, d, W, end_out);
+    return rounds;
+}
+
+}  // namespace ie

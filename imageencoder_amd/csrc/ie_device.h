@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ie_dct.h"
+
 namespace ie {
 
 constexpr int kTPB = 256;  // threads per workgroup: 4 waves of 64
@@ -13,10 +15,13 @@ struct EncTables {
     // FP32 fast path (separable DCT, see encode_fast in ie_encode.hip)
     float cf[64];   // cf[u*N+i] = float(c[u][i])
     float g[64];    // float(S[uv] / q[uv])
-    float thr[64];  // near-tie half-width on |t|: |frac(|t|)-0.5| <= thr -> FP64 re-evaluation; <0: t exact
+    float thr[64];  // bound on |t32 - t_ref|; < 0: t32 exact (coefficient 0 only)
+    float lim[64];  // 0.5 - thr: |t32 - rint(t32)| >= lim flags a possible rounding tie
+    DctConsts dct;  // butterfly constants cos(k pi/16)
     // FP64 reference order (algo.cpp:309-331, Block.cpp:149-152)
     double S[64];   // C(u)*C(v)
     double qd[64];  // double(q[uv])
+    double rq[64];  // 1/q when q is a power of two (exact), else 0 -> divide
     double c[64];   // c[u*N+i] (std::cos, algo.cpp:318-319)
     double P[64 * 64];  // P[uv*NN + ij] = c[u][i]*c[v][j]
     // inverse (algo.cpp:343-363): R[uv*NN + ij] = ((C(u)*C(v))*c[u][i])*c[v][j]
@@ -41,14 +46,13 @@ struct EncArgs {
     uint32_t* out;           // 4-byte aligned, word w = stream bytes [4w, 4w+4)
     uint64_t out_pitch_words;
     uint64_t start_bit;
-    uint64_t* st_agg;        // [ntiles] {tag:8 | aggregate:24 | tail32:32}
-    uint64_t* st_inc;        // [ntiles] {tag:8 | inclusive:56}
-    unsigned long long* ticket;
+    uint64_t* st;            // [2*ntiles]: {tag:8 | aggregate:24 | tail32:32}, {tag:8 | inclusive:56}
+    unsigned long long* ticket;  // nullptr: tiles in blockIdx order; else an atomic ticket
     unsigned long long ticket_base;
     uint32_t tag;            // epoch tag 1..255
     uint64_t* frame_start;   // [nframes] absolute start bit of each frame's payload
     uint64_t* chain_end;     // [nchains] absolute end bit
-    unsigned* err;           // [0] look-back timeouts, [1] fallback coefficient count
+    unsigned* err;           // [0] look-back timeouts, [2..65] fallback coefficient counters
     const EncTables* tab;
     int16_t* coef;           // optional: quantised coefficients, natural order, [nframes*bx*by][N*N]
 };
@@ -63,8 +67,7 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
     int ntiles;
     uint32_t* out;
     uint64_t start_bit;
-    uint64_t* st_agg;
-    uint64_t* st_inc;
+    uint64_t* st;
     unsigned long long* ticket;
     unsigned long long ticket_base;
     uint32_t tag;
@@ -76,18 +79,17 @@ void launch_pack(const PackArgs& a, hipStream_t s);
 void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, hipStream_t s);
 
 struct DecArgs {
-    const uint8_t* in;       // encoded bytes
-    uint64_t len;
-    uint64_t start_bit;
-    const uint64_t* block_bit;  // [nblocks] start bit of every block record (from the index pass)
-    int w, h, nframes, bx, by, rle;
+    const uint64_t* block_bit;  // [nblocks] start bit of every block record (from the walk index)
+    int nframes, bx, by, rle;
     uint8_t* out;
     uint64_t stride, frame_pitch;
     const EncTables* tab;
 };
-void launch_decode(const DecArgs& a, int n, hipStream_t s);
-int launch_decode_index(const uint8_t* in, uint64_t len, uint64_t start_bit, uint64_t nblocks, int n,
-                        int rle, uint64_t* block_bit, uint64_t* end_bit, void* scratch, size_t scratch_bytes,
-                        hipStream_t s);
+// Parallel record index (chunk walks + fix-up rounds) followed by the block decode.  Returns the
+// number of fix-up rounds (>= 0) or < 0 on error.
+int decode_frames_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& da, int n,
+                         uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,
+                         uint64_t* base, uint64_t* block_bit, unsigned* changed, uint64_t* end_out, hipStream_t s,
+                         int max_rounds);
 
 }  // namespace ie

@@ -4,21 +4,23 @@
 //   lane      = one "group" of BPT horizontally adjacent N x N blocks (4 x 4x4 or 1 x 8x8), so a
 //               wave reads 64 x 16 B (or 64 x 8 B) contiguous bytes per pixel row;
 //   workgroup = one tile of kTPB groups (<= 1024 blocks), never straddling a frame.
-// Per tile, in one pass over the pixels (each byte is read from HBM once, each output word
+// Per tile, in one pass over the pixels (each input byte is read from HBM once, each output word
 // written once):
 //   1. level shift + forward DCT + quantise every block (Block.cpp:139-153, algo.cpp:309-331):
-//      FAST = separable FP32 with a rigorous error bound; coefficients whose quotient lies within
-//      that bound of a rounding tie are re-evaluated in the reference's exact FP64 operation
-//      order.  EXACT = every coefficient in FP64 reference order.
+//      FAST = the butterfly FP32 DCT of ie_dct.h, whose error the host bounds rigorously;
+//      coefficients whose quotient lies within that bound of a rounding tie are re-evaluated in
+//      the reference's exact FP64 operation order.  EXACT = every coefficient in FP64 order.
 //   2. zig-zag RLE sizing (Block.cpp:186-232, :383-397): bl, Lw, record length;
 //   3. workgroup exclusive scan of record lengths; the records are written MSB-first into an
 //      LDS image of the tile's bit stream (Block.cpp:372-413, BitStream.cpp:61-77);
-//   4. decoupled look-back over the preceding tiles of the chain for the tile's global bit offset;
+//   4. decoupled look-back over the preceding tiles of the chain for the tile's global bit offset
+//      (the whole workgroup reads 1024 predecessor states per round trip);
 //   5. funnel-shifted, coalesced store of the LDS image into the output words.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "ie_common.cuh"
+#include "ie_dct.h"
 #include "ie_device.h"
 
 namespace ie {
@@ -34,45 +36,67 @@ template <> struct ZigZag<8> {
                                     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 };
 
+// pos[k] = zig-zag position of natural index k (inverse of ZigZag<N>::idx)
+template <int N> struct ZigZagInv;
+template <> struct ZigZagInv<4> {
+    static constexpr int pos[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
+};
+template <> struct ZigZagInv<8> {
+    static constexpr int pos[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                                    3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                                    10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                                    21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+};
+
 template <int N> struct Geo;
 template <> struct Geo<4> { static constexpr int BPT = 4; };  // 16 B per pixel row per lane
 template <> struct Geo<8> { static constexpr int BPT = 1; };  //  8 B per pixel row per lane
 
 // bits-in-tile upper bound: 4 + 16 * (N*N + 1) bits per block
 template <int N> constexpr int image_words() {
-    return (kTPB * Geo<N>::BPT * (4 + 16 * (N * N + 1)) + 31) / 32 + 2;
+    return ((kTPB * Geo<N>::BPT * (4 + 16 * (N * N + 1)) + 31) / 32 + 2 + 3) / 4 * 4;  // keeps misc 16-B aligned
 }
+
+template <int WPR>
+__device__ __forceinline__ uint32_t pix(const uint32_t (&row)[WPR], int byte) {
+    return (row[byte >> 2] >> (8 * (byte & 3))) & 0xFFu;
+}
+
+// The pixel bytes of one block, packed four to a word (row-major): the argument of the
+// out-of-line FP64 path, passed in registers.
+template <int N> struct BlockPx {
+    uint32_t w[N * N / 4];
+};
 
 // Exact coefficient in the reference's FP64 order (algo.cpp:314-325, Block.cpp:149-152):
 //   acc = 0; for i, j: acc = acc + P[uv][ij] * x[ij];  D = acc * (C(u)C(v));  round(D / q)
 // with x[ij] = double(p) - 128 (Block.cpp:141-143).  This file is compiled with
 // -ffp-contract=off, so every product and sum is rounded separately as in the reference; the
-// division is IEEE; the rounding is half away from zero (std::round).
-template <int N, int WPR>
-__device__ __forceinline__ int exact_coef(const EncTables* __restrict__ tab, int k, const uint32_t (&seg)[N][WPR],
-                                          int b) {
+// division is IEEE (a multiply by the exact reciprocal when q is a power of two); the rounding is
+// half away from zero (std::round).  Out of line: it runs only for the few coefficients whose
+// FP32 quotient lies near a rounding tie, and must not inflate the hot path's registers.
+template <int N>
+__device__ __noinline__ int exact_coef(const EncTables* __restrict__ tab, int k, BlockPx<N> px) {
     constexpr int NN = N * N;
     const double* P = &tab->P[k * NN];
     double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < N; i++)
-#pragma unroll
-        for (int j = 0; j < N; j++) {
-            const int byte = b * N + j;
-            const double x = double(int((seg[i][byte >> 2] >> (8 * (byte & 3))) & 0xFFu)) + (-128.0);
-            acc = acc + P[i * N + j] * x;
-        }
+    for (int ij = 0; ij < NN; ij++) {
+        const double x = double(int((px.w[ij >> 2] >> (8 * (ij & 3))) & 0xFFu)) + (-128.0);
+        acc = acc + P[ij] * x;
+    }
     const double D = acc * tab->S[k];
-    const double t = D / tab->qd[k];
+    const double rq = tab->rq[k];
+    const double t = (rq != 0.0) ? D * rq : D / tab->qd[k];
     double r = trunc(t);
     if (fabs(t - r) >= 0.5) r += copysign(1.0, t);
     return int(r);
 }
 
-// Load the pixel rows of one group: seg[r][m] = bytes [4m, 4m+4) of the group's row r.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// Load the pixel rows of one group: seg[r][m] = bytes [4m, 4m+4) of the group's row r.
 template <int N, int WPR>
 __device__ __forceinline__ void load_group(const EncArgs& a, const uint8_t* base, int nblk, uint32_t (&seg)[N][WPR]) {
     constexpr int BPT = Geo<N>::BPT;
@@ -105,33 +129,115 @@ __device__ __forceinline__ void load_group(const EncArgs& a, const uint8_t* base
     }
 }
 
+// Quantise block b of the group into zp[] (zig-zag order, two int16 per word: z[2j] in the low
+// half); returns the number of coefficients re-evaluated in FP64.  The values pass through the
+// thread's private LDS slot `stage` (NN int16), so the rare FP64 re-evaluations patch them at a
+// runtime index without forcing a register array into scratch memory.
+template <int N, int WPR, bool EXACT>
+__device__ __forceinline__ unsigned quantize_block(const EncTables* __restrict__ tab, const uint32_t (&seg)[N][WPR],
+                                                   int b, bool valid, uint32_t* stage, uint32_t (&zp)[N * N / 2]) {
+    constexpr int NN = N * N;
+    uint64_t need = 0;
+    if constexpr (!EXACT) {
+        float x[NN];
+#pragma unroll
+        for (int i = 0; i < N; i++)
+#pragma unroll
+            for (int j = 0; j < N; j++) x[i * N + j] = float(pix<WPR>(seg[i], b * N + j)) - 128.0f;
+        dct2d<N>(x, tab->dct, FloatOp());
+        int qv[NN];
+#pragma unroll
+        for (int k = 0; k < NN; k++) {
+            const float t = x[k] * tab->g[k];
+            if (k == 0 && tab->thr[0] < 0.0f) {
+                // t is exact here (integer sum times a power of two): round half away from zero
+                qv[k] = int(truncf(t + copysignf(0.5f, t)));
+            } else {
+                const float r = rintf(t);
+                need |= uint64_t(fabsf(t - r) >= tab->lim[k]) << k;  // lim = 0.5 - bound
+                qv[k] = int(r);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NN / 2; j++)
+            zp[j] = (uint32_t(qv[ZigZag<N>::idx[2 * j]]) & 0xFFFFu) | (uint32_t(qv[ZigZag<N>::idx[2 * j + 1]]) << 16);
+    } else {
+        if constexpr (NN == 64) need = ~0ull;
+        else need = (1ull << NN) - 1;
+#pragma unroll
+        for (int j = 0; j < NN / 2; j++) zp[j] = 0;
+    }
+    if (!valid) need = 0;
+    unsigned nf = 0;
+    if (need) {  // divergent and rare in FAST mode: the FP64 reference order for flagged k
+        BlockPx<N> px;
+#pragma unroll
+        for (int i = 0; i < N; i++)
+#pragma unroll
+            for (int m = 0; m < N / 4; m++) px.w[i * (N / 4) + m] = seg[i][(b * N) / 4 + m];
+#pragma unroll
+        for (int j = 0; j < NN / 2; j++) stage[j] = zp[j];
+        do {
+            const int k = __ffsll((unsigned long long)need) - 1;
+            need &= need - 1;
+            const uint32_t v = uint32_t(exact_coef<N>(tab, k, px)) & 0xFFFFu;
+            const int kz = ZigZagInv<N>::pos[k];
+            const uint32_t w = stage[kz >> 1];  // patch one int16 half of a word (same type: no aliasing)
+            stage[kz >> 1] = (kz & 1) ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
+            nf++;
+        } while (need);
+#pragma unroll
+        for (int j = 0; j < NN / 2; j++) zp[j] = stage[j];
+    }
+    return nf;
+}
+
 template <int N, bool EXACT>
-__global__ __launch_bounds__(kTPB) void encode_kernel(EncArgs a) {
+__global__ __launch_bounds__(kTPB, 4) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     constexpr int NN = N * N;
     constexpr int BPT = Geo<N>::BPT;
     constexpr int WPR = BPT * N / 4;
     constexpr int IMGW = image_words<N>();
-    __shared__ uint32_t smem[IMGW + 16];
+    __shared__ uint32_t smem[IMGW + 32];
     uint32_t* img = smem;
-    uint32_t* misc = smem + IMGW;  // [0..3] scan, [4] ticket, [5..6] excl lo/hi, [7] pred tail
+    uint32_t* misc = smem + IMGW;  // [0..3] scan, [4] ticket, [5..6] excl, [7] pred tail, [8..31] look-back
 
     const int tid = threadIdx.x;
-    if (tid == 0) misc[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
-    __syncthreads();
-    const int t = int(misc[4]);
-    if (t >= a.ntiles) return;  // ticket desync (a failed earlier launch): never touch memory
-    const int frame = t / a.tiles_per_frame;
-    const int tif = t - frame * a.tiles_per_frame;
-    const EncTables* __restrict__ tab = a.tab;
+    // Tile order = dispatch order.  Workgroups are dispatched in increasing blockIdx per XCD, so
+    // every predecessor of a resident tile is resident or done and the look-back cannot deadlock;
+    // the bounded spins report (never hang) should that ever not hold, and the host then re-runs
+    // with an atomic ticket (a.ticket != nullptr), which orders tiles explicitly.
+    int t;
+    if (a.ticket) {
+        if (tid == 0) misc[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+        __syncthreads();
+        t = int(misc[4]);
+        if (t >= a.ntiles) return;  // ticket desync (a failed earlier launch): never touch memory
+    } else {
+        t = int(blockIdx.x);
+    }
+    // Independent images interleave their tiles in ticket order (frame = t % nframes), so every
+    // frame's chain advances together; a concatenated stream keeps chain order = ticket order.
+    int frame, tif, step;
+    if (a.segmented) {
+        frame = t % a.nframes;
+        tif = t / a.nframes;
+        step = a.nframes;
+    } else {
+        frame = t / a.tiles_per_frame;
+        tif = t - frame * a.tiles_per_frame;
+        step = 1;
+    }
+    const int chain_pos = a.segmented ? tif : t;  // tiles before this one in its chain
 
     // ---------------------------------------------------------------- 1. transform + quantise
     const int gi = tif * kTPB + tid;
     const bool active = gi < a.groups_per_frame;
-    int nblk = 0;
+    int nblk = 0, byi = 0, bx0 = 0;
     uint32_t seg[N][WPR];
     if (active) {
-        const int byi = gi / a.gpr, seg_i = gi - byi * a.gpr;
-        const int bx0 = seg_i * BPT;
+        byi = gi / a.gpr;
+        bx0 = (gi - byi * a.gpr) * BPT;
         nblk = min(BPT, a.bx - bx0);
         const uint8_t* base = a.y + size_t(frame) * a.frame_pitch + size_t(byi) * N * a.stride + size_t(bx0) * N;
         load_group<N, WPR>(a, base, nblk, seg);
@@ -142,86 +248,35 @@ __global__ __launch_bounds__(kTPB) void encode_kernel(EncArgs a) {
             for (int m = 0; m < WPR; m++) seg[r][m] = 0;
     }
 
-    int zq[BPT][NN];        // quantised coefficients, zig-zag order
-    uint32_t blw[BPT];      // bl | Lw << 8
+    uint32_t zp[BPT][NN / 2];  // quantised coefficients, zig-zag order, two int16 per word
+    uint32_t blw[BPT];         // bl | Lw << 8
     uint32_t mybits = 0;
     unsigned nfall = 0;
+    uint32_t* stage = img + tid * (NN / 2);  // private slot; the image is built after the scan
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
-        float x[NN];
-#pragma unroll
-        for (int i = 0; i < N; i++)
-#pragma unroll
-            for (int j = 0; j < N; j++) {
-                const int byte = b * N + j;
-                x[i * N + j] = float((seg[i][byte >> 2] >> (8 * (byte & 3))) & 0xFFu) - 128.0f;
-            }
-        int zn[NN];  // natural order
-        uint64_t need = 0;
-        if constexpr (!EXACT) {
-            // separable FP32: y[i][v] = sum_j cf[v][j] x[i][j];  D[u][v] = sum_i cf[u][i] y[i][v]
-            float yv[NN];
-#pragma unroll
-            for (int i = 0; i < N; i++)
-#pragma unroll
-                for (int v = 0; v < N; v++) {
-                    float acc = 0.0f;
-#pragma unroll
-                    for (int j = 0; j < N; j++) acc = __builtin_fmaf(tab->cf[v * N + j], x[i * N + j], acc);
-                    yv[i * N + v] = acc;
-                }
-#pragma unroll
-            for (int u = 0; u < N; u++)
-#pragma unroll
-                for (int v = 0; v < N; v++) {
-                    float acc = 0.0f;
-#pragma unroll
-                    for (int i = 0; i < N; i++) acc = __builtin_fmaf(tab->cf[u * N + i], yv[i * N + v], acc);
-                    const int k = u * N + v;
-                    const float tq = acc * tab->g[k];
-                    const float av = fabsf(tq);
-                    const float fl = floorf(av);
-                    const float fr = av - fl;
-                    if (fabsf(fr - 0.5f) <= tab->thr[k]) need |= 1ull << k;
-                    const int qi = int(fl) + (fr >= 0.5f ? 1 : 0);
-                    zn[k] = tq < 0.0f ? -qi : qi;
-                }
-        } else {
-            if constexpr (NN == 64) need = ~0ull;
-            else need = (1ull << NN) - 1;
-#pragma unroll
-            for (int k = 0; k < NN; k++) zn[k] = 0;
-        }
-        // FP64 re-evaluation of flagged coefficients; the wave skips k that no lane flagged
-#pragma unroll
-        for (int k = 0; k < NN; k++) {
-            const bool mine = (need >> k) & 1ull;
-            if (__ballot(mine)) {
-                if (mine && b < nblk) {
-                    zn[k] = exact_coef<N, WPR>(tab, k, seg, b);
-                    nfall++;
-                }
-            }
-        }
+        __builtin_amdgcn_sched_barrier(0);  // one block at a time: keeps the live set small
+        nfall += quantize_block<N, WPR, EXACT>(tab, seg, b, b < nblk, stage, zp[b]);
         if (a.coef && b < nblk) {
-            const int byi = gi / a.gpr, bxb = (gi - byi * a.gpr) * BPT + b;
-            int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + size_t(byi) * a.bx + bxb) * NN;
+            int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + size_t(byi) * a.bx + bx0 + b) * NN;
 #pragma unroll
-            for (int k = 0; k < NN; k++) dst[k] = int16_t(zn[k]);
+            for (int k = 0; k < NN; k++) {
+                const int kz = ZigZagInv<N>::pos[k];
+                dst[k] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
+            }
         }
-        // zig-zag + RLE sizing
+        // zig-zag + RLE sizing: bl = max(bits_needed over all values, ffs(L)), ffs(0) = 1
         uint64_t nz = 0;
-        int maxb = 1;
+        uint32_t mo = 0;
 #pragma unroll
         for (int kz = 0; kz < NN; kz++) {
-            const int v = zn[ZigZag<N>::idx[kz]];
-            zq[b][kz] = v;
+            const int v = (kz & 1) ? (int(zp[b][kz >> 1]) >> 16) : (int(zp[b][kz >> 1] << 16) >> 16);
             nz |= uint64_t(v != 0) << kz;
-            const uint32_t s = uint32_t(v ^ (v >> 31));
-            maxb = max(maxb, 33 - __clz(s));
+            mo |= uint32_t(v ^ (v >> 31));
         }
+        const int maxb = 33 - __clz(mo);  // bits_needed (utils.hpp:226-243) of the widest value
         const int L = nz ? 64 - __clzll((long long)nz) : 0;
-        const int ffsL = L ? 32 - __clz(L) : 1;  // ffs(0) == 1 (utils.hpp:210-216)
+        const int ffsL = L ? 32 - __clz(L) : 1;  // utils.hpp:210-216, with ffs(0) == 1
         const int bl = max(maxb, ffsL);
         int lw;
         if (!a.rle) {
@@ -235,7 +290,10 @@ __global__ __launch_bounds__(kTPB) void encode_kernel(EncArgs a) {
         blw[b] = uint32_t(bl) | (uint32_t(lw) << 8);
         if (b < nblk) mybits += 4u + uint32_t(bl) * uint32_t(lw + a.rle);
     }
-    if (!EXACT && nfall) atomicAdd(&a.err[1], nfall);
+    if (!EXACT) {  // fallback statistics: one atomic per wave, spread over 64 counters
+        const unsigned wsum = unsigned(wave_sum64(nfall));
+        if ((tid & 63) == 0 && wsum) atomicAdd(&a.err[2 + ((t * 4 + (tid >> 6)) & 63)], wsum);
+    }
 
     // ---------------------------------------------------------------- 2. tile scan + LDS image
     uint32_t A;
@@ -249,11 +307,18 @@ __global__ __launch_bounds__(kTPB) void encode_kernel(EncArgs a) {
         for (int b = 0; b < BPT; b++) {
             if (b < nblk) {
                 const int bl = int(blw[b] & 0xFF), lw = int(blw[b] >> 8);
-                sink.put(4, uint32_t(bl) & 0xFu);
-                if (a.rle) sink.put(bl, uint32_t(lw));
+                const uint32_t m = (1u << bl) - 1u;
+                if (a.rle) sink.put(4 + bl, ((uint32_t(bl) & 0xFu) << bl) | uint32_t(lw));
+                else sink.put(4, uint32_t(bl) & 0xFu);
+                // value fields in pairs: (z[2j], z[2j+1]) as one 2*bl-bit put
 #pragma unroll
-                for (int kz = 0; kz < NN; kz++)
-                    if (kz < lw) sink.put(bl, uint32_t(zq[b][kz]));
+                for (int j = 0; j < NN / 2; j++) {
+                    if (2 * j < lw) {
+                        const uint32_t lo = zp[b][j] & m, hi = (zp[b][j] >> 16) & m;
+                        if (2 * j + 1 < lw) sink.put(2 * bl, (lo << bl) | hi);
+                        else sink.put(bl, lo);
+                    }
+                }
             }
         }
         sink.finish();
@@ -261,52 +326,60 @@ __global__ __launch_bounds__(kTPB) void encode_kernel(EncArgs a) {
     __syncthreads();
 
     // ---------------------------------------------------------------- 3. look-back
-    const int c0 = a.segmented ? frame * a.tiles_per_frame : 0;
     const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
     uint32_t* out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
-    const uint32_t my_tail = (tid == 0) ? image_tail32(img, A) : 0u;
-    if (tid == 0 && A >= 32) st_state(&a.st_agg[t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | my_tail);
-    if (tid < 64) {
-        uint64_t excl = 0;
-        uint32_t ptail = 0;
-        if (t == c0) {
+    if (tid == 0) {
+        const uint32_t my_tail = image_tail32(img, A);
+        if (chain_pos == 0) {
             // chain start: the bits before start_bit belong to the caller (header); keep them
             const uint64_t P = a.start_bit;
             const uint32_t s = uint32_t(P & 31);
-            ptail = s ? (bswap32(out[P >> 5]) >> (32 - s)) : 0u;
-        } else {
-            excl = lookback(a.st_agg, a.st_inc, t, c0, a.tag, &ptail, a.err);
+            const uint32_t ptail = s ? (bswap32(out[P >> 5]) >> (32 - s)) : 0u;
+            const uint32_t tl = (A >= 32) ? my_tail : ((A ? (ptail << A) : ptail) | my_tail);
+            st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
+            st_state(&a.st[2 * t + 1], (uint64_t(a.tag) << 56) | (uint64_t(A) & kMask56));
+            misc[5] = 0;
+            misc[6] = 0;
+            misc[7] = ptail;
+        } else if (A >= 32) {
+            st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | my_tail);
         }
+    }
+    if (chain_pos != 0) {
+        uint32_t ptail;
+        const uint64_t excl = lookback_wg(a.st, t, chain_pos, step, a.tag, &ptail, a.err, misc + 8);
         if (tid == 0) {
             if (A < 32) {
                 // a short tile publishes its tail only now: it must carry predecessor bits
-                const uint32_t tl = (A ? (ptail << A) : ptail) | my_tail;
-                st_state(&a.st_agg[t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
+                const uint32_t tl = (A ? (ptail << A) : ptail) | image_tail32(img, A);
+                st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
             }
-            st_state(&a.st_inc[t], (uint64_t(a.tag) << 56) | ((excl + A) & kMask56));
+            st_state(&a.st[2 * t + 1], (uint64_t(a.tag) << 56) | ((excl + A) & kMask56));
             misc[5] = uint32_t(excl);
             misc[6] = uint32_t(excl >> 32);
             misc[7] = ptail;
-            const uint64_t P = a.start_bit + excl;
-            if (tif == 0) a.frame_start[frame] = P;
-            if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
         }
     }
     __syncthreads();
+    const uint64_t excl = uint64_t(misc[5]) | (uint64_t(misc[6]) << 32);
+    if (tid == 0) {
+        const uint64_t P = a.start_bit + excl;
+        if (tif == 0) a.frame_start[frame] = P;
+        if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
+    }
 
     // ---------------------------------------------------------------- 4. store
-    const uint64_t excl = uint64_t(misc[5]) | (uint64_t(misc[6]) << 32);
     store_image(out, img, A, a.start_bit + excl, misc[7], chain_last);
 }
 
 void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s) {
     const dim3 grid(a.ntiles), block(kTPB);
     if (n == 4) {
-        if (exact) hipLaunchKernelGGL((encode_kernel<4, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((encode_kernel<4, false>), grid, block, 0, s, a);
+        if (exact) hipLaunchKernelGGL((encode_kernel<4, true>), grid, block, 0, s, a, a.tab);
+        else hipLaunchKernelGGL((encode_kernel<4, false>), grid, block, 0, s, a, a.tab);
     } else {
-        if (exact) hipLaunchKernelGGL((encode_kernel<8, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((encode_kernel<8, false>), grid, block, 0, s, a);
+        if (exact) hipLaunchKernelGGL((encode_kernel<8, true>), grid, block, 0, s, a, a.tab);
+        else hipLaunchKernelGGL((encode_kernel<8, false>), grid, block, 0, s, a, a.tab);
     }
 }
 

@@ -61,20 +61,21 @@ void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long lo
 }
 
 // One tile = kTPB threads x kPackBytesPerThread input bytes, codes of up to 32 bits.
-constexpr int kPackWords = kTPB * kPackBytesPerThread + 2;  // 32 bits per byte worst case
+constexpr int kPackWords = kTPB * kPackBytesPerThread + 4;  // 32 bits per byte worst case
 
 __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
-    __shared__ uint32_t smem[kPackWords + 16];
+    __shared__ uint32_t smem[kPackWords + 32];
     __shared__ uint32_t s_code[256];
     __shared__ uint8_t s_len[256];
     uint32_t* img = smem;
     uint32_t* misc = smem + kPackWords;
     const int tid = threadIdx.x;
-    if (tid == 0) misc[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+    // tile order = dispatch order (see encode_kernel); the atomic ticket is the fallback
+    if (a.ticket && tid == 0) misc[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
     s_code[tid] = a.code[tid];
     s_len[tid] = a.len[tid];
     __syncthreads();
-    const int t = int(misc[4]);
+    const int t = a.ticket ? int(misc[4]) : int(blockIdx.x);
     if (t >= a.ntiles) return;
 
     const uint64_t p = uint64_t(t) * (kTPB * kPackBytesPerThread) + uint64_t(tid) * kPackBytesPerThread;
@@ -108,32 +109,40 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     }
     __syncthreads();
 
+    // look-back (a single chain in ticket order) -- same protocol as encode_kernel
     const bool last = (t == a.ntiles - 1);
-    const uint32_t my_tail = (tid == 0) ? image_tail32(img, A) : 0u;
-    if (tid == 0 && A >= 32) st_state(&a.st_agg[t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | my_tail);
-    if (tid < 64) {
-        uint64_t excl = 0;
-        uint32_t ptail = 0;
+    if (tid == 0) {
+        const uint32_t my_tail = image_tail32(img, A);
         if (t == 0) {
             const uint32_t s = uint32_t(a.start_bit & 31);
-            ptail = s ? (bswap32(a.out[a.start_bit >> 5]) >> (32 - s)) : 0u;
-        } else {
-            excl = lookback(a.st_agg, a.st_inc, t, 0, a.tag, &ptail, a.err);
+            const uint32_t ptail = s ? (bswap32(a.out[a.start_bit >> 5]) >> (32 - s)) : 0u;
+            const uint32_t tl = (A >= 32) ? my_tail : ((A ? (ptail << A) : ptail) | my_tail);
+            st_state(&a.st[0], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
+            st_state(&a.st[1], (uint64_t(a.tag) << 56) | (uint64_t(A) & kMask56));
+            misc[5] = 0;
+            misc[6] = 0;
+            misc[7] = ptail;
+        } else if (A >= 32) {
+            st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | my_tail);
         }
+    }
+    if (t != 0) {
+        uint32_t ptail;
+        const uint64_t excl = lookback_wg(a.st, t, t, 1, a.tag, &ptail, a.err, misc + 8);
         if (tid == 0) {
             if (A < 32) {
-                const uint32_t tl = (A ? (ptail << A) : ptail) | my_tail;
-                st_state(&a.st_agg[t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
+                const uint32_t tl = (A ? (ptail << A) : ptail) | image_tail32(img, A);
+                st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
             }
-            st_state(&a.st_inc[t], (uint64_t(a.tag) << 56) | ((excl + A) & kMask56));
+            st_state(&a.st[2 * t + 1], (uint64_t(a.tag) << 56) | ((excl + A) & kMask56));
             misc[5] = uint32_t(excl);
             misc[6] = uint32_t(excl >> 32);
             misc[7] = ptail;
-            if (last) a.chain_end[0] = a.start_bit + excl + A;
         }
     }
     __syncthreads();
     const uint64_t excl = uint64_t(misc[5]) | (uint64_t(misc[6]) << 32);
+    if (tid == 0 && last) a.chain_end[0] = a.start_bit + excl + A;
     store_image(a.out, img, A, a.start_bit + excl, misc[7], last);
 }
 

@@ -112,8 +112,8 @@ int ie_huffman_hist(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint32_t* hist,
 int ie_huffman_pack(ie_ctx* ctx, const uint8_t* bytes, size_t n, const uint32_t* code, const uint8_t* len,
                     uint8_t* out, size_t out_cap, uint64_t start_bit, uint64_t* end_bit);
 
-/* Copy n bytes shifted right by `shift` bits (0..7) into out starting at bit start_bit (the
- * "no gain" path of Huffman.cpp:329-341 writes '0' + the input). */
+/* Copy n bytes into out starting at bit start_bit, i.e. shifted by start_bit % 8 (the "no gain"
+ * path of Huffman.cpp:329-341 writes '0' + the input: start_bit = 1). */
 int ie_bitcopy(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint8_t* out, size_t out_cap, uint64_t start_bit);
 
 /* ---- Inverse path (ImageDecoder.cpp:55-122, Block.cpp:100-107,163-177,442-472) ------------
