@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -374,6 +375,8 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.err = c->d_err;
     a.tab = c->d_tab;
     a.coef = coef;
+    static const int ablate = getenv("IE_ABLATE") ? atoi(getenv("IE_ABLATE")) : 0;  // profiling only
+    a.ablate = ablate;
     ie::launch_encode(a, c->n, mode == IE_MODE_EXACT, c->stream);
     HIPCHK(c, hipGetLastError());
     if (c->use_ticket) c->ticket_base += uint64_t(g.ntiles);

@@ -55,6 +55,7 @@ struct EncArgs {
     unsigned* err;           // [0] look-back timeouts, [2..65] fallback coefficient counters
     const EncTables* tab;
     int16_t* coef;           // optional: quantised coefficients, natural order, [nframes*bx*by][N*N]
+    int ablate;              // profiling only (IE_ABLATE): 1 no FP64, 2 no emission, 4 no look-back, 8 no store, 16 no DCT
 };
 
 void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s);

@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ie_common.cuh"
 #include "ie_dct.h"
 #include "ie_device.h"
@@ -133,63 +135,99 @@ __device__ __forceinline__ void load_group(const EncArgs& a, const uint8_t* base
 // half); returns the number of coefficients re-evaluated in FP64.  The values pass through the
 // thread's private LDS slot `stage` (NN int16), so the rare FP64 re-evaluations patch them at a
 // runtime index without forcing a register array into scratch memory.
-template <int N, int WPR, bool EXACT>
-__device__ __forceinline__ unsigned quantize_block(const EncTables* __restrict__ tab, const uint32_t (&seg)[N][WPR],
-                                                   int b, bool valid, uint32_t* stage, uint32_t (&zp)[N * N / 2]) {
+template <int N> using NearMask = typename std::conditional<N == 4, uint32_t, uint64_t>::type;
+
+template <int N, int WPR>
+__device__ __forceinline__ NearMask<N> quantize_block(const EncTables* __restrict__ tab, const uint32_t (&seg)[N][WPR],
+                                                      int b, uint32_t (&zp)[N * N / 2]) {
     constexpr int NN = N * N;
-    uint64_t need = 0;
-    if constexpr (!EXACT) {
-        float x[NN];
+    using Mask = NearMask<N>;
+    Mask need = 0;
+    float x[NN];
 #pragma unroll
-        for (int i = 0; i < N; i++)
+    for (int i = 0; i < N; i++)
 #pragma unroll
-            for (int j = 0; j < N; j++) x[i * N + j] = float(pix<WPR>(seg[i], b * N + j)) - 128.0f;
-        dct2d<N>(x, tab->dct, FloatOp());
-        int qv[NN];
+        for (int j = 0; j < N; j++) x[i * N + j] = float(pix<WPR>(seg[i], b * N + j)) - 128.0f;
+    dct2d<N>(x, tab->dct, FloatOp());
+    // t = D * C(u)C(v)/q; y = t + 1.5*2^23 rounds t to the nearest integer (|t| < 2^22) and leaves
+    // int16(rint(t)) in y's low 16 bits; |t - rint(t)| >= 0.5 - bound flags a possible tie.
+    constexpr float kMagic = 12582912.0f;
+    uint32_t yb[NN];
 #pragma unroll
-        for (int k = 0; k < NN; k++) {
-            const float t = x[k] * tab->g[k];
-            if (k == 0 && tab->thr[0] < 0.0f) {
-                // t is exact here (integer sum times a power of two): round half away from zero
-                qv[k] = int(truncf(t + copysignf(0.5f, t)));
-            } else {
-                const float r = rintf(t);
-                need |= uint64_t(fabsf(t - r) >= tab->lim[k]) << k;  // lim = 0.5 - bound
-                qv[k] = int(r);
-            }
+    for (int k = 0; k < NN; k++) {
+        const float t = x[k] * tab->g[k];
+        if (k == 0 && tab->thr[0] < 0.0f) {
+            // t is exact here (integer sum times a power of two): round half away from zero
+            yb[k] = uint32_t(int(truncf(t + copysignf(0.5f, t))));
+        } else {
+            const float y = t + kMagic;
+            const float r = y - kMagic;
+            need |= Mask(fabsf(t - r) >= tab->lim[k]) << k;
+            yb[k] = __float_as_uint(y);
         }
+    }
 #pragma unroll
-        for (int j = 0; j < NN / 2; j++)
-            zp[j] = (uint32_t(qv[ZigZag<N>::idx[2 * j]]) & 0xFFFFu) | (uint32_t(qv[ZigZag<N>::idx[2 * j + 1]]) << 16);
+    for (int j = 0; j < NN / 2; j++)
+        zp[j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
+    return need;
+}
+
+// Replace zig-zag coefficient kz of a packed block by v (a runtime position: a select chain over
+// the words, so the block stays in registers).
+template <int NP>
+__device__ __forceinline__ void patch(uint32_t (&zp)[NP], int kz, uint32_t v) {
+    const int wsel = kz >> 1;
+    const uint32_t lo = v & 0xFFFFu, hi = v << 16;
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const uint32_t w = zp[j];
+        const uint32_t nw = (kz & 1) ? ((w & 0xFFFFu) | hi) : ((w & 0xFFFF0000u) | lo);
+        zp[j] = (j == wsel) ? nw : w;
+    }
+}
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Zig-zag RLE sizing of one packed block (Block.cpp:186-232, :383-397), two coefficients per
+// packed-int16 instruction.  Returns bl | Lw << 8 and the record length in bits.
+template <int N>
+__device__ __forceinline__ uint32_t size_block(const uint32_t (&zp)[N * N / 2], int rle, uint32_t* bits) {
+    constexpr int NN = N * N;
+    constexpr int NP = NN / 2;
+    // nz: bit kz set iff z[kz] != 0 (min(u16, 1) per half, even kz in the low halves)
+    uint64_t nz = 0;
+    uint32_t mo = 0;  // OR of v ^ (v >> 15) per half: its bit length + 1 is the widest bits_needed
+#pragma unroll
+    for (int g = 0; g < NP / 8; g++) {
+        uint32_t M = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t w = zp[g * 8 + j];
+            const u16x2 m = __builtin_elementwise_min(__builtin_bit_cast(u16x2, w), u16x2{1, 1});
+            M |= __builtin_bit_cast(uint32_t, m) << (2 * j);
+            const s16x2 v = __builtin_bit_cast(s16x2, w);
+            mo |= __builtin_bit_cast(uint32_t, v ^ (v >> s16x2{15, 15}));
+        }
+        const uint32_t nz16 = (M & 0x5555u) | ((M >> 15) & 0xAAAAu);
+        nz |= uint64_t(nz16) << (16 * g);
+    }
+    mo = (mo | (mo >> 16)) & 0xFFFFu;
+    const int maxb = 33 - __clz(mo);  // bits_needed (utils.hpp:226-243) of the widest value
+    const int L = nz ? 64 - __clzll((long long)nz) : 0;
+    const int ffsL = L ? 32 - __clz(L) : 1;  // utils.hpp:210-216, with ffs(0) == 1
+    const int bl = max(maxb, ffsL);
+    int lw;
+    if (!rle) {
+        lw = NN;
+    } else if (L == NN && !((nz >> (NN - 2)) & 1ull)) {
+        const uint64_t m = nz & ((1ull << (NN - 1)) - 1);  // drop the last element (Block.cpp:388-390)
+        lw = m ? 64 - __clzll((long long)m) : 0;
     } else {
-        if constexpr (NN == 64) need = ~0ull;
-        else need = (1ull << NN) - 1;
-#pragma unroll
-        for (int j = 0; j < NN / 2; j++) zp[j] = 0;
+        lw = L;
     }
-    if (!valid) need = 0;
-    unsigned nf = 0;
-    if (need) {  // divergent and rare in FAST mode: the FP64 reference order for flagged k
-        BlockPx<N> px;
-#pragma unroll
-        for (int i = 0; i < N; i++)
-#pragma unroll
-            for (int m = 0; m < N / 4; m++) px.w[i * (N / 4) + m] = seg[i][(b * N) / 4 + m];
-#pragma unroll
-        for (int j = 0; j < NN / 2; j++) stage[j] = zp[j];
-        do {
-            const int k = __ffsll((unsigned long long)need) - 1;
-            need &= need - 1;
-            const uint32_t v = uint32_t(exact_coef<N>(tab, k, px)) & 0xFFFFu;
-            const int kz = ZigZagInv<N>::pos[k];
-            const uint32_t w = stage[kz >> 1];  // patch one int16 half of a word (same type: no aliasing)
-            stage[kz >> 1] = (kz & 1) ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
-            nf++;
-        } while (need);
-#pragma unroll
-        for (int j = 0; j < NN / 2; j++) zp[j] = stage[j];
-    }
-    return nf;
+    *bits = 4u + uint32_t(bl) * uint32_t(lw + rle);
+    return uint32_t(bl) | (uint32_t(lw) << 8);
 }
 
 template <int N, bool EXACT>
@@ -248,15 +286,137 @@ __global__ __launch_bounds__(kTPB, 4) void encode_kernel(EncArgs a, const EncTab
             for (int m = 0; m < WPR; m++) seg[r][m] = 0;
     }
 
-    uint32_t zp[BPT][NN / 2];  // quantised coefficients, zig-zag order, two int16 per word
-    uint32_t blw[BPT];         // bl | Lw << 8
-    uint32_t mybits = 0;
-    unsigned nfall = 0;
-    uint32_t* stage = img + tid * (NN / 2);  // private slot; the image is built after the scan
+    constexpr int NP = NN / 2;
+    using Mask = NearMask<N>;
+    uint32_t zp[BPT][NP];  // quantised coefficients, zig-zag order, two int16 per word
+    Mask need[BPT];
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
         __builtin_amdgcn_sched_barrier(0);  // one block at a time: keeps the live set small
-        nfall += quantize_block<N, WPR, EXACT>(tab, seg, b, b < nblk, stage, zp[b]);
+        if constexpr (!EXACT) {
+            if (a.ablate & 16) {
+                need[b] = 0;
+#pragma unroll
+                for (int j = 0; j < NP; j++) zp[b][j] = seg[j % N][(j / N) % WPR] & 0x00FF00FFu;
+            } else {
+                need[b] = quantize_block<N, WPR>(tab, seg, b, zp[b]);
+            }
+        } else {
+            need[b] = (NN == 64) ? ~Mask(0) : Mask((1ull << (NN & 63)) - 1);
+#pragma unroll
+            for (int j = 0; j < NP; j++) zp[b][j] = 0;
+        }
+        if (b >= nblk || (a.ablate & 1)) need[b] = 0;
+    }
+
+    // ---------------------------------------------------------------- 1b. FP64 re-evaluation
+    // Coefficients flagged as possible ties (FAST) or all coefficients (EXACT) take the
+    // reference's FP64 order.  FAST mode compacts a wave's flagged (lane, block, k) triples into
+    // an LDS task list so that one exact evaluation per lane serves up to 64 of them.
+    unsigned nfall = 0;
+    const int lane = tid & 63, wid = tid >> 6;
+    if constexpr (EXACT) {
+#pragma unroll
+        for (int b = 0; b < BPT; b++) {
+            BlockPx<N> px;
+#pragma unroll
+            for (int i = 0; i < N; i++)
+#pragma unroll
+                for (int m = 0; m < N / 4; m++) px.w[i * (N / 4) + m] = seg[i][(b * N) / 4 + m];
+            Mask nd = need[b];
+            while (nd) {
+                const int k = (N == 4) ? (__ffs(uint32_t(nd)) - 1) : (__ffsll((unsigned long long)nd) - 1);
+                nd &= nd - 1;
+                patch<NP>(zp[b], ZigZagInv<N>::pos[k], uint32_t(exact_coef<N>(tab, k, px)));
+            }
+        }
+    } else {
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int b = 0; b < BPT; b++) cnt += (N == 4) ? __popc(uint32_t(need[b])) : __popcll((unsigned long long)need[b]);
+        if (__ballot(cnt != 0)) {
+            // per-wave LDS region (the tile image is not built yet): pixels, tasks, results
+            constexpr int WAVE_WORDS = (IMGW - 4) / (kTPB / 64);
+            constexpr int PIXW = N * WPR;              // pixel words per lane (16 for both N)
+            constexpr int CAP = (WAVE_WORDS - 64 * PIXW) / 2;
+            static_assert(CAP >= 128, "LDS task list too small");
+            uint32_t* wpix = img + wid * WAVE_WORDS;
+            uint32_t* wtask = wpix + 64 * PIXW;
+            int32_t* wres = reinterpret_cast<int32_t*>(wtask + CAP);
+            const uint32_t incl = wave_incl_scan(cnt);
+            const uint32_t off = incl - cnt;
+            const uint32_t T = __shfl(incl, 63, 64);
+            nfall = cnt;
+#pragma unroll
+            for (int i = 0; i < N; i++)
+#pragma unroll
+                for (int m = 0; m < WPR; m++) wpix[lane * PIXW + i * WPR + m] = seg[i][m];
+            {
+                uint32_t o = off;
+#pragma unroll
+                for (int b = 0; b < BPT; b++) {
+                    Mask nd = need[b];
+                    while (nd) {
+                        const int k = (N == 4) ? (__ffs(uint32_t(nd)) - 1) : (__ffsll((unsigned long long)nd) - 1);
+                        nd &= nd - 1;
+                        if (o < CAP) wtask[o] = uint32_t(lane) | (uint32_t(b) << 6) | (uint32_t(k) << 8);
+                        o++;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t TT = min(T, uint32_t(CAP));
+            for (uint32_t base = 0; base < TT; base += 64) {
+                const uint32_t i = base + lane;
+                if (i < TT) {
+                    const uint32_t task = wtask[i];
+                    const int o = int(task & 63), b = int((task >> 6) & 3), k = int(task >> 8);
+                    BlockPx<N> px;
+#pragma unroll
+                    for (int r = 0; r < N; r++)
+#pragma unroll
+                        for (int m = 0; m < N / 4; m++) px.w[r * (N / 4) + m] = wpix[o * PIXW + r * WPR + (b * N) / 4 + m];
+                    wres[i] = exact_coef<N>(tab, k, px);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (cnt) {
+                uint32_t o = off;
+#pragma unroll
+                for (int b = 0; b < BPT; b++) {
+                    Mask nd = need[b];
+                    if (nd) {
+                        BlockPx<N> px;
+#pragma unroll
+                        for (int i = 0; i < N; i++)
+#pragma unroll
+                            for (int m = 0; m < N / 4; m++) px.w[i * (N / 4) + m] = seg[i][(b * N) / 4 + m];
+                        do {
+                            const int k = (N == 4) ? (__ffs(uint32_t(nd)) - 1) : (__ffsll((unsigned long long)nd) - 1);
+                            nd &= nd - 1;
+                            // tasks beyond the list capacity are evaluated by their own lane
+                            const int v = (o < CAP) ? wres[o] : exact_coef<N>(tab, k, px);
+                            patch<NP>(zp[b], ZigZagInv<N>::pos[k], uint32_t(v));
+                            o++;
+                        } while (nd);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        const unsigned wsum = unsigned(wave_sum64(nfall));  // statistics: spread counters
+        if (lane == 0 && wsum) atomicAdd(&a.err[2 + ((t * 4 + wid) & 63)], wsum);
+    }
+
+    // ---------------------------------------------------------------- 1c. zig-zag RLE sizing
+    uint32_t blw[BPT];  // bl | Lw << 8
+    uint32_t mybits = 0;
+#pragma unroll
+    for (int b = 0; b < BPT; b++) {
         if (a.coef && b < nblk) {
             int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + size_t(byi) * a.bx + bx0 + b) * NN;
 #pragma unroll
@@ -265,35 +425,11 @@ __global__ __launch_bounds__(kTPB, 4) void encode_kernel(EncArgs a, const EncTab
                 dst[k] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
             }
         }
-        // zig-zag + RLE sizing: bl = max(bits_needed over all values, ffs(L)), ffs(0) = 1
-        uint64_t nz = 0;
-        uint32_t mo = 0;
-#pragma unroll
-        for (int kz = 0; kz < NN; kz++) {
-            const int v = (kz & 1) ? (int(zp[b][kz >> 1]) >> 16) : (int(zp[b][kz >> 1] << 16) >> 16);
-            nz |= uint64_t(v != 0) << kz;
-            mo |= uint32_t(v ^ (v >> 31));
-        }
-        const int maxb = 33 - __clz(mo);  // bits_needed (utils.hpp:226-243) of the widest value
-        const int L = nz ? 64 - __clzll((long long)nz) : 0;
-        const int ffsL = L ? 32 - __clz(L) : 1;  // utils.hpp:210-216, with ffs(0) == 1
-        const int bl = max(maxb, ffsL);
-        int lw;
-        if (!a.rle) {
-            lw = NN;
-        } else if (L == NN && !((nz >> (NN - 2)) & 1ull)) {
-            const uint64_t m = nz & ((1ull << (NN - 1)) - 1);  // drop the last element (Block.cpp:388-390)
-            lw = m ? 64 - __clzll((long long)m) : 0;
-        } else {
-            lw = L;
-        }
-        blw[b] = uint32_t(bl) | (uint32_t(lw) << 8);
-        if (b < nblk) mybits += 4u + uint32_t(bl) * uint32_t(lw + a.rle);
+        uint32_t rb;
+        blw[b] = size_block<N>(zp[b], a.rle, &rb);
+        if (b < nblk) mybits += rb;
     }
-    if (!EXACT) {  // fallback statistics: one atomic per wave, spread over 64 counters
-        const unsigned wsum = unsigned(wave_sum64(nfall));
-        if ((tid & 63) == 0 && wsum) atomicAdd(&a.err[2 + ((t * 4 + (tid >> 6)) & 63)], wsum);
-    }
+    __syncthreads();  // the per-wave task areas alias the tile image
 
     // ---------------------------------------------------------------- 2. tile scan + LDS image
     uint32_t A;
@@ -301,7 +437,7 @@ __global__ __launch_bounds__(kTPB, 4) void encode_kernel(EncArgs a, const EncTab
     const uint32_t nw = (A + 31) >> 5;
     for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
     __syncthreads();
-    if (mybits) {
+    if (mybits && !(a.ablate & 2)) {
         BitSink sink(img, off);
 #pragma unroll
         for (int b = 0; b < BPT; b++) {
@@ -345,7 +481,14 @@ __global__ __launch_bounds__(kTPB, 4) void encode_kernel(EncArgs a, const EncTab
             st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | my_tail);
         }
     }
-    if (chain_pos != 0) {
+    if (chain_pos != 0 && (a.ablate & 4)) {
+        if (tid == 0) {
+            st_state(&a.st[2 * t + 1], (uint64_t(a.tag) << 56) | (uint64_t(A) & kMask56));
+            misc[5] = uint32_t(uint64_t(tif) * 110000u);
+            misc[6] = 0;
+            misc[7] = 0;
+        }
+    } else if (chain_pos != 0) {
         uint32_t ptail;
         const uint64_t excl = lookback_wg(a.st, t, chain_pos, step, a.tag, &ptail, a.err, misc + 8);
         if (tid == 0) {
@@ -369,7 +512,7 @@ __global__ __launch_bounds__(kTPB, 4) void encode_kernel(EncArgs a, const EncTab
     }
 
     // ---------------------------------------------------------------- 4. store
-    store_image(out, img, A, a.start_bit + excl, misc[7], chain_last);
+    if (!(a.ablate & 8)) store_image(out, img, A, a.start_bit + excl, misc[7], chain_last);
 }
 
 void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s) {
