@@ -74,6 +74,7 @@ def cpu_baseline(cfg, frame: np.ndarray) -> dict | None:
                                 os.path.join(ROOT, "tests", "golden", cfg["matrix"]), str(iters)],
                                env=env, capture_output=True, text=True, timeout=600)
             line = [ln for ln in r.stderr.splitlines() if ln.startswith("{")]
+            why = f"ref_harness rc={r.returncode}: {r.stderr.strip()[-200:]}"
             if r.returncode == 0 and line:
                 res = json.loads(line[-1])
                 return dict(value=round(w * h / (res["mean_ms"] * 1e3), 3), unit="Mpx/s", cores=threads,
@@ -89,7 +90,8 @@ def cpu_baseline(cfg, frame: np.ndarray) -> dict | None:
         oracle.encode_image(frame, cfg["n"], q, rle=True, huffman=cfg["huffman"])
     dt = (time.perf_counter() - t0) / iters
     return dict(value=round(w * h / (dt * 1e6), 3), unit="Mpx/s", cores=threads, kind="port",
-                sample=f"{iters} x {w}x{h} {cfg['gen']} frame, oracle restatement, {threads} threads")
+                sample=f"{iters} x {w}x{h} {cfg['gen']} frame, oracle restatement, {threads} threads",
+                reference_unavailable=locals().get("why", "oracle/_ref not built"))
 
 
 def main():

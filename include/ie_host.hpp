@@ -1,0 +1,235 @@
+// include/ie_host.hpp -- the host-side mirror of the reference's encoder/decoder interface,
+// running its block hot path on MI355X through the C-ABI of include/ie_hip.h.
+//
+// Same class names, constructor arguments, settings keys, bitstream layout and error
+// behaviour as the reference (cited per class), so the encoder/decoder CLIs drop onto it:
+//   util::BitStreamWriter/Reader  BitStream.hpp:91-171      MSB-first bit IO (header, Huffman dict)
+//   dc::ConfigReader              ConfigReader.hpp:41-75    key=value settings file
+//   dc::MatrixReader              MatrixReader.hpp:15-37    N x N quantisation matrix (N now runtime)
+//   algo::Huffman                 Huffman.hpp:109-142       byte Huffman post-pass (tree on the host)
+//   dc::ImageEncoder/ImageDecoder ImageEncoder.hpp, ImageDecoder.hpp
+//   dc::VideoEncoder/VideoDecoder VideoEncoder.hpp, VideoDecoder.hpp (gop = 1: I-frames only)
+// Every block-level operation (DCT, quantisation, RLE, bit packing, the inverse) runs on the
+// GPU; there is no CPU fallback.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ie_hip.h"
+
+namespace util {
+
+class BitStreamWriter {
+public:
+    explicit BitStreamWriter(size_t bytes = 0) : buf_(bytes, 0), pos_(0) {}
+    void put_bit(int v) { put(1, v ? 1u : 0u); }
+    void put(size_t length, uint32_t value);           // low `length` bits, MSB first
+    void flush() { pos_ = (pos_ + 7) & ~size_t(7); }  // byte-align (BitStream.cpp:54-59)
+    size_t get_position() const { return pos_; }
+    size_t get_last_byte_position() const { return (pos_ + 7) / 8; }
+    uint8_t* get_buffer() { return buf_.data(); }
+    const uint8_t* get_buffer() const { return buf_.data(); }
+    std::vector<uint8_t>& bytes() { return buf_; }
+    void set_position(size_t p) { pos_ = p; }
+
+private:
+    std::vector<uint8_t> buf_;
+    size_t pos_;
+};
+
+class BitStreamReader {
+public:
+    BitStreamReader(const uint8_t* b, size_t size) : buf_(b), size_(size), pos_(0) {}
+    uint32_t get_bit();                                // 0 past the end (BitStream.cpp:14-28)
+    uint32_t get(size_t length);
+    size_t get_position() const { return pos_; }
+    void set_position(size_t p) { pos_ = p; }
+    size_t get_size() const { return size_; }
+    size_t get_size_bits() const { return size_ * 8; }
+    const uint8_t* get_buffer() const { return buf_; }
+
+private:
+    const uint8_t* buf_;
+    size_t size_;
+    size_t pos_;
+};
+
+// Logger (Logger.hpp:12-40): stdout + an append-mode file; "" disables it.
+class Logger {
+public:
+    static void Create(const std::string& file);
+    static void Destroy();
+    static void WriteLn(const std::string& text);
+};
+
+}  // namespace util
+
+namespace dc {
+
+enum class ImageSetting : uint8_t { rawfile = 0, encfile, decfile, rle, quantfile, width, height, logfile, AMOUNT };
+enum class VideoSetting : uint8_t {
+    rawfile = 0, encfile, decfile, rle, quantfile, width, height, logfile, gop, merange, motioncompensation, AMOUNT
+};
+
+// ConfigReader.cpp:75-242 semantics: duplicate keys, missing '=', empty keys are errors; an image
+// file has exactly the 8 image keys; a video encoder file has at least the 8 encoder keys.
+class ConfigReader {
+public:
+    bool read(const std::string& fileName);
+    bool verifyForImage();
+    bool verifyForVideo(bool encoder);
+    std::string getValue(ImageSetting key) const;
+    std::string getValue(VideoSetting key) const;
+    std::string getErrorDescription() const { return err_; }
+    std::string toString() const;
+
+private:
+    std::map<std::string, std::string> kv_;
+    std::string err_;
+};
+
+// MatrixReader (MatrixReader.cpp): whitespace separated N x N uint16 values; written to the
+// stream as a 5-bit width followed by N*N values of that width.
+class MatrixReader {
+public:
+    explicit MatrixReader(int n = 4) : n_(n), m_(size_t(n) * n, 0) {}
+    bool read(const std::string& fileName);
+    void write(util::BitStreamWriter& w) const;
+    static MatrixReader fromBitstream(util::BitStreamReader& r, int n);
+    uint8_t getMaxBitLength() const;
+    const uint16_t* data() const { return m_.data(); }
+    int size() const { return n_; }
+    std::string toString() const;
+
+private:
+    int n_;
+    std::vector<uint16_t> m_;
+};
+
+}  // namespace dc
+
+namespace algo {
+
+// Huffman<uint8_t> (Huffman.cpp:233-402).  encode(): device histogram + first occurrence, the
+// tree / dictionary replayed on the host with the reference's own libstdc++ containers, device
+// re-encode.  decode(): dictionary and tree on the host, then the bit walk.
+class Huffman {
+public:
+    // Encode `n` bytes at `in` (host or device).  Returns the output bytes (host).  `ctx` runs
+    // the device stages.
+    static int encode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_t>& out);
+    // Decode a stream that starts with the Huffman flag bit.  passthrough = true: no table, the
+    // payload starts at *start_bit of `in` itself; else `out` receives the decoded bytes.
+    static bool decode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
+                       size_t& start_bit);
+};
+
+}  // namespace algo
+
+namespace dc {
+
+// Owns one device context; one per process is enough for the CLIs.
+class Device {
+public:
+    static ie_ctx* get();
+};
+
+struct EncodeOptions {
+    bool huffman = true;   // the reference's ENABLE_HUFFMAN (makefile:13)
+    int mode = IE_MODE_FAST;
+};
+
+class ImageEncoder {
+public:
+    ImageEncoder(const std::string& source_file, const std::string& dest_file, uint16_t width, uint16_t height,
+                 bool use_rle, MatrixReader& quant_m, EncodeOptions opt = EncodeOptions());
+    bool process();
+    void saveResult() const;
+    const std::vector<uint8_t>& result() const { return out_; }
+    std::string error() const { return err_; }
+
+private:
+    std::string src_, dst_;
+    uint16_t w_, h_;
+    bool rle_;
+    MatrixReader q_;
+    EncodeOptions opt_;
+    std::vector<uint8_t> raw_, out_;
+    std::string err_;
+};
+
+class ImageDecoder {
+public:
+    ImageDecoder(const std::string& source_file, const std::string& dest_file, int block_size = 4);
+    bool process();
+    void saveResult() const;
+    const std::vector<uint8_t>& result() const { return pix_; }
+    uint16_t width() const { return w_; }
+    uint16_t height() const { return h_; }
+    std::string error() const { return err_; }
+
+private:
+    std::string src_, dst_;
+    int n_;
+    uint16_t w_ = 0, h_ = 0;
+    std::vector<uint8_t> pix_;
+    std::string err_;
+};
+
+// gop = 1 video: every frame an I-frame, payloads concatenated bit-contiguously after a 210-bit
+// header (VideoEncoder.cpp:22-107, Frame.cpp:31-45).  gop > 1 needs motion estimation (P-frames),
+// which is outside this library's scope: process() then fails with an explanatory error.
+class VideoEncoder {
+public:
+    VideoEncoder(const std::string& source_file, const std::string& dest_file, uint16_t width, uint16_t height,
+                 bool use_rle, MatrixReader& quant_m, uint16_t gop, uint16_t merange,
+                 EncodeOptions opt = EncodeOptions());
+    bool process();
+    void saveResult() const;
+    const std::vector<uint8_t>& result() const { return out_; }
+    std::string error() const { return err_; }
+
+private:
+    std::string src_, dst_;
+    uint16_t w_, h_, gop_, merange_;
+    bool rle_;
+    MatrixReader q_;
+    EncodeOptions opt_;
+    std::vector<uint8_t> raw_, out_;
+    std::string err_;
+};
+
+class VideoDecoder {
+public:
+    VideoDecoder(const std::string& source_file, const std::string& dest_file, bool motioncomp, int block_size = 4);
+    bool process();
+    void saveResult() const;
+    std::string error() const { return err_; }
+
+private:
+    std::string src_, dst_;
+    int n_;
+    std::vector<uint8_t> out_;
+    std::string err_;
+};
+
+}  // namespace dc
+
+// C entry points of the host library (Python bindings, tests, bench).
+extern "C" {
+// Whole image file as the reference encoder writes it (header + blocks [+ Huffman pass]).
+// y: host or device; out: host.  Returns bytes written, < 0 on error.
+int64_t ieh_encode_image(ie_ctx* ctx, const uint8_t* y, int w, int h, const uint16_t* q, int n, int rle,
+                         int huffman, int mode, uint8_t* out, size_t cap);
+// gop=1 video file from a YUV420 buffer (frame_count = len / (1.5 w h)).
+int64_t ieh_encode_video(ie_ctx* ctx, const uint8_t* yuv, size_t len, int w, int h, const uint16_t* q, int n,
+                         int rle, int huffman, int merange, int mode, uint8_t* out, size_t cap);
+// Decode an image file (host buffer) with block size n: pixels into out (w*h bytes).
+int64_t ieh_decode_image(ie_ctx* ctx, const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap, int* w,
+                         int* h);
+// Huffman post-pass of n bytes (host or device) into out (host).  Returns output bytes.
+int64_t ieh_huffman_encode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap);
+}
