@@ -30,20 +30,27 @@ $(LIBDIR)/libie_hip.so: $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
 
-# ---- host library mirroring the reference interface + encoder/decoder CLIs
-HOSTSRC  := $(wildcard $(CSRC)/host/*.cpp)
-HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC)/host -Wall
-host: $(LIBDIR)/encoder $(LIBDIR)/decoder
+# ---- host library mirroring the reference interface (libie_host.so) + encoder/decoder CLIs
+HOSTSRC   := $(wildcard $(CSRC)/host/*.cpp)
+HOSTHDR   := $(wildcard $(CSRC)/host/*.hpp) include/ie_host.hpp include/ie_hip.h
+HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC)/host -Wall -Wextra -Wno-unused-parameter
+HOSTOBJS  := $(patsubst $(CSRC)/host/%.cpp,$(OBJDIR)/host/%.o,$(HOSTSRC))
+RPATH     := -Wl,-rpath,'$$ORIGIN'
+host: $(LIBDIR)/libie_host.so $(LIBDIR)/encoder $(LIBDIR)/encoder_nohuff $(LIBDIR)/decoder
 
-$(LIBDIR)/libie_host.a: $(HOSTSRC) $(wildcard $(CSRC)/host/*.hpp) include/ie_hip.h
-	@mkdir -p $(OBJDIR)/host $(LIBDIR)
-	for f in $(HOSTSRC); do $(CXX) $(HOSTFLAGS) -c $$f -o $(OBJDIR)/host/$$(basename $$f .cpp).o || exit 1; done
-	ar rcs $@ $(patsubst $(CSRC)/host/%.cpp,$(OBJDIR)/host/%.o,$(HOSTSRC))
+$(OBJDIR)/host/%.o: $(CSRC)/host/%.cpp $(HOSTHDR)
+	@mkdir -p $(OBJDIR)/host
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
-$(LIBDIR)/encoder: $(CSRC)/cli/main.cpp $(LIBDIR)/libie_host.a $(LIBDIR)/libie_hip.so
-	$(CXX) $(HOSTFLAGS) -DENCODER $< -L$(LIBDIR) -lie_host -lie_hip -Wl,-rpath,'$$ORIGIN' -o $@
-$(LIBDIR)/decoder: $(CSRC)/cli/main.cpp $(LIBDIR)/libie_host.a $(LIBDIR)/libie_hip.so
-	$(CXX) $(HOSTFLAGS) -DDECODER $< -L$(LIBDIR) -lie_host -lie_hip -Wl,-rpath,'$$ORIGIN' -o $@
+$(LIBDIR)/libie_host.so: $(HOSTOBJS) $(LIBDIR)/libie_hip.so
+	$(CXX) -shared $(HOSTOBJS) -L$(LIBDIR) -lie_hip $(RPATH) -o $@
+
+$(LIBDIR)/encoder: $(CSRC)/cli/main.cpp $(LIBDIR)/libie_host.so
+	$(CXX) $(HOSTFLAGS) -DENCODER -DENABLE_HUFFMAN $< -L$(LIBDIR) -lie_host -lie_hip $(RPATH) -o $@
+$(LIBDIR)/encoder_nohuff: $(CSRC)/cli/main.cpp $(LIBDIR)/libie_host.so
+	$(CXX) $(HOSTFLAGS) -DENCODER $< -L$(LIBDIR) -lie_host -lie_hip $(RPATH) -o $@
+$(LIBDIR)/decoder: $(CSRC)/cli/main.cpp $(LIBDIR)/libie_host.so
+	$(CXX) $(HOSTFLAGS) -DDECODER $< -L$(LIBDIR) -lie_host -lie_hip $(RPATH) -o $@
 
 oracle:
 	$(MAKE) -C oracle oracle

@@ -19,11 +19,13 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIBDIR, "libie_hip.so")
+HOST_LIB_PATH = os.path.join(LIBDIR, "libie_host.so")
 
 IE_OK, IE_EINVAL, IE_ECAP, IE_EHIP, IE_ENOQUANT, IE_EFORMAT, IE_EDEVICE = 0, -1, -2, -3, -4, -5, -6
 MODE_FAST, MODE_EXACT = 0, 1
 
 _lib = None
+_host = None
 
 
 class IEError(RuntimeError):
@@ -73,8 +75,38 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     if hasattr(L, "ie_decode_frames"):
         L.ie_decode_frames.argtypes = [vp, u8p, C.c_size_t, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
                                        u8p, C.c_size_t, C.c_size_t, u64p]
+    L.ie_malloc.argtypes = [vp, C.c_size_t, C.POINTER(C.c_void_p)]
+    L.ie_free.argtypes = [vp, vp]
+    L.ie_memcpy.argtypes = [vp, vp, vp, C.c_size_t]
+    L.ie_memset.argtypes = [vp, vp, C.c_int, C.c_size_t]
+    L.ie_is_device_ptr.argtypes = [vp]
     _lib = L
     return L
+
+
+def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
+    """Load libie_host.so: the file-level encoders/decoders (include/ie_host.hpp)."""
+    global _host
+    if _host is not None:
+        return _host
+    load_library()
+    if not os.path.exists(path):
+        raise IEError(IE_EHIP, f"{path} not built -- run `make host` (or __graft_entry__.build())")
+    H = C.CDLL(path)
+    vp, ip = C.c_void_p, C.POINTER(C.c_int)
+    H.ieh_encode_image.argtypes = [vp, vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp,
+                                   C.c_size_t]
+    H.ieh_encode_video.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int,
+                                   C.c_int, vp, C.c_size_t]
+    H.ieh_decode_image.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip]
+    H.ieh_decode_video.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip, ip]
+    H.ieh_huffman_encode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t]
+    H.ieh_release.argtypes = [vp]
+    H.ieh_release.restype = None
+    for f in ("ieh_encode_image", "ieh_encode_video", "ieh_decode_image", "ieh_decode_video", "ieh_huffman_encode"):
+        getattr(H, f).restype = C.c_int64
+    _host = H
+    return H
 
 
 def _ptr(a):
@@ -112,6 +144,8 @@ class Codec:
 
     def close(self):
         if getattr(self, "h", None):
+            if _host is not None:
+                _host.ieh_release(self.h)
             self.L.ie_destroy(self.h)
             self.h = None
 
@@ -183,3 +217,101 @@ class Codec:
         v = C.c_uint64(0)
         self._chk(self.L.ie_last_fallbacks(self.h, C.byref(v)))
         return int(v.value)
+
+    # ---- Huffman post-pass (Huffman.cpp:233-344) and the inverse path
+    def huffman_hist(self, data):
+        """(hist[256] uint32, first_pos[256] uint64) of the bytes in ``data`` (host or device)."""
+        hist = np.zeros(256, dtype=np.uint32)
+        first = np.zeros(256, dtype=np.uint64)
+        self._chk(self.L.ie_huffman_hist(self.h, _ptr(data), _nbytes(data), hist.ctypes.data,
+                                         first.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return hist, first
+
+    def huffman_pack(self, data, code, length, out, start_bit: int = 0) -> int:
+        code = np.ascontiguousarray(code, dtype=np.uint32)
+        length = np.ascontiguousarray(length, dtype=np.uint8)
+        end = C.c_uint64(0)
+        self._chk(self.L.ie_huffman_pack(self.h, _ptr(data), _nbytes(data), code.ctypes.data, length.ctypes.data,
+                                         _ptr(out), _nbytes(out), start_bit, C.byref(end)))
+        return int(end.value)
+
+    def bitcopy(self, data, out, start_bit: int):
+        self._chk(self.L.ie_bitcopy(self.h, _ptr(data), _nbytes(data), _ptr(out), _nbytes(out), start_bit))
+
+    def decode_frames(self, stream, w: int, h: int, out, start_bit: int = 0, nframes: int = 1, rle: bool = True,
+                      stride: int | None = None, frame_pitch: int | None = None, length: int | None = None) -> int:
+        """Decode ``nframes`` frames of block records from bit ``start_bit``; returns the end bit."""
+        stride = w if stride is None else stride
+        frame_pitch = stride * h if frame_pitch is None else frame_pitch
+        end = C.c_uint64(0)
+        n = _nbytes(stream) if length is None else length
+        self._chk(self.L.ie_decode_frames(self.h, _ptr(stream), n, start_bit, w, h, nframes, int(rle), _ptr(out),
+                                          stride, frame_pitch, C.byref(end)))
+        return int(end.value)
+
+    # ---- whole files (libie_host.so, include/ie_host.hpp)
+    def _host_chk(self, r: int) -> int:
+        if r < 0:
+            raise IEError(int(r), self.L.ie_last_error(self.h).decode())
+        return int(r)
+
+    def encode_image_file(self, y, w: int, h: int, q, n: int, rle: bool = True, huffman: bool = True,
+                          mode: int = MODE_FAST) -> bytes:
+        H = load_host_library()
+        q = np.ascontiguousarray(np.asarray(q, dtype=np.uint16).ravel())
+        cap = stream_bound(w, h, n, 1, 2048) + 64
+        out = np.zeros(cap, dtype=np.uint8)
+        r = self._host_chk(H.ieh_encode_image(self.h, _ptr(y), w, h, q.ctypes.data, n, int(rle), int(huffman), mode,
+                                              out.ctypes.data, cap))
+        return out[:r].tobytes()
+
+    def encode_video_file(self, yuv, w: int, h: int, q, n: int, rle: bool = True, huffman: bool = True,
+                          merange: int = 0, mode: int = MODE_FAST) -> bytes:
+        H = load_host_library()
+        q = np.ascontiguousarray(np.asarray(q, dtype=np.uint16).ravel())
+        frames = _nbytes(yuv) // (w * h + w * h // 2)
+        cap = stream_bound(w, h, n, max(frames, 1), 2048) + 64
+        out = np.zeros(cap, dtype=np.uint8)
+        r = self._host_chk(H.ieh_encode_video(self.h, _ptr(yuv), _nbytes(yuv), w, h, q.ctypes.data, n, int(rle),
+                                              int(huffman), merange, mode, out.ctypes.data, cap))
+        return out[:r].tobytes()
+
+    def decode_image_file(self, data: bytes, n: int):
+        """Pixels (h, w) uint8 of an encoded image file (ImageDecoder)."""
+        H = load_host_library()
+        src = np.frombuffer(data, dtype=np.uint8).copy()
+        w, h = C.c_int(0), C.c_int(0)
+        cap = 32767 * 32767
+        # size from the header first: decode into a small buffer to learn w, h
+        r = H.ieh_decode_image(self.h, src.ctypes.data, src.size, n, src.ctypes.data, 0, C.byref(w), C.byref(h))
+        if r != IE_ECAP:
+            self._host_chk(r)
+        cap = w.value * h.value
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        r = self._host_chk(H.ieh_decode_image(self.h, src.ctypes.data, src.size, n, out.ctypes.data, cap, C.byref(w),
+                                              C.byref(h)))
+        return out[:r].reshape(h.value, w.value)
+
+    def decode_video_file(self, data: bytes, n: int):
+        """Decoded YUV420 frames (Y + 0x80 UV fill), flat uint8, plus (w, h, frames)."""
+        H = load_host_library()
+        src = np.frombuffer(data, dtype=np.uint8).copy()
+        w, h, f = C.c_int(0), C.c_int(0), C.c_int(0)
+        r = H.ieh_decode_video(self.h, src.ctypes.data, src.size, n, src.ctypes.data, 0, C.byref(w), C.byref(h),
+                               C.byref(f))
+        if r != IE_ECAP:
+            self._host_chk(r)
+        cap = (w.value * h.value + w.value * h.value // 2) * f.value
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        r = self._host_chk(H.ieh_decode_video(self.h, src.ctypes.data, src.size, n, out.ctypes.data, cap, C.byref(w),
+                                              C.byref(h), C.byref(f)))
+        return out[:r], (w.value, h.value, f.value)
+
+    def huffman_encode(self, data) -> bytes:
+        """The Huffman post-pass alone (host or device input)."""
+        H = load_host_library()
+        n = _nbytes(data)
+        cap = 4 * n + 4096
+        out = np.zeros(cap, dtype=np.uint8)
+        r = self._host_chk(H.ieh_huffman_encode(self.h, _ptr(data), n, out.ctypes.data, cap))
+        return out[:r].tobytes()

@@ -1,0 +1,380 @@
+// imageencoder_amd/csrc/host/codec.cpp -- file-level encoders/decoders over the GPU codec:
+// the settings header on the host (ImageEncoder.cpp:84-94, VideoEncoder.cpp:60-73), block
+// records by ie_encode_frames straight behind it in device memory, the optional Huffman pass on
+// the device bytes, one copy of the finished file to the host.  Decoding mirrors
+// ImageProcessor(source, dest) (ImageBase.cpp:90-125) + ImageDecoder::process.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iterator>
+#include <map>
+#include <memory>
+#include <mutex>
+
+#include "host_internal.hpp"
+#include "ie_host.hpp"
+
+namespace dc {
+
+bool is_device(ie_ctx*, const void* p) { return ie_is_device_ptr(p) != 0; }
+
+struct Scratch {
+    DeviceBuffer enc, huf;
+    explicit Scratch(ie_ctx* c) : enc(c), huf(c) {}
+};
+std::mutex g_mu;
+std::map<ie_ctx*, std::unique_ptr<Scratch>> g_scratch;
+
+Scratch& scratch(ie_ctx* c) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& s = g_scratch[c];
+    if (!s) s.reset(new Scratch(c));
+    return *s;
+}
+
+namespace {
+
+bool read_file(const std::string& name, std::vector<uint8_t>& out) {
+    std::ifstream f(name, std::ios::binary);
+    if (!f) return false;
+    out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return true;
+}
+
+bool write_file(const std::string& name, const std::vector<uint8_t>& data) {
+    std::ofstream f(name, std::ios::binary | std::ios::trunc);
+    if (!f) return false;
+    f.write(reinterpret_cast<const char*>(data.data()), std::streamsize(data.size()));
+    return bool(f);
+}
+
+int block_size_from_env() {
+    const char* e = std::getenv("IE_BLOCKSIZE");
+    return (e && std::atoi(e) == 8) ? 8 : 4;
+}
+
+std::string fmt(const char* f, double a, double b = 0, double c = 0) {
+    char buf[256];
+    std::snprintf(buf, sizeof(buf), f, a, b, c);
+    return buf;
+}
+
+}  // namespace
+
+ie_ctx* Device::get() {
+    static ie_ctx* ctx = [] {
+        ie_ctx* c = nullptr;
+        const char* d = std::getenv("IE_DEVICE");
+        if (ie_create(d ? std::atoi(d) : 0, &c) != IE_OK) return static_cast<ie_ctx*>(nullptr);
+        return c;
+    }();
+    return ctx;
+}
+
+int encode_file(ie_ctx* c, const uint8_t* y, const FileParams& p, std::vector<uint8_t>& out, std::string& err) {
+    if (!c) return (err = "no GPU context", IE_EHIP);
+    int r;
+    if ((r = ie_set_quant(c, p.q, p.n))) return (err = ie_last_error(c), r);
+    // settings header (Huffman off: a leading '0' bit, ImageEncoder.cpp:84-86)
+    util::BitStreamWriter hdr(64);
+    if (!p.huffman) hdr.put_bit(0);
+    const uint16_t* qv = p.q;  // MatrixReader::write (MatrixReader.cpp:145-158)
+    int qb = 0;
+    for (int k = 0; k < p.n * p.n; k++) qb = std::max(qb, qv[k] ? 32 - __builtin_clz(uint32_t(qv[k])) : 1);
+    hdr.put(5, uint32_t(qb));
+    for (int k = 0; k < p.n * p.n; k++) hdr.put(size_t(qb), qv[k]);
+    hdr.put(1, p.rle ? 1u : 0u);
+    hdr.put(15, uint32_t(p.w));
+    hdr.put(15, uint32_t(p.h));
+    if (p.video) {
+        hdr.put(15, uint32_t(p.frames));
+        hdr.put(15, uint32_t(p.gop));
+        hdr.put(15, uint32_t(p.merange));
+    }
+    const uint64_t H = hdr.get_position();
+
+    Scratch& s = scratch(c);
+    const size_t cap = ie_stream_bound(p.w, p.h, p.n, p.frames, H);
+    if (!cap) return (err = "invalid dimensions", IE_EINVAL);
+    if ((r = s.enc.reserve(cap))) return (err = ie_last_error(c), r);
+    const size_t hb = size_t((H + 7) / 8);
+    if ((r = ie_memset(c, s.enc.p, 0, hb + 4))) return (err = ie_last_error(c), r);
+    if ((r = ie_memcpy(c, s.enc.p, hdr.get_buffer(), hb))) return (err = ie_last_error(c), r);
+    uint64_t end = 0;
+    if ((r = ie_encode_frames(c, y, p.w, p.h, size_t(p.w), p.frame_pitch, p.frames, p.rle ? 1 : 0, p.mode, s.enc.p,
+                              s.enc.cap, H, nullptr, &end)))
+        return (err = ie_last_error(c), r);
+    const size_t bytes = size_t((end + 7) / 8);
+    if (!p.huffman) {
+        out.resize(bytes);
+        if ((r = ie_memcpy(c, out.data(), s.enc.p, bytes))) return (err = ie_last_error(c), r);
+        return IE_OK;
+    }
+    const int64_t hl = algo::huffman_device(c, s.enc.p, bytes, s.huf, err);
+    if (hl < 0) return int(hl);
+    out.resize(size_t(hl));
+    if ((r = ie_memcpy(c, out.data(), s.huf.p, size_t(hl)))) return (err = ie_last_error(c), r);
+    return IE_OK;
+}
+
+// Parse a (Huffman-decoded) image or video stream header.  Returns false on a short stream.
+struct StreamHeader {
+    std::vector<uint16_t> q;
+    int rle = 0, w = 0, h = 0, frames = 1, gop = 1, merange = 0;
+    uint64_t payload_bit = 0;
+};
+
+static bool parse_header(const uint8_t* src, size_t len, size_t start, int n, bool video, StreamHeader& sh) {
+    util::BitStreamReader rd(src, len);
+    rd.set_position(start);
+    MatrixReader m = MatrixReader::fromBitstream(rd, n);  // MatrixReader.cpp:46-56
+    sh.q.assign(m.data(), m.data() + n * n);
+    sh.rle = int(rd.get(1));
+    sh.w = int(rd.get(15));
+    sh.h = int(rd.get(15));
+    if (video) {
+        sh.frames = int(rd.get(15));
+        sh.gop = int(rd.get(15));
+        sh.merange = int(rd.get(15));
+    }
+    sh.payload_bit = rd.get_position();
+    return sh.payload_bit <= uint64_t(len) * 8;
+}
+
+// Decode a file image into frames of pixels.  out_frame_pitch bytes per decoded frame.
+// Video frames come out as Y followed by w*h/2 bytes of UV fill.
+static int decode_file(ie_ctx* c, const uint8_t* enc, size_t len, int n, bool video, StreamHeader& sh,
+                       std::vector<uint8_t>& pix, std::string& err) {
+    if (!c) return (err = "no GPU context", IE_EHIP);
+    std::vector<uint8_t> dec;
+    bool pass = false;
+    size_t start = 0;
+    if (!algo::Huffman::decode(enc, len, dec, pass, start)) return (err = "malformed Huffman stream", IE_EFORMAT);
+    const uint8_t* src = pass ? enc : dec.data();
+    const size_t srclen = pass ? len : dec.size();
+    if (!parse_header(src, srclen, start, n, video, sh)) return (err = "stream shorter than its header", IE_EFORMAT);
+    if (video && sh.gop != 1)
+        return (err = "P-frames (gop > 1) are not supported: only gop = 1 streams decode", IE_EINVAL);
+    int r;
+    if ((r = ie_set_quant(c, sh.q.data(), n))) return (err = ie_last_error(c), r);
+    const size_t fbytes = size_t(sh.w) * sh.h;
+    const size_t pitch = video ? fbytes + fbytes / 2 : fbytes;
+    pix.assign(pitch * size_t(sh.frames), video ? 0x80 : 0);  // UV fill (Frame.cpp:121-124)
+    if (!fbytes || !sh.frames) return IE_OK;
+    if ((r = ie_decode_frames(c, src, srclen, sh.payload_bit, sh.w, sh.h, sh.frames, sh.rle, pix.data(), size_t(sh.w),
+                              pitch, nullptr)))
+        return (err = ie_last_error(c), r);
+    return IE_OK;
+}
+
+// ------------------------------------------------------------------------------- ImageEncoder
+ImageEncoder::ImageEncoder(const std::string& source_file, const std::string& dest_file, uint16_t width,
+                           uint16_t height, bool use_rle, MatrixReader& quant_m, EncodeOptions opt)
+    : src_(source_file), dst_(dest_file), w_(width), h_(height), rle_(use_rle), q_(quant_m), opt_(opt) {
+    if (!read_file(src_, raw_)) err_ = "Could not read file '" + src_ + "'";
+}
+
+bool ImageEncoder::process() {
+    if (!err_.empty()) return false;
+    util::Logger::WriteLn("[ImageEncoder] Processing image...");
+    const int n = q_.size();
+    if (w_ % n || h_ % n) return (err_ = "width and height must be multiples of the block size", false);
+    if (raw_.size() != size_t(w_) * h_) return (err_ = "raw file size differs from width x height", false);
+    FileParams p;
+    p.w = w_;
+    p.h = h_;
+    p.n = n;
+    p.q = q_.data();
+    p.rle = rle_;
+    p.huffman = opt_.huffman;
+    p.mode = opt_.mode;
+    if (encode_file(Device::get(), raw_.data(), p, out_, err_) != IE_OK) return false;
+    return true;
+}
+
+void ImageEncoder::saveResult() const {
+    if (!write_file(dst_, out_)) util::Logger::WriteLn("[ImageEncoder] Could not write '" + dst_ + "'");
+    util::Logger::WriteLn(fmt("[ImageProcessor] Original file size: %8.0f bytes", double(raw_.size())));
+    util::Logger::WriteLn(fmt("[ImageProcessor]        Encoded size: %8.0f bytes  => Ratio: %.2f%%",
+                              double(out_.size()), raw_.empty() ? 0.0 : 100.0 * double(out_.size()) / raw_.size()));
+    util::Logger::WriteLn("[ImageProcessor] Saved file at: " + dst_);
+}
+
+// ------------------------------------------------------------------------------- ImageDecoder
+ImageDecoder::ImageDecoder(const std::string& source_file, const std::string& dest_file, int block_size)
+    : src_(source_file), dst_(dest_file), n_(block_size ? block_size : block_size_from_env()) {}
+
+bool ImageDecoder::process() {
+    std::vector<uint8_t> enc;
+    if (!read_file(src_, enc)) return (err_ = "Could not read file '" + src_ + "'", false);
+    util::Logger::WriteLn("[ImageDecoder] Processing image...");
+    StreamHeader sh;
+    if (decode_file(Device::get(), enc.data(), enc.size(), n_, false, sh, pix_, err_) != IE_OK) return false;
+    w_ = uint16_t(sh.w);
+    h_ = uint16_t(sh.h);
+    return true;
+}
+
+void ImageDecoder::saveResult() const {
+    if (!write_file(dst_, pix_)) util::Logger::WriteLn("[ImageDecoder] Could not write '" + dst_ + "'");
+    util::Logger::WriteLn("[ImageProcessor] Saved file at: " + dst_);
+}
+
+// ------------------------------------------------------------------------------- VideoEncoder
+VideoEncoder::VideoEncoder(const std::string& source_file, const std::string& dest_file, uint16_t width,
+                           uint16_t height, bool use_rle, MatrixReader& quant_m, uint16_t gop, uint16_t merange,
+                           EncodeOptions opt)
+    : src_(source_file), dst_(dest_file), w_(width), h_(height), gop_(gop ? gop : 1), merange_(merange),
+      rle_(use_rle), q_(quant_m), opt_(opt) {
+    if (!read_file(src_, raw_)) err_ = "Could not read file '" + src_ + "'";
+}
+
+bool VideoEncoder::process() {
+    if (!err_.empty()) return false;
+    util::Logger::WriteLn("[VideoEncoder] Processing video...");
+    const int n = q_.size();
+    if (w_ % n || h_ % n) return (err_ = "width and height must be multiples of the block size", false);
+    if (gop_ != 1) return (err_ = "P-frames (gop > 1) need motion estimation, which this encoder does not provide", false);
+    const size_t pitch = size_t(w_) * h_ + size_t(w_) * h_ / 2;  // Y + UV (VideoBase.cpp:8-9)
+    const size_t frames = pitch ? raw_.size() / pitch : 0;
+    if (frames == 0 || frames > 32767) return (err_ = "frame count must be in 1..32767", false);
+    FileParams p;
+    p.w = w_;
+    p.h = h_;
+    p.n = n;
+    p.q = q_.data();
+    p.rle = rle_;
+    p.huffman = opt_.huffman;
+    p.mode = opt_.mode;
+    p.video = true;
+    p.frames = int(frames);
+    p.gop = gop_;
+    p.merange = merange_;
+    p.frame_pitch = pitch;
+    return encode_file(Device::get(), raw_.data(), p, out_, err_) == IE_OK;
+}
+
+void VideoEncoder::saveResult() const {
+    if (!write_file(dst_, out_)) util::Logger::WriteLn("[VideoEncoder] Could not write '" + dst_ + "'");
+    util::Logger::WriteLn(fmt("[VideoProcessor] Original file size: %8.0f bytes", double(raw_.size())));
+    util::Logger::WriteLn(fmt("[VideoProcessor]       Encoded size: %8.0f bytes  => Ratio: %.2f%%",
+                              double(out_.size()), raw_.empty() ? 0.0 : 100.0 * double(out_.size()) / raw_.size()));
+    util::Logger::WriteLn("[VideoProcessor] Saved file at: " + dst_);
+}
+
+// ------------------------------------------------------------------------------- VideoDecoder
+VideoDecoder::VideoDecoder(const std::string& source_file, const std::string& dest_file, bool, int block_size)
+    : src_(source_file), dst_(dest_file), n_(block_size ? block_size : block_size_from_env()) {}
+
+bool VideoDecoder::process() {
+    std::vector<uint8_t> enc;
+    if (!read_file(src_, enc)) return (err_ = "Could not read file '" + src_ + "'", false);
+    util::Logger::WriteLn("[VideoDecoder] Processing video...");
+    StreamHeader sh;
+    return decode_file(Device::get(), enc.data(), enc.size(), n_, true, sh, out_, err_) == IE_OK;
+}
+
+void VideoDecoder::saveResult() const {
+    if (!write_file(dst_, out_)) util::Logger::WriteLn("[VideoDecoder] Could not write '" + dst_ + "'");
+    util::Logger::WriteLn("[VideoProcessor] Saved file at: " + dst_);
+}
+
+}  // namespace dc
+
+// ---------------------------------------------------------------------------------- C entry
+extern "C" {
+
+int64_t ieh_encode_image(ie_ctx* c, const uint8_t* y, int w, int h, const uint16_t* q, int n, int rle, int huffman,
+                         int mode, uint8_t* out, size_t cap) {
+    if (!c || !y || !q || !out) return IE_EINVAL;
+    dc::FileParams p;
+    p.w = w;
+    p.h = h;
+    p.n = n;
+    p.q = q;
+    p.rle = rle != 0;
+    p.huffman = huffman != 0;
+    p.mode = mode;
+    std::vector<uint8_t> v;
+    std::string err;
+    const int r = dc::encode_file(c, y, p, v, err);
+    if (r) return r;
+    if (v.size() > cap) return IE_ECAP;
+    std::memcpy(out, v.data(), v.size());
+    return int64_t(v.size());
+}
+
+int64_t ieh_encode_video(ie_ctx* c, const uint8_t* yuv, size_t len, int w, int h, const uint16_t* q, int n, int rle,
+                         int huffman, int merange, int mode, uint8_t* out, size_t cap) {
+    if (!c || !yuv || !q || !out || w <= 0 || h <= 0) return IE_EINVAL;
+    dc::FileParams p;
+    p.w = w;
+    p.h = h;
+    p.n = n;
+    p.q = q;
+    p.rle = rle != 0;
+    p.huffman = huffman != 0;
+    p.mode = mode;
+    p.video = true;
+    p.frame_pitch = size_t(w) * h + size_t(w) * h / 2;
+    p.frames = int(len / p.frame_pitch);
+    p.gop = 1;
+    p.merange = merange;
+    if (p.frames <= 0 || p.frames > 32767) return IE_EINVAL;
+    std::vector<uint8_t> v;
+    std::string err;
+    const int r = dc::encode_file(c, yuv, p, v, err);
+    if (r) return r;
+    if (v.size() > cap) return IE_ECAP;
+    std::memcpy(out, v.data(), v.size());
+    return int64_t(v.size());
+}
+
+int64_t ieh_decode_image(ie_ctx* c, const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap, int* w, int* h) {
+    if (!c || !enc || !out) return IE_EINVAL;
+    dc::StreamHeader sh;
+    std::vector<uint8_t> pix;
+    std::string err;
+    const int r = dc::decode_file(c, enc, len, n, false, sh, pix, err);
+    if (w) *w = sh.w;
+    if (h) *h = sh.h;
+    if (r) return r;
+    if (pix.size() > cap) return IE_ECAP;
+    std::memcpy(out, pix.data(), pix.size());
+    return int64_t(pix.size());
+}
+
+int64_t ieh_decode_video(ie_ctx* c, const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap, int* w, int* h,
+                         int* frames) {
+    if (!c || !enc || !out) return IE_EINVAL;
+    dc::StreamHeader sh;
+    std::vector<uint8_t> pix;
+    std::string err;
+    const int r = dc::decode_file(c, enc, len, n, true, sh, pix, err);
+    if (w) *w = sh.w;
+    if (h) *h = sh.h;
+    if (frames) *frames = sh.frames;
+    if (r) return r;
+    if (pix.size() > cap) return IE_ECAP;
+    std::memcpy(out, pix.data(), pix.size());
+    return int64_t(pix.size());
+}
+
+void ieh_release(ie_ctx* c) {
+    std::lock_guard<std::mutex> lk(dc::g_mu);
+    dc::g_scratch.erase(c);
+}
+
+int64_t ieh_huffman_encode(ie_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap) {
+    if (!c || (!in && n) || !out) return IE_EINVAL;
+    std::vector<uint8_t> v;
+    const int r = algo::Huffman::encode(c, in, n, v);
+    if (r) return r;
+    if (v.size() > cap) return IE_ECAP;
+    std::memcpy(out, v.data(), v.size());
+    return int64_t(v.size());
+}
+
+}  // extern "C"

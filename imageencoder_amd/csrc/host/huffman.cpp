@@ -1,0 +1,265 @@
+// imageencoder_amd/csrc/host/huffman.cpp -- the byte Huffman post-pass, algo::Huffman<uint8_t>
+// (Huffman.cpp:233-402), with its O(bytes) stages on the GPU and only the 256-symbol tree here.
+//
+// Why the host replay is exact: the reference's output is a function of (a) the count of every
+// byte value and (b) the order in which the values were first inserted into its
+// std::unordered_map<uint8_t, uint32_t> (Huffman.cpp:237-243) -- that container's iteration
+// order depends only on the insertion sequence, and it fixes the priority-queue push order, hence
+// the tie-breaking of equal frequencies, the tree, the DFS dictionary order and (through the
+// unstable std::sort of Huffman.cpp:287) the emitted dictionary order.  ie_huffman_hist returns
+// both (a) and the first position of every value, so inserting the values in first-position
+// order into the same libstdc++ containers reproduces every step.
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <queue>
+#include <stdexcept>
+#include <unordered_map>
+#include <vector>
+
+#include "ie_host.hpp"
+#include "host_internal.hpp"
+
+namespace algo {
+namespace {
+
+struct Node {
+    uint8_t data;
+    size_t freq;
+    Node* left = nullptr;
+    Node* right = nullptr;
+    Node(uint8_t d, size_t f, Node* l = nullptr, Node* r = nullptr) : data(d), freq(f), left(l), right(r) {}
+    ~Node() {
+        delete left;
+        delete right;
+    }
+    bool leaf() const { return !left && !right; }
+};
+struct ByFreq {  // Node::comparator (Huffman.hpp:63-67): lower frequency = higher priority
+    bool operator()(const Node* a, const Node* b) const { return a->freq > b->freq; }
+};
+struct Codeword {
+    uint32_t word, len;
+};
+
+void walk(const Node* nd, std::vector<bool> path, std::unordered_map<uint8_t, Codeword>& dict) {
+    if (!nd) return;
+    if (nd->leaf()) {
+        uint32_t w = 0;
+        for (bool b : path) w = (w << 1) | uint32_t(b);
+        dict[nd->data] = Codeword{w, uint32_t(path.size())};
+        return;
+    }
+    std::vector<bool> lp(path);
+    lp.push_back(false);
+    path.push_back(true);
+    walk(nd->left, lp, dict);
+    walk(nd->right, path, dict);
+}
+
+}  // namespace
+
+// Dictionary + code table from the device histogram.  Returns the dictionary bit image in `hdr`.
+bool build_code(const uint32_t* hist, const uint64_t* first, util::BitStreamWriter& hdr, uint32_t* code,
+                uint8_t* len, uint64_t& data_bits, std::string& err) {
+    std::vector<int> order;
+    for (int b = 0; b < 256; b++)
+        if (hist[b]) order.push_back(b);
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return first[a] < first[b]; });
+    std::unordered_map<uint8_t, uint32_t> freqs;
+    for (int b : order) freqs[uint8_t(b)] = hist[b];
+
+    std::priority_queue<Node*, std::vector<Node*>, ByFreq> pq;
+    for (const auto& pr : freqs) pq.push(new Node(pr.first, pr.second));
+    while (pq.size() > 1) {
+        Node* l = pq.top();
+        pq.pop();
+        Node* r = pq.top();
+        pq.pop();
+        pq.push(new Node(uint8_t(-1), l->freq + r->freq, l, r));
+    }
+    std::unique_ptr<Node> root(pq.top());
+    std::unordered_map<uint8_t, Codeword> dict;
+    walk(root.get(), std::vector<bool>(), dict);
+
+    std::vector<std::pair<uint8_t, Codeword>> sorted(dict.begin(), dict.end());
+    std::sort(sorted.begin(), sorted.end(),
+              [](const std::pair<uint8_t, Codeword>& a, const std::pair<uint8_t, Codeword>& b) {
+                  return a.second.len > b.second.len;
+              });
+    std::unordered_map<uint32_t, uint32_t> group;
+    for (const auto& e : sorted) group[e.second.len]++;
+
+    // dictionary: groups of equal code length, {1, count:7, len:4} then {key:8, code:len}...
+    uint32_t left = 0, bl = 0;
+    for (const auto& e : sorted) {
+        if (left == 0) {
+            bl = e.second.len;
+            left = group[bl];
+            hdr.put(8, 0x80u | (left & 0x7Fu));  // Huffman.cpp:39-43 (7-bit count, 4-bit length)
+            hdr.put(4, bl & 0xFu);
+        }
+        hdr.put(8, e.first);
+        hdr.put(bl, e.second.word);
+        left--;
+    }
+    hdr.put_bit(0);  // stop bit
+
+    std::memset(code, 0, 256 * sizeof(uint32_t));
+    std::memset(len, 0, 256);
+    data_bits = 0;
+    for (const auto& e : dict) {
+        if (e.second.len > 32) {
+            err = "Huffman code longer than 32 bits";
+            return false;
+        }
+        code[e.first] = e.second.word;
+        len[e.first] = uint8_t(e.second.len);
+        data_bits += uint64_t(hist[e.first]) * e.second.len;
+    }
+    return true;
+}
+
+// Encode n device-resident bytes into the device buffer `out` (grown and zeroed as needed).
+// Returns the output length in bytes or a negative error.
+int64_t huffman_device(ie_ctx* c, const uint8_t* din, size_t n, dc::DeviceBuffer& out, std::string& err) {
+    uint32_t hist[256];
+    uint64_t first[256];
+    int r;
+    if ((r = ie_huffman_hist(c, din, n, hist, first))) return (err = ie_last_error(c), r);
+    if (n == 0) {  // the reference pops an empty queue here; emit the bare stop bit
+        if ((r = out.reserve(8)) || (r = ie_memset(c, out.p, 0, 8))) return (err = ie_last_error(c), r);
+        return 1;
+    }
+    util::BitStreamWriter hdr(64);
+    uint32_t code[256];
+    uint8_t len[256];
+    uint64_t data_bits = 0;
+    if (!build_code(hist, first, hdr, code, len, data_bits, err)) return IE_EINVAL;
+    const uint64_t dict_bits = hdr.get_position();
+    const uint64_t total = (dict_bits + data_bits + 7) / 8;
+    if (n < total) {
+        // no gain: '0' + the input bytes, n + 1 bytes (Huffman.cpp:329-341)
+        const size_t need = ie_stream_bound_bytes(1 + 8 * uint64_t(n));
+        if ((r = out.reserve(need))) return (err = ie_last_error(c), r);
+        if ((r = ie_memset(c, out.p, 0, 4))) return (err = ie_last_error(c), r);
+        if ((r = ie_bitcopy(c, din, n, out.p, out.cap, 1))) return (err = ie_last_error(c), r);
+        return int64_t(n + 1);
+    }
+    unsigned maxlen = 0;
+    for (int b = 0; b < 256; b++) maxlen = std::max<unsigned>(maxlen, len[b]);
+    const size_t need = ie_stream_bound_bytes(dict_bits + uint64_t(maxlen) * n);
+    if ((r = out.reserve(need))) return (err = ie_last_error(c), r);
+    // the packer completes the dictionary's last word from these bytes; later words it overwrites
+    const size_t hb = size_t((dict_bits + 7) / 8);
+    if ((r = ie_memset(c, out.p, 0, hb + 4))) return (err = ie_last_error(c), r);
+    if ((r = ie_memcpy(c, out.p, hdr.get_buffer(), hb))) return (err = ie_last_error(c), r);
+    uint64_t end = 0;
+    if ((r = ie_huffman_pack(c, din, n, code, len, out.p, out.cap, dict_bits, &end))) return (err = ie_last_error(c), r);
+    if (end != dict_bits + data_bits) return (err = "Huffman pack length mismatch", IE_EDEVICE);
+    return int64_t(total);
+}
+
+int Huffman::encode(ie_ctx* c, const uint8_t* in, size_t n, std::vector<uint8_t>& out) {
+    dc::DeviceBuffer src(c), dst(c);
+    std::string err;
+    int r;
+    const uint8_t* din = in;
+    if (!dc::is_device(c, in)) {
+        if ((r = src.reserve(n + 4))) return r;
+        if ((r = ie_memcpy(c, src.p, in, n))) return r;
+        din = src.p;
+    }
+    const int64_t bytes = huffman_device(c, din, n, dst, err);
+    if (bytes < 0) return int(bytes);
+    out.resize(size_t(bytes));
+    return ie_memcpy(c, out.data(), dst.p, size_t(bytes));
+}
+
+// ----------------------------------------------------------------------------------- decode
+// Huffman<uint8_t>::decode (Huffman.cpp:120-204, 354-402): the dictionary rebuilds the tree
+// leaf by leaf; no dictionary entry = passthrough (the stream continues after the stop bit).
+// The bit walk uses a 12-bit lookup table over the tree instead of one pointer hop per bit.
+bool Huffman::decode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
+                     size_t& start_bit) {
+    util::BitStreamReader rd(in, n);
+    struct T {
+        int child[2] = {-1, -1};
+        int sym = -1;
+    };
+    std::vector<T> tree(1);
+    bool any = false;
+    while (rd.get_bit()) {
+        uint32_t cnt = rd.get(7);
+        const uint32_t bl = rd.get(4);
+        while (cnt--) {
+            const uint32_t key = rd.get(8), word = rd.get(bl);
+            any = true;
+            int cur = 0;
+            // treeAddLeaf (Huffman.cpp:143-173): bl = 0 puts the leaf under the root's left edge
+            const int steps = bl ? int(bl) : 1;
+            for (int b = steps - 1; b >= 0; b--) {
+                const int dir = bl ? int((word >> b) & 1u) : 0;
+                if (tree[cur].child[dir] < 0) {
+                    tree[cur].child[dir] = int(tree.size());
+                    tree.emplace_back();
+                }
+                cur = tree[cur].child[dir];
+            }
+            tree[cur].sym = int(key);
+        }
+    }
+    if (!any) {
+        passthrough = true;
+        start_bit = rd.get_position();
+        return true;
+    }
+    passthrough = false;
+    start_bit = 0;
+    constexpr int K = 12;
+    // table[prefix of K bits] = {symbol, bits consumed} when a leaf is reached within K bits
+    std::vector<int32_t> tab(size_t(1) << K);
+    for (uint32_t p = 0; p < (1u << K); p++) {
+        int cur = 0, used = 0;
+        while (used < K && (tree[cur].child[0] >= 0 || tree[cur].child[1] >= 0)) {
+            cur = tree[cur].child[(p >> (K - 1 - used)) & 1u];
+            used++;
+            if (cur < 0) break;
+        }
+        if (cur >= 0 && tree[cur].child[0] < 0 && tree[cur].child[1] < 0)
+            tab[p] = (tree[cur].sym << 8) | used;
+        else
+            tab[p] = -1;
+    }
+    const uint64_t raw_bits = uint64_t(n) * 8;
+    out.clear();
+    out.reserve(n * 2);
+    uint64_t pos = rd.get_position();
+    auto peek = [&](uint64_t at) -> uint32_t {  // K bits from `at`, zeros past the end
+        uint32_t v = 0;
+        for (int b = 0; b < 3; b++) {
+            const uint64_t byte = (at >> 3) + uint64_t(b);
+            v = (v << 8) | (byte < n ? in[byte] : 0u);
+        }
+        return (v >> (24 - K - (at & 7))) & ((1u << K) - 1u);
+    };
+    while (pos < raw_bits) {
+        const int32_t e = tab[peek(pos)];
+        if (e >= 0) {
+            out.push_back(uint8_t(e >> 8));
+            pos += uint64_t(e & 0xFF);
+            continue;
+        }
+        int cur = 0;  // code longer than K bits (or invalid): walk the tree
+        while (tree[cur].child[0] >= 0 || tree[cur].child[1] >= 0) {
+            const uint32_t bit = pos < raw_bits ? (in[pos >> 3] >> (7 - (pos & 7))) & 1u : 0u;
+            pos++;
+            cur = tree[cur].child[bit];
+            if (cur < 0) return false;
+        }
+        out.push_back(uint8_t(tree[cur].sym));
+    }
+    return true;
+}
+
+}  // namespace algo

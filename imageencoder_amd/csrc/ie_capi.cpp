@@ -577,6 +577,7 @@ int ie_set_quant(ie_ctx* c, const uint16_t* q, int n) {
     if (n != 4 && n != 8) return fail(c, IE_EINVAL, "block size must be 4 or 8");
     for (int k = 0; k < n * n; k++)
         if (q[k] == 0) return fail(c, IE_EINVAL, "quantisation matrix entries must be > 0");
+    if (c->n == n && std::memcmp(c->q, q, sizeof(uint16_t) * n * n) == 0) return IE_OK;  // unchanged
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));  // tables may be in use by a running launch
     if (!build_tables(n, q, c->h_tab)) return fail(c, IE_EINVAL, "FP32 transform does not match the reference map");
@@ -635,6 +636,52 @@ int ie_last_fallbacks(ie_ctx* c, uint64_t* count) {
     if (r) return r;
     *count = c->last_fallbacks;
     if (timeouts) return fail(c, IE_EDEVICE, "tile look-back timed out");
+    return IE_OK;
+}
+
+int ie_is_device_ptr(const void* p) { return is_device_ptr(p) ? 1 : 0; }
+
+int ie_malloc(ie_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return IE_EINVAL;
+    *out = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMalloc(out, bytes ? bytes : 4));
+    return IE_OK;
+}
+
+int ie_free(ie_ctx* c, void* p) {
+    if (!c) return IE_EINVAL;
+    if (!p) return IE_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(p));
+    return IE_OK;
+}
+
+int ie_memcpy(ie_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c || (bytes && (!dst || !src))) return IE_EINVAL;
+    if (!bytes) return IE_OK;
+    const bool dd = is_device_ptr(dst), sd = is_device_ptr(src);
+    const hipMemcpyKind k = dd ? (sd ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
+                               : (sd ? hipMemcpyDeviceToHost : hipMemcpyHostToHost);
+    if (k == hipMemcpyHostToHost) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        std::memcpy(dst, src, bytes);
+        return IE_OK;
+    }
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, k, c->stream));
+    if (k != hipMemcpyDeviceToDevice) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return IE_OK;
+}
+
+int ie_memset(ie_ctx* c, void* dst, int value, size_t bytes) {
+    if (!c || (bytes && !dst)) return IE_EINVAL;
+    if (!bytes) return IE_OK;
+    if (!is_device_ptr(dst)) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        std::memset(dst, value, bytes);
+        return IE_OK;
+    }
+    HIPCHK(c, hipMemsetAsync(dst, value, bytes, c->stream));
     return IE_OK;
 }
 

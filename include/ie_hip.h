@@ -101,6 +101,16 @@ int ie_quantize_frames(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t strid
 /* Fallback statistics of the last FAST-mode encode: coefficients re-evaluated in FP64. */
 int ie_last_fallbacks(ie_ctx* ctx, uint64_t* count);
 
+/* ---- Device memory on the context's stream (for hosts that keep streams device-resident
+ * between stages, e.g. the host library's encode -> Huffman pipeline).  ie_memcpy infers the
+ * direction of each pointer and is asynchronous only when both are device memory. */
+int ie_malloc(ie_ctx* ctx, size_t bytes, void** out);
+int ie_free(ie_ctx* ctx, void* p);
+int ie_memcpy(ie_ctx* ctx, void* dst, const void* src, size_t bytes);
+int ie_memset(ie_ctx* ctx, void* dst, int value, size_t bytes);
+/* 1 if p is device (hipMalloc) memory, 0 otherwise. */
+int ie_is_device_ptr(const void* p);
+
 /* ---- Huffman post-pass (config 5; Huffman.cpp:233-344) ----------------------------------
  * hist[b] = occurrences of byte value b; first_pos[b] = index of its first occurrence
  * (UINT64_MAX if absent).  The first-occurrence order is the insertion order of the reference's

@@ -230,6 +230,11 @@ int64_t ieh_encode_video(ie_ctx* ctx, const uint8_t* yuv, size_t len, int w, int
 // Decode an image file (host buffer) with block size n: pixels into out (w*h bytes).
 int64_t ieh_decode_image(ie_ctx* ctx, const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap, int* w,
                          int* h);
+// Decode a gop=1 video file: frames of Y + w*h/2 bytes of 0x80 (Frame.cpp:121-124).
+int64_t ieh_decode_video(ie_ctx* ctx, const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap, int* w,
+                         int* h, int* frames);
+// Free the host library's device scratch for ctx (call before ie_destroy).
+void ieh_release(ie_ctx* ctx);
 // Huffman post-pass of n bytes (host or device) into out (host).  Returns output bytes.
 int64_t ieh_huffman_encode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap);
 }

@@ -35,3 +35,32 @@ def test_stream_bound_cpu():
     assert stream_bound(8, 8, 4, 1, 0) == ((4 * 276 + 31) // 32) * 4
     assert stream_bound(8, 8, 8, 1, 165) == ((165 + 1044 + 31) // 32) * 4
     assert stream_bound(8, 8, 5, 1, 0) == 0
+
+
+def _declared_host():
+    src = open(os.path.join(ROOT, "include", "ie_host.hpp")).read()
+    body = src[src.index('extern "C"'):]
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(ieh_\w+)\s*\(", body, flags=re.M)))
+
+
+def test_host_library_exports_every_declared_symbol():
+    import ctypes
+    from imageencoder_amd import HOST_LIB_PATH, load_library
+    assert os.path.exists(HOST_LIB_PATH), "libie_host.so not built"
+    load_library()
+    lib = ctypes.CDLL(HOST_LIB_PATH)
+    names = _declared_host()
+    assert {"ieh_encode_image", "ieh_encode_video", "ieh_decode_image", "ieh_huffman_encode"} <= set(names)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_no_oracle_in_product_libraries():
+    """The product libraries must not link or embed the CPU oracle."""
+    import subprocess
+    from imageencoder_amd import HOST_LIB_PATH, LIB_PATH
+    for p in (LIB_PATH, HOST_LIB_PATH):
+        syms = subprocess.run(["nm", "-D", p], capture_output=True, text=True).stdout
+        assert "ieo_" not in syms, p
+        deps = subprocess.run(["ldd", p], capture_output=True, text=True).stdout
+        assert "oracle" not in deps, p

@@ -1,0 +1,138 @@
+"""The encoder / decoder command lines (imageencoder_amd/csrc/cli/main.cpp) against the reference
+CLI's contract (main.cpp:20-178): settings-file checks and exit codes 1-5 (CPU, no device call
+happens before those exits), and byte-identical files on the GPU.
+"""
+import hashlib
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests import oracle_lib as O
+
+ROOT = O.ROOT
+BIN = os.path.join(ROOT, "imageencoder_amd", "lib")
+
+
+def _bin(name):
+    p = os.path.join(BIN, name)
+    if not os.path.exists(p):
+        pytest.skip(f"{name} not built (make host)")
+    return p
+
+
+def _write_conf(d, **kv):
+    p = os.path.join(d, "set.conf")
+    with open(p, "w") as f:
+        for k, v in kv.items():
+            f.write(f"{k}={v}\n")
+    return p
+
+
+def _image_conf(d, **over):
+    kv = dict(rawfile="in.raw", encfile="out.enc", decfile="out.dec", width=8, height=8, rle=1,
+              quantfile="matrix.txt", logfile="log.txt")
+    kv.update(over)
+    return _write_conf(d, **kv)
+
+
+def _run(exe, conf, cwd, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([exe, conf], cwd=cwd, capture_output=True, text=True, timeout=120, env=e)
+
+
+@pytest.fixture
+def work(tmp_path):
+    shutil.copy(os.path.join(O.GOLDEN, "matrix.txt"), tmp_path / "matrix.txt")
+    shutil.copy(os.path.join(O.GOLDEN, "matrix8_1.txt"), tmp_path / "matrix8_1.txt")
+    shutil.copy(os.path.join(O.GOLDEN, "ex0.raw"), tmp_path / "in.raw")
+    return str(tmp_path)
+
+
+# ------------------------------------------------------------------ exit codes (CPU only)
+def test_exit_1_argument_count(work):
+    r = subprocess.run([_bin("encoder")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1
+    assert "One argument" in r.stderr
+
+
+def test_exit_2_unreadable_or_malformed(work):
+    exe = _bin("encoder")
+    assert _run(exe, os.path.join(work, "missing.conf"), work).returncode == 2
+    p = os.path.join(work, "bad.conf")
+    open(p, "w").write("rawfile=a\nno equals sign\n")
+    r = _run(exe, p, work)
+    assert r.returncode == 2 and "Can't find '='" in r.stderr
+    open(p, "w").write("rawfile=a\nrawfile=b\n")
+    r = _run(exe, p, work)
+    assert r.returncode == 2 and "more than once" in r.stderr
+    open(p, "w").write("=x\n")
+    assert _run(exe, p, work).returncode == 2
+
+
+def test_exit_3_inconsistent_settings(work):
+    exe = _bin("encoder")
+    p = _write_conf(work, rawfile="in.raw", encfile="out.enc")  # neither image nor video
+    r = _run(exe, p, work)
+    assert r.returncode == 3 and "Error in settings!" in r.stderr
+    r = _run(exe, _image_conf(work, encfile="in.raw"), work)  # encfile == rawfile
+    assert r.returncode == 3
+    r = _run(_bin("decoder"), _image_conf(work, decfile="out.enc"), work)  # decfile == encfile
+    assert r.returncode == 3
+
+
+def test_exit_4_bad_matrix(work):
+    exe = _bin("encoder")
+    open(os.path.join(work, "m3.txt"), "w").write("1 2 3\n4 5 6\n7 8 9\n")
+    assert _run(exe, _image_conf(work, quantfile="m3.txt"), work).returncode == 4
+    open(os.path.join(work, "mx.txt"), "w").write("1 2 3 4\n4 5 x 6\n1 1 1 1\n1 1 1 1\n")
+    assert _run(exe, _image_conf(work, quantfile="mx.txt"), work).returncode == 4
+    assert _run(exe, _image_conf(work, quantfile="nope.txt"), work).returncode == 4
+    # an 8x8 matrix needs the 8x8 build (IE_BLOCKSIZE=8), like the reference's BlockSize
+    assert _run(exe, _image_conf(work, quantfile="matrix8_1.txt"), work).returncode == 4
+
+
+def test_exit_5_bad_number(work):
+    exe = _bin("encoder")
+    assert _run(exe, _image_conf(work, width="abc"), work).returncode == 5
+
+
+# ------------------------------------------------------------------ byte-identical files (GPU)
+CLI_CASES = [c for c in O.manifest() if c["input"]["kind"] == "asset" and "file" in c]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", CLI_CASES, ids=[c["name"] for c in CLI_CASES])
+def test_cli_encode_decode_golden(work, c):
+    shutil.copy(os.path.join(O.GOLDEN, c["input"]["file"]), os.path.join(work, "in.raw"))
+    conf = _image_conf(work, width=c["w"], height=c["h"], rle=c["rle"], quantfile=c["matrix"])
+    env = {"IE_BLOCKSIZE": str(c["n"])}
+    enc_exe = _bin("encoder" if c["huffman"] else "encoder_nohuff")
+    r = _run(enc_exe, conf, work, env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = open(os.path.join(work, "out.enc"), "rb").read()
+    assert got == O.case_expected(c), c["name"]
+    if c.get("decode"):
+        r = _run(_bin("decoder"), conf, work, env)
+        assert r.returncode == 0, r.stdout + r.stderr
+        dec = open(os.path.join(work, "out.dec"), "rb").read()
+        assert hashlib.md5(dec).hexdigest() == c["dec_md5"]
+
+
+@pytest.mark.gpu
+def test_cli_video_gop1(work):
+    c = next(c for c in O.manifest() if c["name"] == "vidU64x48x5_4x4_huff")
+    open(os.path.join(work, "in.yuv"), "wb").write(O.case_input(c))
+    conf = _write_conf(work, rawfile="in.yuv", encfile="v.enc", decfile="v.dec", width=64, height=48, rle=1,
+                       quantfile="matrix.txt", logfile="", gop=1, merange=16)
+    r = _run(_bin("encoder"), conf, work)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert open(os.path.join(work, "v.enc"), "rb").read() == O.case_expected(c)
+    conf = _write_conf(work, encfile="v.enc", decfile="v.dec", motioncompensation=0)
+    r = _run(_bin("decoder"), conf, work)
+    assert r.returncode == 0, r.stdout + r.stderr
+    dec = np.frombuffer(open(os.path.join(work, "v.dec"), "rb").read(), np.uint8)
+    assert dec.size == 5 * 64 * 48 * 3 // 2

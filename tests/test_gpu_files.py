@@ -1,0 +1,210 @@
+"""GPU parity of the whole-file path (libie_host.so over libie_hip.so): settings header, block
+records, the Huffman post-pass (device histogram + host tree replay + device re-encode) and the
+inverse path (ie_decode_frames), against the reference's golden files and the CPU oracle.
+Bit-exact is the bar for every byte and pixel.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from imageencoder_amd import MODE_EXACT, MODE_FAST, synth
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from imageencoder_amd import Codec
+    return Codec(0)
+
+
+def _md5(b: bytes) -> str:
+    return hashlib.md5(b).hexdigest()
+
+
+def _cases(pred):
+    return [c for c in O.manifest() if pred(c)]
+
+
+def _ids(cs):
+    return [c["name"] for c in cs]
+
+
+def _check(c, got: bytes):
+    assert len(got) == c["size"], (c["name"], len(got), c["size"])
+    exp = O.case_expected(c)
+    if exp is not None:
+        if got != exp:
+            a = np.frombuffer(got, np.uint8)
+            b = np.frombuffer(exp, np.uint8)
+            i = int(np.nonzero(a != b)[0][0])
+            pytest.fail(f"{c['name']}: first differing byte {i}: {a[i]:#04x} != {b[i]:#04x}")
+    else:
+        assert _md5(got) == c["md5"], c["name"]
+
+
+def _encode_case(codec, c, mode=MODE_FAST) -> bytes:
+    raw = O.case_input(c)
+    q = O.read_matrix(c["matrix"], c["n"])
+    y = np.frombuffer(raw, dtype=np.uint8)
+    if c["video"]:
+        return codec.encode_video_file(y, c["w"], c["h"], q, c["n"], rle=bool(c["rle"]), huffman=c["huffman"],
+                                       merange=16, mode=mode)
+    return codec.encode_image_file(y, c["w"], c["h"], q, c["n"], rle=bool(c["rle"]), huffman=c["huffman"],
+                                   mode=mode)
+
+
+SMALL = _cases(lambda c: c["w"] * c["h"] < 1920 * 1080)
+BIG = _cases(lambda c: c["w"] * c["h"] >= 1920 * 1080)
+
+
+@pytest.mark.parametrize("c", SMALL, ids=_ids(SMALL))
+def test_file_golden_small(codec, c):
+    """Every small golden file (image + video, Huffman on/off, RLE on/off, 4x4/8x8)."""
+    _check(c, _encode_case(codec, c))
+
+
+@pytest.mark.parametrize("c", BIG, ids=_ids(BIG))
+def test_file_golden_full_size(codec, c):
+    """4K / 1080p golden files, including the 4K Huffman file (config C5)."""
+    _check(c, _encode_case(codec, c))
+
+
+def test_file_exact_mode_matches(codec):
+    c = next(c for c in SMALL if c["name"] == "synU256_8x8_huff")
+    _check(c, _encode_case(codec, c, MODE_EXACT))
+
+
+# ---------------------------------------------------------------------------- Huffman stages
+def _byte_sets():
+    rng = np.random.default_rng(7)
+    yield "uniform", rng.integers(0, 256, 200_003, dtype=np.uint8).tobytes()
+    yield "skewed", np.minimum(rng.geometric(0.08, 150_001), 255).astype(np.uint8).tobytes()
+    yield "few", rng.choice(np.array([3, 9, 200], np.uint8), 70_001, p=[0.7, 0.2, 0.1]).tobytes()
+    yield "two", bytes([5, 6] * 50)
+    yield "tiny", bytes([1, 2, 3])
+    yield "one_byte", bytes([42])
+    yield "fib", b"".join(bytes([i]) * f for i, f in enumerate([1, 1, 2, 3, 5, 8, 13, 21, 34, 55, 89, 144]))
+    enc = O.load().encode_blocks(synth.frame("U", 512, 256), 4, O.read_matrix("matrix.txt", 4))[0]
+    yield "encoded", enc[:60_000].tobytes()
+
+
+BYTE_SETS = list(_byte_sets())
+
+
+@pytest.mark.parametrize("name,data", BYTE_SETS, ids=[n for n, _ in BYTE_SETS])
+def test_huffman_hist(codec, name, data):
+    hist, first = codec.huffman_hist(np.frombuffer(data, np.uint8).copy())
+    eh, ef = O.load().histogram(data)
+    assert np.array_equal(hist, eh)
+    assert np.array_equal(first, ef)
+
+
+@pytest.mark.parametrize("name,data", BYTE_SETS, ids=[n for n, _ in BYTE_SETS])
+def test_huffman_encode(codec, name, data):
+    got = codec.huffman_encode(np.frombuffer(data, np.uint8).copy())
+    assert got == O.load().huffman_encode(data)
+
+
+def test_huffman_encode_device_input(codec):
+    torch = pytest.importorskip("torch")
+    data = BYTE_SETS[1][1]
+    t = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).cuda()
+    assert codec.huffman_encode(t) == O.load().huffman_encode(data)
+
+
+def test_huffman_no_gain_revert(codec):
+    """Uniform bytes do not compress: '0' + the input (Huffman.cpp:329-341), n + 1 bytes."""
+    data = BYTE_SETS[0][1]
+    got = codec.huffman_encode(np.frombuffer(data, np.uint8).copy())
+    assert len(got) == len(data) + 1
+    bits = np.unpackbits(np.frombuffer(got, np.uint8))
+    assert bits[0] == 0
+    assert np.packbits(bits[1:1 + 8 * len(data)]).tobytes() == data
+
+
+@pytest.mark.parametrize("start_bit", [0, 1, 7, 8, 13, 31, 32, 45])
+def test_bitcopy(codec, start_bit):
+    rng = np.random.default_rng(start_bit)
+    data = rng.integers(0, 256, 9_999, dtype=np.uint8)
+    out = np.zeros((start_bit + 8 * data.size) // 8 + 64, np.uint8)
+    head = rng.integers(0, 256, (start_bit + 7) // 8, dtype=np.uint8)
+    hb = np.unpackbits(head)[:start_bit] if start_bit else np.zeros(0, np.uint8)
+    if start_bit:
+        out[: head.size] = np.packbits(np.concatenate([hb, np.zeros(head.size * 8 - start_bit, np.uint8)]))
+    codec.bitcopy(data, out, start_bit)
+    bits = np.unpackbits(out)
+    assert np.array_equal(bits[:start_bit], hb)
+    assert np.array_equal(bits[start_bit:start_bit + 8 * data.size], np.unpackbits(data))
+
+
+def test_huffman_pack_codes(codec):
+    """Variable-length codes up to 32 bits land MSB-first at arbitrary start bits."""
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 30_011, dtype=np.uint8)
+    length = rng.integers(0, 33, 256).astype(np.uint8)
+    code = np.array([int(rng.integers(0, 1 << int(l))) if l else 0 for l in length], np.uint64).astype(np.uint32)
+    for start in (0, 5, 77):
+        out = np.zeros(start // 8 + 4 * data.size + 64, np.uint8)
+        end = codec.huffman_pack(data, code, length, out, start)
+        ref = []
+        for b in data:
+            l = int(length[b])
+            ref.extend((int(code[b]) >> (l - 1 - k)) & 1 for k in range(l))
+        assert end == start + len(ref)
+        bits = np.unpackbits(out)
+        assert np.array_equal(bits[start:end], np.array(ref, np.uint8))
+        assert not bits[:start].any()
+
+
+# ---------------------------------------------------------------------------------- decoder
+DEC = _cases(lambda c: c.get("decode") and not c["video"])
+
+
+@pytest.mark.parametrize("c", DEC, ids=_ids(DEC))
+def test_decode_golden(codec, c):
+    """ImageDecoder parity: the reference decoder's pixels from the reference's own file."""
+    enc = O.case_expected(c)
+    if enc is None:
+        enc = _encode_case(codec, c)
+        assert _md5(enc) == c["md5"]
+    pix = codec.decode_image_file(enc, c["n"])
+    assert pix.shape == (c["h"], c["w"])
+    assert _md5(pix.tobytes()) == c["dec_md5"], c["name"]
+
+
+@pytest.mark.parametrize("n,gen", [(4, "U"), (8, "U"), (4, "M"), (8, "M")])
+@pytest.mark.parametrize("rle", [True, False])
+def test_decode_random_vs_oracle(codec, n, gen, rle):
+    y = synth.frame(gen, 328, 176, seed=1234 + n)
+    q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+    enc = codec.encode_image_file(y, 328, 176, q, n, rle=rle, huffman=False)
+    assert enc == O.load().encode_image(y, n, q, rle=rle)
+    pix = codec.decode_image_file(enc, n)
+    assert np.array_equal(pix, O.load().decode_image(enc, n))
+
+
+def test_decode_4k_roundtrip(codec):
+    """Full-size inverse path against the pinned reference decode (md5 of synM4k)."""
+    c = next(c for c in O.manifest() if c["name"] == "synM4k_4x4")
+    enc = _encode_case(codec, c)
+    assert _md5(enc) == c["md5"]
+    pix = codec.decode_image_file(enc, 4)
+    assert _md5(pix.tobytes()) == c["dec_md5"]
+
+
+def test_decode_video_gop1(codec):
+    c = next(c for c in O.manifest() if c["name"] == "vidM64x48x5_4x4_huff")
+    enc = _encode_case(codec, c)
+    _check(c, enc)
+    out, (w, h, f) = codec.decode_video_file(enc, 4)
+    assert (w, h, f) == (64, 48, 5)
+    frames = out.reshape(f, h * w * 3 // 2)
+    assert (frames[:, w * h:] == 0x80).all()
+    yuv = np.frombuffer(O.case_input(c), np.uint8).reshape(f, -1)
+    q = O.read_matrix("matrix.txt", 4)
+    for k in range(f):
+        one = O.load().encode_image(yuv[k, : w * h].reshape(h, w).copy(), 4, q)
+        assert np.array_equal(frames[k, : w * h].reshape(h, w), O.load().decode_image(one, 4))
