@@ -23,6 +23,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -70,8 +71,11 @@ def cpu_baseline(cfg, frame: np.ndarray) -> dict | None:
         with tempfile.TemporaryDirectory() as d:
             raw = os.path.join(d, "in.raw")
             frame.tofile(raw)
-            r = subprocess.run([harness, "time4", raw, str(w), str(h), "1",
-                                os.path.join(ROOT, "tests", "golden", cfg["matrix"]), str(iters)],
+            # the reference opens the matrix with std::fstream(in|out): it needs a writable copy
+            mat = os.path.join(d, cfg["matrix"])
+            shutil.copyfile(os.path.join(ROOT, "tests", "golden", cfg["matrix"]), mat)
+            os.chmod(mat, 0o644)
+            r = subprocess.run([harness, "time4", raw, str(w), str(h), "1", mat, str(iters)],
                                env=env, capture_output=True, text=True, timeout=600)
             line = [ln for ln in r.stderr.splitlines() if ln.startswith("{")]
             why = f"ref_harness rc={r.returncode}: {r.stderr.strip()[-200:]}"
@@ -94,6 +98,37 @@ def cpu_baseline(cfg, frame: np.ndarray) -> dict | None:
                 reference_unavailable=locals().get("why", "oracle/_ref not built"))
 
 
+class Timer:
+    """K timed steps bracketed by barrier + synchronize; HIP events on the encoder's stream for
+    the per-launch device time of the dominant kernel."""
+
+    def __init__(self, torch, dist, dev, stream, world):
+        self.torch, self.dist, self.dev, self.stream, self.world = torch, dist, dev, stream, world
+
+    def run(self, step, warmup, steps):
+        torch, dist = self.torch, self.dist
+        for i in range(warmup):
+            step(i)
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(self.stream)
+        for i in range(steps):
+            step(warmup + i)
+        ev1.record(self.stream)
+        torch.cuda.synchronize(self.dev)
+        wall = time.perf_counter() - t0
+        if self.world > 1:
+            dist.barrier()
+        t = torch.tensor([wall], dtype=torch.float64, device=self.dev)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), ev0.elapsed_time(ev1) / 1e3
+
+
 def main():
     global ARGS
     ARGS = args = parse()
@@ -105,7 +140,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from imageencoder_amd import MODE_EXACT, MODE_FAST, Codec, stream_bound, synth
+    from imageencoder_amd import MODE_EXACT, MODE_FAST, Codec, stream_bound, synth, write_header
+    from imageencoder_amd import dist as D
     from tests import oracle_lib as O
 
     if world > 1:
@@ -123,60 +159,130 @@ def main():
     torch.cuda.set_stream(stream)
     codec.set_stream(stream.cuda_stream)
     mode = MODE_EXACT if args.mode == "exact" else MODE_FAST
+    timer = Timer(torch, dist, dev, stream, world)
 
     # resident synthetic frames, distinct per rank (seed offset), generated on the host once
     seed = synth.DEFAULT_SEED + 1000 * rank
     frames = torch.empty((R, h, w), dtype=torch.uint8, device=dev)
     for i in range(R):
         frames[i].copy_(torch.from_numpy(synth.frame(cfg["gen"], w, h, seed + i)))
-    hdr_bits = 165 if n == 4 else 549
-    pitch = (stream_bound(w, h, n, 1, hdr_bits) + 255) // 256 * 256
     nslots = R // B
-    outs = [torch.zeros(pitch * B, dtype=torch.uint8, device=dev) for _ in range(min(nslots, 2))]
+    extra = {}
 
-    def step(i):
-        slot = i % nslots
-        y = frames[slot * B:(slot + 1) * B]
-        codec.encode_images(y, w, h, outs[i % len(outs)], out_pitch=pitch, nframes=B, start_bit=hdr_bits,
-                            mode=mode, want_sizes=False)
+    if args.workload in ("c2", "c3", "c5"):
+        hdr_bits = write_header(n, q, True, w, h, huffman=cfg["huffman"])[1]
+        pitch = (stream_bound(w, h, n, 1, hdr_bits) + 255) // 256 * 256
+        outs = [torch.zeros(pitch * B, dtype=torch.uint8, device=dev) for _ in range(min(nslots, 2))]
+        # sizes for the algorithmic byte count (deterministic per frame)
+        ends_per_slot = []
+        for slot in range(nslots):
+            ends_per_slot.append(codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, outs[0],
+                                                     out_pitch=pitch, nframes=B, start_bit=hdr_bits, mode=mode))
+        out_bytes_per_launch = sum(int(sum((int(e) - hdr_bits + 7) // 8 for e in ends))
+                                   for ends in ends_per_slot) / nslots
+        fallbacks = codec.last_fallbacks()
 
-    # sizes for the algorithmic byte count (deterministic per frame)
-    out_bytes = 0
-    for slot in range(nslots):
-        ends = codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, outs[0], out_pitch=pitch, nframes=B,
-                                   start_bit=hdr_bits, mode=mode)
-        out_bytes += int(sum((int(e) - hdr_bits + 7) // 8 for e in ends))
-    out_bytes_per_launch = out_bytes / nslots
-    in_bytes_per_launch = B * w * h
-    fallbacks = codec.last_fallbacks()
+        if not cfg["huffman"]:
+            def step(i):
+                slot = i % nslots
+                codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, outs[i % len(outs)], out_pitch=pitch,
+                                    nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False)
+        else:
+            hpitch = 2 * pitch  # >= 32-bit codes x payload bytes
+            houts = torch.zeros(hpitch * B, dtype=torch.uint8, device=dev)
+            hsizes = []
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(args.warmup + i)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    gpu_s = ev0.elapsed_time(ev1) / 1e3
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
+            def step(i):
+                slot = i % nslots
+                out = outs[i % len(outs)]
+                ends = codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, out, out_pitch=pitch,
+                                           nframes=B, start_bit=hdr_bits, mode=mode)
+                hsizes.clear()
+                for k in range(B):
+                    nb = (int(ends[k]) + 7) // 8
+                    hsizes.append(codec.huffman_encode_device(out[k * pitch:], nb,
+                                                              houts[k * hpitch:(k + 1) * hpitch]))
+        wall, gpu_s = timer.run(step, args.warmup, args.steps)
+        px_total = world * args.steps * B * w * h
+        in_bytes_per_launch = B * w * h
+        # dominant kernel alone: the block encoder's launch time on its stream
+        enc_s = gpu_s / args.steps
+        if cfg["huffman"]:
+            def enc_only(i):
+                slot = i % nslots
+                codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, outs[i % len(outs)], out_pitch=pitch,
+                                    nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False)
+            _, g2 = timer.run(enc_only, 1, args.steps)
+            enc_s = g2 / args.steps
+            extra["huffman_bytes_per_image"] = int(sum(hsizes) / max(len(hsizes), 1))
+        # one 4K frame per launch: the latency of the single-image configuration
+        one = outs[0][:pitch]
 
-    px_total = world * args.steps * B * w * h
-    value = px_total / wall_max / 1e6
-    per_launch_s = gpu_s / args.steps
+        def single(i):
+            f = i % R
+            codec.encode_images(frames[f:f + 1], w, h, one, out_pitch=pitch, nframes=1, start_bit=hdr_bits,
+                                mode=mode, want_sizes=False)
+        _, g1 = timer.run(single, 2, 4 * B)
+        extra["single_frame"] = {"us_per_frame": round(g1 / (4 * B) * 1e6, 2),
+                                 "Mpx_s": round(w * h / (g1 / (4 * B)) / 1e6, 1)}
+        workload = (f"{args.workload}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
+                    f"{' +Huffman' if cfg['huffman'] else ''}, batch of {B} independent images per step, "
+                    f"{R} distinct resident frames per GPU ({R * w * h / 2**20:.0f} MiB)")
+        parallelism = f"independent images sharded x{world} (no collective)"
+    else:  # c4: one gop=1 video stream, frames sharded over ranks, RCCL gather to rank 0
+        F = B * world
+        f0, f1 = D.frame_range(F, rank, world)
+        nloc = f1 - f0
+        hdr, hb = write_header(n, q, True, w, h, video=True, frames=F, gop=1, merange=16)
+        root_cap = stream_bound(w, h, n, F, hb) + 64
+        out_root = torch.zeros(root_cap if rank == 0 else 8, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            out_root[:hdr.size].copy_(torch.from_numpy(hdr))
+        seg_cap = stream_bound(w, h, n, max(nloc, 1), 0) + 64
+        seg = torch.zeros(seg_cap, dtype=torch.uint8, device=dev)
+        shifted = torch.zeros(seg_cap + 8, dtype=torch.uint8, device=dev)
+
+        def shift(src, nbytes, start):
+            shifted[:8].zero_()
+            codec.bitcopy(src[:nbytes], shifted, start)
+            return shifted
+
+        def new_bytes(k):
+            return torch.zeros(k, dtype=torch.uint8, device=dev)
+
+        stats = {}
+
+        def encode_local(i):
+            slot = (i * nloc) % max(R - nloc + 1, 1)
+            y = frames[slot:slot + nloc]
+            if rank == 0:
+                _, end = codec.encode_frames(y, w, h, out_root, start_bit=hb, nframes=nloc, mode=mode)
+                return None, end - hb
+            _, end = codec.encode_frames(y, w, h, seg, start_bit=0, nframes=nloc, mode=mode)
+            return seg, end
+
+        def step(i):
+            sg, bits = encode_local(i)
+            stats["total_bits"] = D.gather_stream(dist, rank, world, sg, bits, hb, out_root, shift, new_bytes) \
+                if world > 1 else hb + bits
+
+        wall, gpu_s = timer.run(step, args.warmup, args.steps)
+        wall_enc, gpu_enc = timer.run(lambda i: encode_local(i), 1, args.steps)
+        px_total = world * args.steps * nloc * w * h
+        extra["encode_only_Mpx_s"] = round(px_total / wall_enc / 1e6, 2)
+        extra["stream_bytes"] = (stats["total_bits"] + 7) // 8
+        in_bytes_per_launch = nloc * w * h
+        out_bytes_per_launch = extra["stream_bytes"] / world
+        enc_s = gpu_enc / args.steps
+        fallbacks = codec.last_fallbacks()
+        B = nloc
+        workload = (f"c4: {F} x {w}x{h} gop=1 video ({nloc} frames per GPU), {n}x{n} {cfg['matrix']} RLE, "
+                    f"ONE stream assembled on rank 0 (all_gather of sizes + bit re-shift + P2P gather)")
+        parallelism = f"frame-sharded x{world} + RCCL gather"
+
+    value = px_total / wall / 1e6
     alg_bytes = in_bytes_per_launch + out_bytes_per_launch
-    achieved = alg_bytes / per_launch_s / 1e9
+    achieved = alg_bytes / enc_s / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -194,18 +300,14 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8->f32 (f64 near-tie re-evaluation)",
+            "dtype": "f32",
             "data": "synthetic (splitmix64 uniform 8-bit frames, seeded per rank)",
-            "config": {
-                "workload": f"{args.workload}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
-                            f"{' +Huffman' if cfg['huffman'] else ''}, batch of {B} independent images per step, "
-                            f"{R} distinct resident frames per GPU ({R * w * h / 2**20:.0f} MiB)",
-                "block": n, "batch_frames": B, "mode": args.mode, "parallelism": f"frame-sharded x{world}",
-            },
+            "config": {"workload": workload, "block": n, "frames_per_step_per_gpu": B, "mode": args.mode,
+                       "parallelism": parallelism},
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -215,11 +317,14 @@ def main():
                 "traffic": traffic,
                 "kernel": "encode_kernel",
                 "alg_bytes_per_launch": int(alg_bytes),
-                "launch_us": round(per_launch_s * 1e6, 2),
+                "launch_us": round(enc_s * 1e6, 2),
+                "read_only_frac": round(in_bytes_per_launch / enc_s / 1e9 / HBM_PEAK_GBS, 4),
             },
             "cpu_baseline": cpu,
             "fallback_coefs_per_launch": fallbacks,
+            "arith": "FP32 separable DCT + FP64 re-evaluation of near-tie coefficients (bit-exact)",
         }
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -101,6 +101,11 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
     H.ieh_decode_image.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip]
     H.ieh_decode_video.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip, ip]
     H.ieh_huffman_encode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t]
+    H.ieh_write_header.argtypes = [vp, C.c_size_t, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                   C.c_int, C.c_int, C.c_int]
+    H.ieh_write_header.restype = C.c_int64
+    H.ieh_huffman_encode_device.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t]
+    H.ieh_huffman_encode_device.restype = C.c_int64
     H.ieh_release.argtypes = [vp]
     H.ieh_release.restype = None
     for f in ("ieh_encode_image", "ieh_encode_video", "ieh_decode_image", "ieh_decode_video", "ieh_huffman_encode"):
@@ -122,6 +127,19 @@ def _nbytes(a) -> int:
     if isinstance(a, np.ndarray):
         return a.nbytes
     return a.numel() * a.element_size()
+
+
+def write_header(n: int, q, rle: bool, w: int, h: int, huffman: bool = False, video: bool = False,
+                 frames: int = 0, gop: int = 1, merange: int = 0):
+    """Settings header bytes + bit length (host library; ImageEncoder.cpp:84-94, VideoEncoder.cpp:60-73)."""
+    H = load_host_library()
+    q = np.ascontiguousarray(np.asarray(q, dtype=np.uint16).ravel())
+    out = np.zeros(256, dtype=np.uint8)
+    bits = H.ieh_write_header(out.ctypes.data, out.size, n, q.ctypes.data, int(rle), w, h, int(huffman),
+                              int(video), frames, gop, merange)
+    if bits < 0:
+        raise IEError(int(bits), "ieh_write_header")
+    return out[: (bits + 7) // 8].copy(), int(bits)
 
 
 def stream_bound(w: int, h: int, n: int, nframes: int = 1, start_bit: int = 0) -> int:
@@ -306,6 +324,11 @@ class Codec:
         r = self._host_chk(H.ieh_decode_video(self.h, src.ctypes.data, src.size, n, out.ctypes.data, cap, C.byref(w),
                                               C.byref(h), C.byref(f)))
         return out[:r], (w.value, h.value, f.value)
+
+    def huffman_encode_device(self, data, nbytes: int, out) -> int:
+        """Huffman pass from device ``data[:nbytes]`` into device ``out``; returns output bytes."""
+        H = load_host_library()
+        return self._host_chk(H.ieh_huffman_encode_device(self.h, _ptr(data), nbytes, _ptr(out), _nbytes(out)))
 
     def huffman_encode(self, data) -> bytes:
         """The Huffman post-pass alone (host or device input)."""

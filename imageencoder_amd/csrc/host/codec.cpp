@@ -73,26 +73,30 @@ ie_ctx* Device::get() {
     return ctx;
 }
 
-int encode_file(ie_ctx* c, const uint8_t* y, const FileParams& p, std::vector<uint8_t>& out, std::string& err) {
-    if (!c) return (err = "no GPU context", IE_EHIP);
-    int r;
-    if ((r = ie_set_quant(c, p.q, p.n))) return (err = ie_last_error(c), r);
+void write_header(util::BitStreamWriter& hdr, const FileParams& p) {
     // settings header (Huffman off: a leading '0' bit, ImageEncoder.cpp:84-86)
-    util::BitStreamWriter hdr(64);
     if (!p.huffman) hdr.put_bit(0);
     const uint16_t* qv = p.q;  // MatrixReader::write (MatrixReader.cpp:145-158)
     int qb = 0;
     for (int k = 0; k < p.n * p.n; k++) qb = std::max(qb, qv[k] ? 32 - __builtin_clz(uint32_t(qv[k])) : 1);
     hdr.put(5, uint32_t(qb));
     for (int k = 0; k < p.n * p.n; k++) hdr.put(size_t(qb), qv[k]);
-    hdr.put(1, p.rle ? 1u : 0u);
+    hdr.put(1, p.rle ? 1u : 0u);  // ImageEncoder.cpp:92-94
     hdr.put(15, uint32_t(p.w));
     hdr.put(15, uint32_t(p.h));
-    if (p.video) {
+    if (p.video) {  // VideoEncoder.cpp:71-73
         hdr.put(15, uint32_t(p.frames));
         hdr.put(15, uint32_t(p.gop));
         hdr.put(15, uint32_t(p.merange));
     }
+}
+
+int encode_file(ie_ctx* c, const uint8_t* y, const FileParams& p, std::vector<uint8_t>& out, std::string& err) {
+    if (!c) return (err = "no GPU context", IE_EHIP);
+    int r;
+    if ((r = ie_set_quant(c, p.q, p.n))) return (err = ie_last_error(c), r);
+    util::BitStreamWriter hdr(64);
+    write_header(hdr, p);
     const uint64_t H = hdr.get_position();
 
     Scratch& s = scratch(c);
@@ -286,6 +290,29 @@ void VideoDecoder::saveResult() const {
 // ---------------------------------------------------------------------------------- C entry
 extern "C" {
 
+int64_t ieh_write_header(uint8_t* out, size_t cap, int n, const uint16_t* q, int rle, int w, int h, int huffman,
+                         int video, int frames, int gop, int merange) {
+    if (!out || !q || (n != 4 && n != 8)) return IE_EINVAL;
+    dc::FileParams p;
+    p.w = w;
+    p.h = h;
+    p.n = n;
+    p.q = q;
+    p.rle = rle != 0;
+    p.huffman = huffman != 0;
+    p.video = video != 0;
+    p.frames = frames;
+    p.gop = gop;
+    p.merange = merange;
+    util::BitStreamWriter hdr(64);
+    dc::write_header(hdr, p);
+    const size_t bytes = hdr.get_last_byte_position();
+    if (bytes > cap) return IE_ECAP;
+    std::memset(out, 0, cap);
+    std::memcpy(out, hdr.get_buffer(), bytes);
+    return int64_t(hdr.get_position());
+}
+
 int64_t ieh_encode_image(ie_ctx* c, const uint8_t* y, int w, int h, const uint16_t* q, int n, int rle, int huffman,
                          int mode, uint8_t* out, size_t cap) {
     if (!c || !y || !q || !out) return IE_EINVAL;
@@ -360,6 +387,14 @@ int64_t ieh_decode_video(ie_ctx* c, const uint8_t* enc, size_t len, int n, uint8
     if (pix.size() > cap) return IE_ECAP;
     std::memcpy(out, pix.data(), pix.size());
     return int64_t(pix.size());
+}
+
+int64_t ieh_huffman_encode_device(ie_ctx* c, const uint8_t* din, size_t n, uint8_t* dout, size_t cap) {
+    if (!c || (!din && n) || !dout) return IE_EINVAL;
+    if ((n && !dc::is_device(c, din)) || !dc::is_device(c, dout)) return IE_EINVAL;
+    dc::DeviceBuffer out(c, dout, cap);
+    std::string err;
+    return algo::huffman_device(c, din, n, out, err);
 }
 
 void ieh_release(ie_ctx* c) {

@@ -19,14 +19,18 @@ struct DeviceBuffer {
     ie_ctx* c;
     uint8_t* p = nullptr;
     size_t cap = 0;
+    bool owned = true;
     explicit DeviceBuffer(ie_ctx* ctx) : c(ctx) {}
+    // a caller's device buffer: never reallocated or freed
+    DeviceBuffer(ie_ctx* ctx, uint8_t* ext, size_t n) : c(ctx), p(ext), cap(n), owned(false) {}
     DeviceBuffer(const DeviceBuffer&) = delete;
     DeviceBuffer& operator=(const DeviceBuffer&) = delete;
     ~DeviceBuffer() {
-        if (p) ie_free(c, p);
+        if (p && owned) ie_free(c, p);
     }
     int reserve(size_t n) {
         if (n <= cap && p) return IE_OK;
+        if (!owned) return IE_ECAP;
         if (p) ie_free(c, p);
         p = nullptr;
         cap = 0;
@@ -59,6 +63,7 @@ struct FileParams {
     int frames = 1, gop = 1, merange = 0;
     size_t frame_pitch = 0;
 };
+void write_header(util::BitStreamWriter& hdr, const FileParams& p);
 // Encode into `out` (host).  y may be host or device memory.  Returns IE_OK or an IE_E* code
 // with the reason in `err`.
 int encode_file(ie_ctx* c, const uint8_t* y, const FileParams& p, std::vector<uint8_t>& out, std::string& err);

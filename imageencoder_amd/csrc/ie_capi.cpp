@@ -779,7 +779,12 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     HIPCHK(c, hipMemcpyAsync(&end, c->d_misc, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
-    if (!out_dev) HIPCHK(c, hipMemcpy(out, dpix, pix_bytes, hipMemcpyDeviceToHost));
+    if (!out_dev) {
+        // copy only the pixel rows: bytes between rows / frames belong to the caller
+        for (int f = 0; f < nframes; f++)
+            HIPCHK(c, hipMemcpy2D(out + size_t(f) * frame_pitch, stride, dpix + size_t(f) * frame_pitch, stride,
+                                  size_t(w), size_t(h), hipMemcpyDeviceToHost));
+    }
     if (end_bit) *end_bit = end;
     return IE_OK;
 }

@@ -220,6 +220,10 @@ private:
 
 // C entry points of the host library (Python bindings, tests, bench).
 extern "C" {
+// The settings header alone (ImageEncoder.cpp:84-94; video adds frame_count, gop, merange,
+// VideoEncoder.cpp:60-73) into out (host, zeroed by this call).  Returns its length in BITS.
+int64_t ieh_write_header(uint8_t* out, size_t cap, int n, const uint16_t* q, int rle, int w, int h, int huffman,
+                         int video, int frames, int gop, int merange);
 // Whole image file as the reference encoder writes it (header + blocks [+ Huffman pass]).
 // y: host or device; out: host.  Returns bytes written, < 0 on error.
 int64_t ieh_encode_image(ie_ctx* ctx, const uint8_t* y, int w, int h, const uint16_t* q, int n, int rle,
@@ -233,6 +237,9 @@ int64_t ieh_decode_image(ie_ctx* ctx, const uint8_t* enc, size_t len, int n, uin
 // Decode a gop=1 video file: frames of Y + w*h/2 bytes of 0x80 (Frame.cpp:121-124).
 int64_t ieh_decode_video(ie_ctx* ctx, const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap, int* w,
                          int* h, int* frames);
+// Huffman post-pass entirely between device buffers (in, out device memory; out needs
+// ~n + 4 KiB).  Returns output bytes; only the 256-entry histogram and code table cross PCIe.
+int64_t ieh_huffman_encode_device(ie_ctx* ctx, const uint8_t* din, size_t n, uint8_t* dout, size_t cap);
 // Free the host library's device scratch for ctx (call before ie_destroy).
 void ieh_release(ie_ctx* ctx);
 // Huffman post-pass of n bytes (host or device) into out (host).  Returns output bytes.

@@ -4,7 +4,6 @@ happens before those exits), and byte-identical files on the GPU.
 """
 import hashlib
 import os
-import shutil
 import subprocess
 
 import numpy as np
@@ -44,11 +43,17 @@ def _run(exe, conf, cwd, env=None):
     return subprocess.run([exe, conf], cwd=cwd, capture_output=True, text=True, timeout=120, env=e)
 
 
+def _put(src, dst):
+    """Copy contents only (the repo files may be read-only; the copies must stay writable)."""
+    with open(src, "rb") as f, open(dst, "wb") as g:
+        g.write(f.read())
+
+
 @pytest.fixture
 def work(tmp_path):
-    shutil.copy(os.path.join(O.GOLDEN, "matrix.txt"), tmp_path / "matrix.txt")
-    shutil.copy(os.path.join(O.GOLDEN, "matrix8_1.txt"), tmp_path / "matrix8_1.txt")
-    shutil.copy(os.path.join(O.GOLDEN, "ex0.raw"), tmp_path / "in.raw")
+    for m in ("matrix.txt", "matrix4_2.txt", "matrix8_1.txt", "matrix8_2.txt"):
+        _put(os.path.join(O.GOLDEN, m), tmp_path / m)
+    _put(os.path.join(O.GOLDEN, "ex0.raw"), tmp_path / "in.raw")
     return str(tmp_path)
 
 
@@ -107,7 +112,7 @@ CLI_CASES = [c for c in O.manifest() if c["input"]["kind"] == "asset" and "file"
 @pytest.mark.gpu
 @pytest.mark.parametrize("c", CLI_CASES, ids=[c["name"] for c in CLI_CASES])
 def test_cli_encode_decode_golden(work, c):
-    shutil.copy(os.path.join(O.GOLDEN, c["input"]["file"]), os.path.join(work, "in.raw"))
+    _put(os.path.join(O.GOLDEN, c["input"]["file"]), os.path.join(work, "in.raw"))
     conf = _image_conf(work, width=c["w"], height=c["h"], rle=c["rle"], quantfile=c["matrix"])
     env = {"IE_BLOCKSIZE": str(c["n"])}
     enc_exe = _bin("encoder" if c["huffman"] else "encoder_nohuff")

@@ -1,0 +1,109 @@
+"""Multi-rank stream assembly (imageencoder_amd/dist.py) on CPU with gloo: frame-sharded gop=1
+video encode, all_gather of segment sizes, per-rank bit re-shift, point-to-point gather to rank 0.
+The per-rank encode here is the CPU oracle (test infrastructure); the protocol under test is the
+product's.  The assembled stream must equal the single-process reference stream byte for byte.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from imageencoder_amd import dist as D
+from imageencoder_amd import synth, write_header
+from tests import oracle_lib as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, w, h, nframes, gen, n, rle, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+        ys = synth.frames(gen, w, h, nframes, seed=77)
+        f0, f1 = D.frame_range(nframes, rank, world)
+        hdr, hb = write_header(n, q, rle, w, h, video=True, frames=nframes, gop=1, merange=16)
+        oracle = O.load()
+        cap = (hb + 7) // 8 + nframes * (w * h * 17 // 8 + w * h // (n * n)) + 64
+        out_root = torch.zeros(cap, dtype=torch.uint8)
+        seg, seg_bits = None, 0
+        if f1 > f0:
+            if rank == 0:
+                buf = np.zeros(cap, np.uint8)
+                buf[:hdr.size] = hdr
+                _, end, _ = oracle.encode_blocks(ys[f0:f1], n, q, rle=rle, start_bit=hb, out=buf)
+                out_root = torch.from_numpy(buf)
+                seg_bits = end - hb
+            else:
+                buf, end, _ = oracle.encode_blocks(ys[f0:f1], n, q, rle=rle, start_bit=0)
+                seg, seg_bits = torch.from_numpy(buf), end
+        elif rank == 0:
+            out_root[:hdr.size] = torch.from_numpy(hdr)
+
+        def shift(src, nbytes, start):
+            return torch.from_numpy(D.numpy_shift(src.numpy(), nbytes, start))
+
+        total = D.gather_stream(dist, rank, world, seg, seg_bits, hb, out_root, shift,
+                                lambda k: torch.zeros(k, dtype=torch.uint8))
+        if rank == 0:
+            result_q.put((total, out_root[: (total + 7) // 8].numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, w, h, nframes, gen, n=4, rle=True):
+    ctx = mp.get_context("spawn")
+    qres = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, nframes, gen, n, rle, qres))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    total, got = qres.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ys = synth.frames(gen, w, h, nframes, seed=77)
+    q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+    ref = O.load().encode_video(synth.yuv420(ys), w, h, n, q, rle=rle, huffman=False, merange=16)
+    return total, got, ref
+
+
+@pytest.mark.parametrize("world,nframes,gen", [(2, 5, "U"), (2, 4, "M"), (3, 7, "M")])
+def test_sharded_video_stream_matches_reference(world, nframes, gen):
+    total, got, ref = _run(world, 64, 48, nframes, gen)
+    assert got == ref
+    assert (total + 7) // 8 == len(ref)
+
+
+def test_sharded_more_ranks_than_frames():
+    """Ranks with no frames contribute empty segments."""
+    total, got, ref = _run(3, 32, 16, 2, "U")
+    assert got == ref
+
+
+def test_segment_starts_and_ranges():
+    assert D.segment_starts(210, [5, 0, 11]) == [210, 215, 215, 226]
+    rs = [D.frame_range(512, r, 8) for r in range(8)]
+    assert rs[0] == (0, 64) and rs[-1] == (448, 512)
+    assert sum(b - a for a, b in rs) == 512
+
+
+@pytest.mark.parametrize("start", range(8))
+def test_numpy_shift(start):
+    rng = np.random.default_rng(start)
+    src = rng.integers(0, 256, 37, dtype=np.uint8)
+    out = D.numpy_shift(src, 37, start)
+    bits = np.unpackbits(out)
+    assert not bits[:start].any()
+    assert np.array_equal(bits[start:start + 37 * 8], np.unpackbits(src))
