@@ -34,11 +34,13 @@ class IEError(RuntimeError):
         self.code = code
 
 
-def load_library(path: str = LIB_PATH) -> C.CDLL:
-    """Load libie_hip.so (raises if absent: the HIP path is the only path)."""
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load libie_hip.so (raises if absent: the HIP path is the only path).  IE_LIB overrides
+    the path (kernel variants built by tools/variants.sh)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("IE_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise IEError(IE_EHIP, f"{path} not built -- run `make lib` (or __graft_entry__.build())")
     # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so (same SONAME as

@@ -26,7 +26,7 @@ struct ie_ctx {
     ie::EncTables* d_tab = nullptr;
 
     // decoupled look-back state
-    uint64_t* d_state = nullptr;  // [2 * cap_tiles]
+    uint64_t* d_state = nullptr;  // [3 * cap_tiles] tile chain granules (ie_common.cuh)
     size_t cap_tiles = 0;
     uint32_t tag = 0;
     unsigned long long* d_ticket = nullptr;
@@ -112,12 +112,15 @@ int ensure(ie_ctx* c, T*& p, size_t& cap, size_t need_elems) {
 
 
 // ---- rigorous error bound of the FP32 fast path -----------------------------------------
-// Trk = an exact real linear form of the block's pixels x (|x| <= 128) plus a bound E on the
-// FP32 rounding error accumulated so far.  TrkOp mirrors every operation of ie_dct.h: the real
-// coefficients follow the FP32 constants exactly; each rounded operation adds u*|result| with
-// |result| <= 128*sum|coef| + E.  Sums/differences of integers below 2^24 round exactly (integ).
+// Trk = an exact real affine form c0 + sum_k a_k x_k of the block's RAW pixels x_k in [0, 255]
+// plus a bound E on the FP32 rounding error accumulated so far.  TrkOp mirrors every operation
+// of the quotient transforms in ie_dct.h: the real coefficients follow the FP32 constants
+// exactly; each rounded operation adds u*(|result| + E) with |result| <= |c0 + 127.5 sum a| +
+// 127.5 sum|a| (the box bound).  Results that are integers below 2^24 are exact (integ), and so
+// is a product of an exact value by a power of two.
 struct Trk {
     double a[64];
+    double c0;
     double E;
     bool integ;
 };
@@ -126,46 +129,62 @@ struct TrkOp {
     int nn;
     static constexpr double u = 1.0 / 16777216.0;  // 2^-24
     double mag(const Trk& t) const {
-        double m = 0;
-        for (int k = 0; k < nn; k++) m += std::fabs(t.a[k]);
-        return 128.0 * m;
+        double s = 0, m = 0;
+        for (int k = 0; k < nn; k++) {
+            s += t.a[k];
+            m += std::fabs(t.a[k]);
+        }
+        return std::fabs(t.c0 + 127.5 * s) + 127.5 * m;
     }
     static bool is_int(double c) { return c == std::rint(c); }
-    Trk lin(const Trk& x, double cx, const Trk* y, double cy, double Ein, bool integ) const {
+    static bool is_pow2(double c) {
+        int e = 0;
+        return c != 0.0 && std::fabs(std::frexp(c, &e)) == 0.5;
+    }
+    Trk lin(const Trk& x, double cx, const Trk* y, double cy, double cadd, double Ein, bool integ, bool exact) const {
         Trk r;
         for (int k = 0; k < nn; k++) r.a[k] = cx * x.a[k] + (y ? cy * y->a[k] : 0.0);
         for (int k = nn; k < 64; k++) r.a[k] = 0.0;
+        r.c0 = cx * x.c0 + (y ? cy * y->c0 : 0.0) + cadd;
         const double m = mag(r);
         r.integ = integ && m < 16777216.0;
-        r.E = Ein + (r.integ ? 0.0 : u * (m + Ein));
+        r.E = Ein + ((r.integ || exact) ? 0.0 : u * (m + Ein));
         return r;
     }
-    Trk add(const Trk& x, const Trk& y) const { return lin(x, 1, &y, 1, x.E + y.E, x.integ && y.integ); }
-    Trk sub(const Trk& x, const Trk& y) const { return lin(x, 1, &y, -1, x.E + y.E, x.integ && y.integ); }
+    Trk add(const Trk& x, const Trk& y) const { return lin(x, 1, &y, 1, 0, x.E + y.E, x.integ && y.integ, false); }
+    Trk sub(const Trk& x, const Trk& y) const { return lin(x, 1, &y, -1, 0, x.E + y.E, x.integ && y.integ, false); }
     Trk mul(const Trk& x, float c) const {
-        return lin(x, double(c), nullptr, 0, std::fabs(double(c)) * x.E, x.integ && is_int(c));
+        const bool exact = x.E == 0.0 && is_pow2(double(c));
+        return lin(x, double(c), nullptr, 0, 0, std::fabs(double(c)) * x.E, x.integ && is_int(c), exact);
     }
     Trk fma(const Trk& x, float c, const Trk& y) const {
-        return lin(x, double(c), &y, 1, std::fabs(double(c)) * x.E + y.E, x.integ && y.integ && is_int(c));
+        return lin(x, double(c), &y, 1, 0, std::fabs(double(c)) * x.E + y.E, x.integ && y.integ && is_int(c), false);
     }
+    Trk fms(const Trk& x, float c, const Trk& y) const {
+        return lin(x, double(c), &y, -1, 0, std::fabs(double(c)) * x.E + y.E, x.integ && y.integ && is_int(c), false);
+    }
+    Trk addc(const Trk& x, float c) const { return lin(x, 1, nullptr, 0, double(c), x.E, x.integ && is_int(c), false); }
 };
 
 inline double Cf(int i) { return i == 0 ? 0.5 : M_SQRT1_2; }  // algo.cpp:294-297
 
 // Build the per-matrix tables.  The cos values are the reference's own expression evaluated with
 // the host libm (algo.cpp:312,318-319); P, S and R are the double products it forms.  For the
-// FP32 path, the tracked run of dct2d gives per coefficient k the real linear map alpha_k the
-// FP32 code implements and its rounding bound E_k; with alpha*_k the reference's map
-// (S*P/q) the FP32 quotient is within
-//     thr_k = 2 * ( E_k + 128 * sum|alpha_k - alpha*_k| + 1e-9 )
-// of the reference's FP64 quotient (1e-9 covers the reference's own FP64 rounding, <= 1e-10).
-// Returns false if alpha deviates from alpha* beyond FP32 constant rounding (a butterfly bug).
+// FP32 path, the tracked run of the kernel's quotient transform (quot4 / quot8 in ie_dct.h) on
+// raw pixels gives per coefficient k the real affine map the FP32 code implements and its
+// rounding bound E_k.  With alpha*_k the reference's map (S*P/q on centred pixels) the FP32
+// quotient is within
+//     bound_k = E_k + 128 * sum|alpha_k - alpha*_k| + |value of our map at x = 128| + 1e-9
+// of the reference's FP64 quotient (1e-9 covers the reference's own FP64 rounding, <= 1e-10);
+// |t32 - rint(t32)| >= 0.5 - 2*bound_k flags a possible tie.  Returns false if alpha deviates
+// from alpha* beyond FP32 constant rounding (a transform bug).
 bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
     const int nn = n * n;
     std::memset(T, 0, sizeof(*T));
     const double factor = M_PI_2 / double(n);
     for (int u = 0; u < n; u++)
         for (int i = 0; i < n; i++) T->c[u * n + i] = std::cos(double(2.0 * i + 1.0) * double(u) * factor);
+    std::vector<double> sq(nn);
     for (int u = 0; u < n; u++)
         for (int v = 0; v < n; v++) {
             const int k = u * n + v;
@@ -173,6 +192,8 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
             T->qd[k] = double(q[k]);
             int e2 = 0;
             T->rq[k] = (std::frexp(double(q[k]), &e2) == 0.5) ? 1.0 / double(q[k]) : 0.0;
+            sq[k] = T->S[k] / T->qd[k];
+            T->g[k] = float(sq[k]);
             for (int i = 0; i < n; i++)
                 for (int j = 0; j < n; j++) {
                     T->P[k * nn + i * n + j] = T->c[u * n + i] * T->c[v * n + j];
@@ -181,41 +202,62 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
         }
     for (int k = 0; k < nn; k++) T->cf[k] = float(T->c[k]);
     for (int k = 0; k <= 8; k++) T->dct.K[k] = float(std::cos(double(k) * M_PI / 16.0));
+    // 4x4 plan: K2 = cos(pi/8), K4 = cos(pi/4), K6 = cos(3pi/8); row outputs R1, R3 carry 1/K2
+    {
+        const double K2 = std::cos(M_PI / 8.0), K4 = std::cos(M_PI / 4.0), K6 = std::cos(3.0 * M_PI / 8.0);
+        T->plan4.r = float(K6 / K2);
+        if (n == 4) {
+            for (int v = 0; v < 4; v++) {
+                const double Kv = (v == 0) ? 1.0 : (v == 2) ? K4 : K2;
+                float* G = T->plan4.col[v];
+                G[0] = float(Kv * sq[0 * 4 + v]);
+                G[1] = float(K4 * Kv * sq[2 * 4 + v]);
+                G[2] = float(K2 * Kv * sq[1 * 4 + v]);
+                G[3] = float(K6 * Kv * sq[1 * 4 + v]);
+                G[4] = float(K6 * Kv * sq[3 * 4 + v]);
+                G[5] = float(-K2 * Kv * sq[3 * 4 + v]);
+            }
+        }
+    }
 
-    // tracked run of the kernel's transform
+    // tracked run of the kernel's transform on raw pixels
     std::vector<Trk> b(nn);
     for (int k = 0; k < nn; k++) {
         for (int m = 0; m < 64; m++) b[k].a[m] = (m == k) ? 1.0 : 0.0;
+        b[k].c0 = 0.0;
         b[k].E = 0.0;
         b[k].integ = true;
     }
     TrkOp op{nn};
-    if (n == 4) ie::dct2d<4>(b.data(), T->dct, op);
-    else ie::dct2d<8>(b.data(), T->dct, op);
+    if (n == 4) ie::quot4(b.data(), T->plan4, op);
+    else ie::quot8(b.data(), T->dct, T->g, op);
     bool ok = true;
+    T->dc_exact = 0;
+    T->lim_min = 0.5f;
     for (int k = 0; k < nn; k++) {
-        const double sq = T->S[k] / T->qd[k];
-        const float g = float(sq);
-        T->g[k] = g;
-        const Trk t = op.mul(b[k], g);
-        double dev = 0.0, amax = 0.0;
+        const Trk& t = b[k];
+        double dev = 0.0, amax = 0.0, sa = 0.0;
         for (int m = 0; m < nn; m++) {
-            const double ref = sq * T->P[k * nn + m];
+            const double ref = sq[k] * T->P[k * nn + m];
             dev += std::fabs(t.a[m] - ref);
             amax = std::max(amax, std::fabs(ref));
+            sa += t.a[m];
         }
         if (dev > 1e-5 * (amax + 1e-30) * nn) ok = false;  // FP32 constants differ by ~1e-7 relative
-        const double bound = t.E + 128.0 * dev + 1e-9;
-        // coefficient 0: an integer sum scaled by a power of two is exact in FP32, and the
-        // reference computes it exactly too (c[0][*] = 1, C(0)^2 = 1/4, q a power of two)
-        int e2 = 0;
-        const bool pow2 = std::frexp(sq, &e2) == 0.5;
-        if (k == 0 && b[0].integ && b[0].E == 0.0 && pow2 && double(g) == sq) {
+        const double bound = t.E + 128.0 * dev + std::fabs(t.c0 + 128.0 * sa) + 1e-9;
+        // coefficient 0: an integer sum (minus 128*N*N) scaled by a power of two is exact in FP32,
+        // and the reference computes it exactly too (c[0][*] = 1, C(0)^2 = 1/4, q a power of two)
+        if (k == 0 && t.E == 0.0 && double(T->g[0]) == sq[0] && TrkOp::is_pow2(sq[0])) {
             T->thr[k] = -1.0f;
             T->lim[k] = 1.0f;  // never flagged
+            T->dc_exact = 1;
         } else {
             T->thr[k] = float(2.0 * bound);
             T->lim[k] = float(0.5 - 2.0 * bound);
+            // the structural coefficients (0,N/2), (N/2,0), (N/2,N/2) are flagged one by one
+            const int h = n / 2;
+            const bool structural = (k == h) || (k == h * n) || (k == h * n + h);
+            if (!structural) T->lim_min = std::min(T->lim_min, T->lim[k]);
         }
     }
     return ok;
@@ -228,14 +270,14 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
             HIPCHK(c, hipFree(c->d_state));
         }
         const size_t cap = std::max<size_t>(ntiles, c->cap_tiles * 2);
-        HIPCHK(c, hipMalloc(&c->d_state, 2 * cap * sizeof(uint64_t)));
-        HIPCHK(c, hipMemsetAsync(c->d_state, 0, 2 * cap * sizeof(uint64_t), c->stream));
+        HIPCHK(c, hipMalloc(&c->d_state, 3 * cap * sizeof(uint64_t)));
+        HIPCHK(c, hipMemsetAsync(c->d_state, 0, 3 * cap * sizeof(uint64_t), c->stream));
         c->cap_tiles = cap;
         c->tag = 0;
     }
     c->tag++;
     if (c->tag > 255) {
-        HIPCHK(c, hipMemsetAsync(c->d_state, 0, 2 * c->cap_tiles * sizeof(uint64_t), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->d_state, 0, 3 * c->cap_tiles * sizeof(uint64_t), c->stream));
         c->tag = 1;
     }
     if (size_t(nframes) > c->cap_frames) {
@@ -271,12 +313,13 @@ struct Geometry {
 
 Geometry geometry(int w, int h, int n, int nframes) {
     Geometry g;
-    const int bpt = (n == 4) ? 4 : 1;
+    const int bpt = ie::encode_blocks_per_thread(n);
     g.bx = w / n;
     g.by = h / n;
     g.gpr = (g.bx + bpt - 1) / bpt;
     g.gpf = g.gpr * g.by;
-    g.tpf = (g.gpf + ie::kTPB - 1) / ie::kTPB;
+    const int tpt = ie::encode_threads_per_tile();
+    g.tpf = (g.gpf + tpt - 1) / tpt;
     g.ntiles = g.tpf * nframes;
     return g;
 }
@@ -314,8 +357,8 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
         HIPCHK(c, hipMemcpyAsync(c->d_in, y, in_bytes, hipMemcpyHostToDevice, c->stream));
         dy = c->d_in;
     }
-    const int bpt = (c->n == 4) ? 4 : 1;
-    const bool vec_ok = (reinterpret_cast<uintptr_t>(dy) % 16 == 0) && (stride % (bpt * c->n) == 0) &&
+    const int bpt = ie::encode_blocks_per_thread(c->n);
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(dy) % size_t(bpt * c->n) == 0) && (stride % (bpt * c->n) == 0) &&
                         (nframes == 1 || frame_pitch % (bpt * c->n) == 0);
 
     // output
@@ -377,8 +420,25 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.coef = coef;
     static const int ablate = getenv("IE_ABLATE") ? atoi(getenv("IE_ABLATE")) : 0;  // profiling only
     a.ablate = ablate;
+    static const char* stamp_file = getenv("IE_STAMPS");  // profiling only: per-tile phase stamps
+    uint64_t* d_stamps = nullptr;
+    if (stamp_file) {
+        HIPCHK(c, hipMalloc(&d_stamps, size_t(g.ntiles) * ie::kStamps * sizeof(uint64_t)));
+        HIPCHK(c, hipMemsetAsync(d_stamps, 0, size_t(g.ntiles) * ie::kStamps * sizeof(uint64_t), c->stream));
+    }
+    a.stamps = d_stamps;
     ie::launch_encode(a, c->n, mode == IE_MODE_EXACT, c->stream);
     HIPCHK(c, hipGetLastError());
+    if (d_stamps) {
+        std::vector<uint64_t> h(size_t(g.ntiles) * ie::kStamps);
+        HIPCHK(c, hipMemcpyAsync(h.data(), d_stamps, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(d_stamps));
+        if (FILE* f = std::fopen(stamp_file, "wb")) {
+            std::fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+            std::fclose(f);
+        }
+    }
     if (c->use_ticket) c->ticket_base += uint64_t(g.ntiles);
 
     const bool want = frame_bits || end_bits || !out_dev;

@@ -16,6 +16,20 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations but not for its
+// global loads, so a prefetch of the next tile's pixels stays in flight across it (a
+// __syncthreads() would drain it).  Global memory is never handed between the threads of a
+// workgroup through these barriers.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Make a wave's LDS writes visible to its other lanes (LDS operations of one wave execute in
+// order; this only stops the compiler from moving accesses across).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Inclusive wave scan of a 32-bit value (64 lanes).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     const int l = lane_id();
@@ -37,16 +51,21 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
-// Exclusive workgroup scan of per-thread bit counts.  scratch: >= 4 words of LDS.
-// Returns the thread's exclusive offset; *total receives the workgroup sum.
+// Exclusive workgroup scan of per-thread bit counts (TPB threads).  scratch: >= TPB/64 words of
+// LDS.  Returns the thread's exclusive offset; *total receives the workgroup sum.
+template <int TPB = kTPB>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
     const int tid = threadIdx.x, wid = tid >> 6;
     const uint32_t incl = wave_incl_scan(v);
+    if constexpr (TPB == 64) {
+        *total = __shfl(incl, 63, 64);
+        return incl - v;
+    }
     if ((tid & 63) == 63) scratch[wid] = incl;
-    __syncthreads();
+    lds_barrier();
     uint32_t before = 0, sum = 0;
 #pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) {
+    for (int w = 0; w < TPB / 64; w++) {
         const uint32_t s = scratch[w];
         before += (w < wid) ? s : 0u;
         sum += s;
@@ -107,127 +126,160 @@ __device__ __forceinline__ void st_state(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Decoupled look-back executed by the WHOLE workgroup (all kTPB threads must call it).
-// Tile t sits at position chain_pos of its chain; its d-th predecessor (d = 0, 1, ...) is tile
-// t - step*(d+1).  Every tile publishes two 8-byte granules st[2t] = {tag:8, aggregate:24,
-// tail32:32} and st[2t+1] = {tag:8, inclusive:56}, each with ONE agent-scope store, so the
-// payload travels inside the atomic word and no fence is needed.  One round trip reads 4*kTPB
-// predecessor states; the exclusive prefix is the sum of aggregates up to the nearest
-// inclusive value.  Returns the exclusive prefix (chain-relative bits); *pred_tail receives the
-// last 32 bits of the chain before t (the immediate predecessor's tail granule).
-// sh: >= 8 words of LDS scratch.
-__device__ uint64_t lookback_wg(uint64_t* st, int t, int chain_pos, int step, uint32_t tag, uint32_t* pred_tail,
-                                unsigned* err, uint32_t* sh) {
-    constexpr int Q = 4;                  // predecessors per thread per round
-    constexpr int WIN = kTPB * Q;
-    constexpr int NONE = 0x7FFFFFFF;
-    const int tid = threadIdx.x, wid = tid >> 6;
-    int* s_min = reinterpret_cast<int*>(sh);      // [0] nearest inclusive distance
-    int* s_x = reinterpret_cast<int*>(sh + 1);    // [1] a not-ready state before it
-    uint64_t* s_sum = reinterpret_cast<uint64_t*>(sh + 2);  // [2..9] per-wave sums
+// ---- tile chain protocol ------------------------------------------------------------------
+// A chain is a sequence of tiles whose bit images are concatenated; tile t sits at position
+// chain_pos of its chain and its d-th predecessor (d = 0, 1, ...) is tile t - step*(d+1).
+// Every tile publishes three 8-byte granules, each with ONE agent-scope store so the payload
+// travels inside the atomic word and no fence is needed:
+//   st[3t+0] = {tag:8 | aggregate:56}   as soon as the tile's bit count is known (before emission)
+//   st[3t+1] = {tag:8 | inclusive:56}   once the look-back has resolved the exclusive prefix
+//   st[3t+2] = {tag:8 | tail:32}        the last 32 bits of the chain up to and including t
+// The early aggregate lets successors resolve their offsets while this tile is still emitting.
+constexpr int kGran = 3;
+
+__device__ __forceinline__ void publish(uint64_t* st, int t, int g, uint32_t tag, uint64_t v) {
+    st_state(&st[kGran * t + g], (uint64_t(tag) << 56) | (v & kMask56));
+}
+
+// A look-back probe: the states of the 64 chain predecessors d0 .. d0+63 of tile t (both
+// granules at once) and, for d0 = 0, the immediate predecessor's tail, loaded by one wave.  The
+// first probe is issued right after the tile publishes its own count, so its loads are in flight
+// while the tile emits its records; it is evaluated afterwards.
+struct Probe {
+    uint64_t gi, ga, gt;
+};
+
+__device__ __forceinline__ Probe probe_issue(const uint64_t* st, int t, int chain_pos, int step, int d0) {
+    Probe p;
+    p.gi = p.ga = p.gt = 0;
+    const int lane = lane_id();
+    const int d = d0 + lane;
+    if (chain_pos - 1 - d >= 0) {
+        const int idx = t - step * (d + 1);
+        p.gi = ld_state(&st[kGran * idx + 1]);
+        p.ga = ld_state(&st[kGran * idx]);
+    }
+    if (d0 == 0 && lane == 0 && chain_pos > 0) p.gt = ld_state(&st[kGran * (t - step) + 2]);
+    return p;
+}
+
+// Exclusive prefix of tile t, executed by ONE wave from a first probe: the sum of aggregates up
+// to the nearest inclusive value (normally inside the first window: predecessors publish their
+// aggregate as soon as their bit count is known).  Returns the prefix in every lane.
+__device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
+                                  unsigned* err, unsigned* rounds = nullptr) {
+    const int lane = lane_id();
     uint64_t excl = 0;
     int d0 = 0;
     unsigned spins = 0;
-    if (tid == 0) {
-        *s_min = NONE;
-        *s_x = 0;
-    }
-    __syncthreads();
+    if (rounds) *rounds = 0;
     for (;;) {
-        int status[Q];
-        uint64_t agg[Q], inc[Q];
-        int myP = NONE;
-#pragma unroll
-        for (int q = 0; q < Q; q++) {
-            const int d = d0 + tid * Q + q;
-            agg[q] = inc[q] = 0;
-            if (chain_pos - 1 - d < 0) {
-                status[q] = 2;  // before the chain start: a virtual inclusive prefix of 0
+        const int d = d0 + lane;
+        int status = 2;  // before the chain start: a virtual inclusive prefix of 0
+        uint64_t val = 0;
+        if (chain_pos - 1 - d >= 0) {
+            if (uint32_t(p.gi >> 56) == tag) {
+                val = p.gi & kMask56;
             } else {
-                const int idx = t - step * (d + 1);
-                const uint64_t gi = ld_state(&st[2 * idx + 1]);
-                if (uint32_t(gi >> 56) == tag) {
-                    status[q] = 2;
-                    inc[q] = gi & kMask56;
-                } else {
-                    const uint64_t ga = ld_state(&st[2 * idx]);
-                    if (uint32_t(ga >> 56) == tag) {
-                        status[q] = 1;
-                        agg[q] = (ga >> 32) & 0xFFFFFFull;
-                    } else {
-                        status[q] = 0;
-                    }
-                }
-            }
-            if (status[q] == 2 && myP == NONE) myP = d;
-        }
-        if (myP != NONE) atomicMin(s_min, myP);
-        __syncthreads();
-        const int dP = *s_min;
-        uint64_t contrib = 0;
-        bool x = false;
-#pragma unroll
-        for (int q = 0; q < Q; q++) {
-            const int d = d0 + tid * Q + q;
-            if (d < dP) {
-                x |= (status[q] == 0);
-                contrib += agg[q];
-            } else if (d == dP) {
-                contrib += inc[q];
+                status = (uint32_t(p.ga >> 56) == tag) ? 1 : 0;
+                val = p.ga & kMask56;
             }
         }
-        if (x) atomicOr(s_x, 1);
-        contrib = wave_sum64(contrib);
-        if ((tid & 63) == 0) s_sum[wid] = contrib;
-        __syncthreads();
-        const bool retry = *s_x != 0;
-        uint64_t tot = 0;
-#pragma unroll
-        for (int w = 0; w < kTPB / 64; w++) tot += s_sum[w];
-        __syncthreads();
-        if (tid == 0) {
-            *s_min = NONE;
-            *s_x = 0;
-        }
-        if (retry) {
+        const uint64_t incl = __ballot(status == 2);
+        const int dP = incl ? (__ffsll((unsigned long long)incl) - 1) : 64;
+        const uint64_t before = (dP < 64) ? ((1ull << dP) - 1ull) : ~0ull;
+        if (__ballot(status == 0) & before) {
             if (++spins > kSpinLimit) {
-                if (tid == 0) atomicAdd(&err[0], 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-            __syncthreads();
-            continue;
-        }
-        excl += tot;
-        __syncthreads();
-        if (dP != NONE) break;
-        d0 += WIN;
-    }
-    // the immediate predecessor's tail (published with or before its inclusive value)
-    uint32_t tail = 0;
-    if (tid == 0) {
-        const int idx = t - step;
-        unsigned sp = 0;
-        for (;;) {
-            const uint64_t ga = ld_state(&st[2 * idx]);
-            if (uint32_t(ga >> 56) == tag) {
-                tail = uint32_t(ga);
-                break;
-            }
-            if (++sp > kSpinLimit) {
-                atomicAdd(&err[0], 1u);
-                break;
+                if (lane == 0) atomicAdd(&err[0], 1u);
+                return excl;
             }
             __builtin_amdgcn_s_sleep(1);
+            p = probe_issue(st, t, chain_pos, step, d0);
+            if (rounds) *rounds += 1;
+            continue;
+        }
+        excl += wave_sum64((lane <= dP) ? val : 0ull);
+        if (dP < 64) return excl;
+        d0 += 64;
+        p = probe_issue(st, t, chain_pos, step, d0);
+        if (rounds) *rounds += 0x10000;
+    }
+}
+
+// The tail granule of tile idx (one thread).
+__device__ __forceinline__ uint32_t wait_tail(const uint64_t* st, int idx, uint32_t tag, unsigned* err,
+                                              unsigned* polls = nullptr) {
+    unsigned sp = 0;
+    for (;;) {
+        const uint64_t g = ld_state(&st[kGran * idx + 2]);
+        if (polls) *polls += 1;
+        if (uint32_t(g >> 56) == tag) return uint32_t(g);
+        if (++sp > kSpinLimit) {
+            atomicAdd(&err[0], 1u);
+            return 0u;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Phase A, right after the tile's bit count A is known: publish the aggregate (and, for a
+// chain's first tile, the inclusive prefix).  Thread 0 only.
+__device__ __forceinline__ void chain_publish_count(uint64_t* st, int t, int chain_pos, uint32_t tag, uint32_t A) {
+    publish(st, t, 0, tag, A);
+    if (chain_pos == 0) publish(st, t, 1, tag, A);
+}
+
+// Phase B, after the LDS image is complete (all threads): tail publication, look-back from the
+// probe `pr` wave 0 issued after phase A, and the
+// values the store needs (wave 0 resolves; the others wait at the closing barrier).  out: the
+// chain's output words; start: the chain's first bit.  Returns the exclusive prefix; misc[7]
+// receives the 32 bits preceding the tile (its store's `prev`).
+__device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
+                                                  const uint32_t* img, uint32_t A, const uint32_t* out,
+                                                  uint64_t start, unsigned* err, uint32_t* misc, const Probe& pr,
+                                                  uint64_t* dbg = nullptr) {
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        const uint32_t my_tail = image_tail32(img, A);
+        if (chain_pos == 0) {
+            // chain start: the bits before `start` belong to the caller (header); keep them
+            const uint32_t s = uint32_t(start & 31);
+            const uint32_t ptail = s ? (bswap32(out[start >> 5]) >> (32 - s)) : 0u;
+            const uint32_t tl = (A >= 32) ? my_tail : ((A ? (ptail << A) : ptail) | my_tail);
+            publish(st, t, 2, tag, tl);
+            misc[5] = 0;
+            misc[6] = 0;
+            misc[7] = ptail;
+        } else if (A >= 32) {
+            publish(st, t, 2, tag, my_tail);
         }
     }
-    *pred_tail = tail;  // meaningful in thread 0 (the only reader)
-    return excl;
+    if (chain_pos != 0 && tid < 64) {
+        unsigned rounds = 0, polls = 0;
+        const uint64_t excl = lookback_wave(pr, st, t, chain_pos, step, tag, err, dbg ? &rounds : nullptr);
+        if (tid == 0) {
+            publish(st, t, 1, tag, excl + A);
+            const uint32_t ptail = (uint32_t(pr.gt >> 56) == tag) ? uint32_t(pr.gt)
+                                                                  : wait_tail(st, t - step, tag, err, &polls);
+            if (dbg) *dbg = (uint64_t(rounds) << 32) | polls;
+            if (A < 32) {
+                // a short tile's tail carries predecessor bits
+                publish(st, t, 2, tag, (A ? (ptail << A) : ptail) | image_tail32(img, A));
+            }
+            misc[5] = uint32_t(excl);
+            misc[6] = uint32_t(excl >> 32);
+            misc[7] = ptail;
+        }
+    }
+    lds_barrier();
+    return uint64_t(misc[5]) | (uint64_t(misc[6]) << 32);
 }
 
 // Store a tile's bit image L (bits bits, tile bit 0 at absolute stream bit P) into the word
 // array out.  Word floor(P/32) is completed with `prev` (the 32 bits that precede bit P,
-// right-aligned).  The last partial word is left to the successor unless `last`.
+// right-aligned).  The last partial word is left to the successor unless `last`.  Aligned runs of
+// four words go out as one 16-byte store per thread (TPB threads).
+template <int TPB = kTPB>
 __device__ __forceinline__ void store_image(uint32_t* out, const uint32_t* L, uint32_t bits, uint64_t P,
                                             uint32_t prev, bool last) {
     const uint64_t w0 = P >> 5;
@@ -236,17 +288,27 @@ __device__ __forceinline__ void store_image(uint32_t* out, const uint32_t* L, ui
     const uint64_t w1 = last ? ((end + 31) >> 5) : (end >> 5);
     const uint32_t nL = (bits + 31) >> 5;
     const uint32_t nw = uint32_t(w1 - w0);
-    for (uint32_t r = threadIdx.x; r < nw; r += kTPB) {
+    auto word = [&](uint32_t r) -> uint32_t {
         const uint32_t cur = (r < nL) ? L[r] : 0u;
-        uint32_t v;
-        if (s == 0) {
-            v = cur;
-        } else {
-            const uint32_t pw = (r == 0) ? prev : L[r - 1];
-            v = (pw << (32 - s)) | (cur >> s);
-        }
-        out[w0 + r] = bswap32(v);
+        const uint32_t pw = (r == 0) ? prev : L[r - 1];
+        return bswap32(s ? ((pw << (32 - s)) | (cur >> s)) : cur);
+    };
+    const uint32_t tid = threadIdx.x;
+    const uint32_t head = min(nw, uint32_t((4u - uint32_t(w0 & 3u)) & 3u));
+    if (tid < head) out[w0 + tid] = word(tid);
+    const uint32_t nq = (nw - head) >> 2;
+#pragma unroll 4
+    for (uint32_t q = tid; q < nq; q += TPB) {
+        const uint32_t r = head + 4u * q;
+        uint4 v;
+        v.x = word(r);
+        v.y = word(r + 1);
+        v.z = word(r + 2);
+        v.w = word(r + 3);
+        *reinterpret_cast<uint4*>(out + w0 + r) = v;
     }
+    const uint32_t t0 = head + 4u * nq;
+    if (tid < nw - t0) out[w0 + t0 + tid] = word(t0 + tid);
 }
 
 }  // namespace ie

@@ -83,11 +83,64 @@ __host__ __device__ inline void dct2d(T* b, const DctConsts& k, const Op& op) {
     }
 }
 
+// ---- quotient transforms: raw pixels in, t[uv] ~ D[uv] / q[uv] out -------------------------
+// The level shift (x - 128, Block.cpp:141-143) is folded into the DC term: every other
+// coefficient's linear form has coefficient sum 0 (its butterfly path passes through a
+// difference), so shifting all pixels by 128 leaves it unchanged, and the DC path is an exact
+// integer sum, from which 128*N*N is subtracted exactly before the scaling.
+
+// N = 4, with the per-coefficient scale C(u)C(v)/q and the butterfly constants folded into the
+// column stage.  Row stage (8 ops/row): R0 = s0+s1, R2 = s0-s1, R1 = d0 + r*d1, R3 = r*d0 - d1
+// (r = cos(3pi/8)/cos(pi/8); the common factors K4, K2 move into the column constants).
+// Column stage for column v (12 ops): t[0v] = (s0+s1)*G0, t[2v] = (s0-s1)*G2,
+// t[1v] = d0*G1a + d1*G1b, t[3v] = d0*G3a + d1*G3b.
+struct Dct4Plan {
+    float r;
+    float col[4][6];  // per column v: G0, G2, G1a, G1b, G3a, G3b
+};
+
+template <class T, class Op>
+__host__ __device__ inline void quot4(T* b, const Dct4Plan& P, const Op& op) {
+    T R[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const T s0 = op.add(b[4 * i + 0], b[4 * i + 3]), s1 = op.add(b[4 * i + 1], b[4 * i + 2]);
+        const T d0 = op.sub(b[4 * i + 0], b[4 * i + 3]), d1 = op.sub(b[4 * i + 1], b[4 * i + 2]);
+        R[4 * i + 0] = op.add(s0, s1);
+        R[4 * i + 2] = op.sub(s0, s1);
+        R[4 * i + 1] = op.fma(d1, P.r, d0);
+        R[4 * i + 3] = op.fms(d0, P.r, d1);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        const float* G = P.col[v];
+        const T s0 = op.add(R[v], R[12 + v]), s1 = op.add(R[4 + v], R[8 + v]);
+        const T d0 = op.sub(R[v], R[12 + v]), d1 = op.sub(R[4 + v], R[8 + v]);
+        T e = op.add(s0, s1);
+        if (v == 0) e = op.addc(e, -2048.0f);  // level shift: -128 * 16, exact
+        b[0 * 4 + v] = op.mul(e, G[0]);
+        b[2 * 4 + v] = op.mul(op.sub(s0, s1), G[1]);
+        b[1 * 4 + v] = op.fma(d1, G[3], op.mul(d0, G[2]));
+        b[3 * 4 + v] = op.fma(d1, G[5], op.mul(d0, G[4]));
+    }
+}
+
+// N = 8: the separable butterfly (dct2d<8>), the exact DC level shift, then the scale g.
+template <class T, class Op>
+__host__ __device__ inline void quot8(T* b, const DctConsts& k, const float* g, const Op& op) {
+    dct2d<8>(b, k, op);
+    b[0] = op.addc(b[0], -8192.0f);  // -128 * 64, exact (integer sum)
+#pragma unroll
+    for (int m = 0; m < 64; m++) b[m] = op.mul(b[m], g[m]);
+}
+
 struct FloatOp {
     __device__ __forceinline__ float add(float a, float b) const { return a + b; }
     __device__ __forceinline__ float sub(float a, float b) const { return a - b; }
     __device__ __forceinline__ float mul(float a, float c) const { return a * c; }
     __device__ __forceinline__ float fma(float a, float c, float b) const { return __builtin_fmaf(a, c, b); }
+    __device__ __forceinline__ float fms(float a, float c, float b) const { return __builtin_fmaf(a, c, -b); }
+    __device__ __forceinline__ float addc(float a, float c) const { return a + c; }
 };
 
 }  // namespace ie

@@ -18,6 +18,9 @@ struct EncTables {
     float thr[64];  // bound on |t32 - t_ref|; < 0: t32 exact (coefficient 0 only)
     float lim[64];  // 0.5 - thr: |t32 - rint(t32)| >= lim flags a possible rounding tie
     DctConsts dct;  // butterfly constants cos(k pi/16)
+    Dct4Plan plan4; // 4x4 folded quotient transform (quot4)
+    float lim_min;  // min of lim[k] over the non-structural coefficients: one compare per block
+    int dc_exact;   // t[0] is exact in FP32 (q[0] a power of two): round it directly
     // FP64 reference order (algo.cpp:309-331, Block.cpp:149-152)
     double S[64];   // C(u)*C(v)
     double qd[64];  // double(q[uv])
@@ -38,7 +41,7 @@ struct EncArgs {
     int bx, by;              // blocks per row / column
     int gpr;                 // thread groups per block row = ceil(bx / BPT)
     int groups_per_frame;    // gpr * by
-    int tiles_per_frame;     // ceil(groups_per_frame / kTPB)
+    int tiles_per_frame;     // ceil(groups_per_frame / encode_threads_per_tile())
     int ntiles;
     int rle;
     int segmented;
@@ -46,7 +49,7 @@ struct EncArgs {
     uint32_t* out;           // 4-byte aligned, word w = stream bytes [4w, 4w+4)
     uint64_t out_pitch_words;
     uint64_t start_bit;
-    uint64_t* st;            // [2*ntiles]: {tag:8 | aggregate:24 | tail32:32}, {tag:8 | inclusive:56}
+    uint64_t* st;            // [3*ntiles] tile chain granules (ie_common.cuh)
     unsigned long long* ticket;  // nullptr: tiles in blockIdx order; else an atomic ticket
     unsigned long long ticket_base;
     uint32_t tag;            // epoch tag 1..255
@@ -56,9 +59,13 @@ struct EncArgs {
     const EncTables* tab;
     int16_t* coef;           // optional: quantised coefficients, natural order, [nframes*bx*by][N*N]
     int ablate;              // profiling only (IE_ABLATE): 1 no FP64, 2 no emission, 4 no look-back, 8 no store, 16 no DCT
+    uint64_t* stamps;        // profiling only (IE_STAMPS): [tile][kStamps] s_memtime per phase, thread 0
 };
 
+constexpr int kStamps = 16;
 void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s);
+int encode_blocks_per_thread(int n);  // horizontally adjacent blocks per lane (Geo<N>::BPT)
+int encode_threads_per_tile();       // threads per encoder workgroup (= tile)
 
 struct PackArgs {            // Huffman re-encode / bit copy: one variable-length code per byte
     const uint8_t* in;

@@ -50,13 +50,33 @@ template <> struct ZigZagInv<8> {
                                     21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 };
 
+#ifndef IE_BPT4
+#define IE_BPT4 4
+#endif
+#ifndef IE_WAVES4
+#define IE_WAVES4 4
+#endif
+// Threads per tile (= per workgroup).  256 (four waves, 1024 4x4 blocks); 64 makes every wave an
+// independent tile (no workgroup barriers, 16 tiles per CU) but quadruples the look-backs, which
+// measured slower.
+#ifndef IE_TPB
+#define IE_TPB 256
+#endif
+constexpr int kEncTPB = IE_TPB;
 template <int N> struct Geo;
-template <> struct Geo<4> { static constexpr int BPT = 4; };  // 16 B per pixel row per lane
-template <> struct Geo<8> { static constexpr int BPT = 1; };  //  8 B per pixel row per lane
+template <> struct Geo<4> {  // IE_BPT4 blocks side by side: 4 * IE_BPT4 bytes per pixel row per lane
+    static constexpr int BPT = IE_BPT4;
+    static constexpr int WAVES = IE_WAVES4;  // __launch_bounds__ occupancy hint (waves per SIMD)
+};
+template <> struct Geo<8> {  // one block: 8 bytes per pixel row per lane
+    static constexpr int BPT = 1;
+    static constexpr int WAVES = 2;
+};
 
-// bits-in-tile upper bound: 4 + 16 * (N*N + 1) bits per block
+// bits-in-tile upper bound: 4 + 16 * (N*N + 1) bits per block, plus slack for the zero bits the
+// pair emission may OR in past the last record (<= 2 * 16 bits) and the store's look-ahead word
 template <int N> constexpr int image_words() {
-    return ((kTPB * Geo<N>::BPT * (4 + 16 * (N * N + 1)) + 31) / 32 + 2 + 3) / 4 * 4;  // keeps misc 16-B aligned
+    return ((kEncTPB * Geo<N>::BPT * (4 + 16 * (N * N + 1)) + 31) / 32 + 4 + 3) / 4 * 4;  // keeps misc 16-B aligned
 }
 
 template <int WPR>
@@ -78,7 +98,7 @@ template <int N> struct BlockPx {
 // half away from zero (std::round).  Out of line: it runs only for the few coefficients whose
 // FP32 quotient lies near a rounding tie, and must not inflate the hot path's registers.
 template <int N>
-__device__ __noinline__ int exact_coef(const EncTables* __restrict__ tab, int k, BlockPx<N> px) {
+__device__ __forceinline__ int exact_coef_inl(const EncTables* __restrict__ tab, int k, BlockPx<N> px) {
     constexpr int NN = N * N;
     const double* P = &tab->P[k * NN];
     double acc = 0.0;
@@ -95,6 +115,12 @@ __device__ __noinline__ int exact_coef(const EncTables* __restrict__ tab, int k,
     return int(r);
 }
 
+// Out-of-line copy for the EXACT mode's per-coefficient loop.
+template <int N>
+__device__ __noinline__ int exact_coef(const EncTables* __restrict__ tab, int k, BlockPx<N> px) {
+    return exact_coef_inl<N>(tab, k, px);
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -109,9 +135,11 @@ __device__ __forceinline__ void load_group(const EncArgs& a, const uint8_t* base
             if constexpr (WPR == 4) {
                 const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
                 seg[r][0] = v.x; seg[r][1] = v.y; seg[r][2] = v.z; seg[r][3] = v.w;
-            } else {
+            } else if constexpr (WPR == 2) {
                 const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
                 seg[r][0] = v.x; seg[r][1] = v.y;
+            } else {
+                seg[r][0] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
             }
         }
     } else {
@@ -131,72 +159,130 @@ __device__ __forceinline__ void load_group(const EncArgs& a, const uint8_t* base
     }
 }
 
-// Quantise block b of the group into zp[] (zig-zag order, two int16 per word: z[2j] in the low
-// half); returns the number of coefficients re-evaluated in FP64.  The values pass through the
-// thread's private LDS slot `stage` (NN int16), so the rare FP64 re-evaluations patch them at a
-// runtime index without forcing a register array into scratch memory.
-template <int N> using NearMask = typename std::conditional<N == 4, uint32_t, uint64_t>::type;
+template <int N> struct Packed {
+    uint32_t w[N * N / 2];  // zig-zag order, two int16 per word: z[2j] in the low half
+};
 
-template <int N, int WPR>
-__device__ __forceinline__ NearMask<N> quantize_block(const EncTables* __restrict__ tab, const uint32_t (&seg)[N][WPR],
-                                                      int b, uint32_t (&zp)[N * N / 2]) {
+constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23: t + kMagic rounds t (|t| < 2^22) to an integer
+
+// The "structural" coefficients (0,N/2), (N/2,0), (N/2,N/2): their reference value is, up to
+// FP64 rounding, a rational multiple of an integer pixel sum (every c[u][i]c[v][j] is +-1/2 or
+// +-sqrt(1/2)), so their quotients land EXACTLY on rounding ties for 1/(4q) of all blocks, where
+// only the reference's own FP64 rounding decides.  They are flagged per coefficient and
+// re-evaluated alone; the other coefficients reach a tie only within the FP32 error bound.
+template <int N> struct Structural {
+    static constexpr int k[3] = {N / 2, (N / 2) * N, (N / 2) * N + N / 2};
+    static constexpr int zpos(int s) { return ZigZagInv<N>::pos[k[s]]; }
+};
+
+// Round the FP32 quotients t[] to int16 (zig-zag packed).  y = t + 1.5*2^23 leaves
+// int16(rint(t)) in y's low 16 bits and |t - (y - 1.5*2^23)| is the rounding residual.  Returns
+// the largest residual of the ordinary (non-structural, non-exact) coefficients -- >= lim_ord means
+// the block may hold a tie within the error bound -- and in *sflags bit s a possible tie of
+// structural coefficient s.
+template <int N>
+__device__ __forceinline__ float round_block(const EncTables* __restrict__ tab, const float (&t)[N * N],
+                                             uint32_t (&zp)[N * N / 2], uint32_t* sflags) {
     constexpr int NN = N * N;
-    using Mask = NearMask<N>;
-    Mask need = 0;
-    float x[NN];
-#pragma unroll
-    for (int i = 0; i < N; i++)
-#pragma unroll
-        for (int j = 0; j < N; j++) x[i * N + j] = float(pix<WPR>(seg[i], b * N + j)) - 128.0f;
-    dct2d<N>(x, tab->dct, FloatOp());
-    // t = D * C(u)C(v)/q; y = t + 1.5*2^23 rounds t to the nearest integer (|t| < 2^22) and leaves
-    // int16(rint(t)) in y's low 16 bits; |t - rint(t)| >= 0.5 - bound flags a possible tie.
-    constexpr float kMagic = 12582912.0f;
     uint32_t yb[NN];
+    float e[NN];
 #pragma unroll
     for (int k = 0; k < NN; k++) {
-        const float t = x[k] * tab->g[k];
-        if (k == 0 && tab->thr[0] < 0.0f) {
-            // t is exact here (integer sum times a power of two): round half away from zero
-            yb[k] = uint32_t(int(truncf(t + copysignf(0.5f, t))));
-        } else {
-            const float y = t + kMagic;
-            const float r = y - kMagic;
-            need |= Mask(fabsf(t - r) >= tab->lim[k]) << k;
-            yb[k] = __float_as_uint(y);
-        }
+        const float y = t[k] + kMagic;
+        e[k] = fabsf(t[k] - (y - kMagic));
+        yb[k] = __float_as_uint(y);
     }
+    // t[0] exact (q[0] a power of two): std::round's half-away-from-zero directly
+    const uint32_t dc = uint32_t(int(truncf(t[0] + copysignf(0.5f, t[0]))));
+    const bool dcx = tab->dc_exact != 0;
+    yb[0] = dcx ? dc : yb[0];
+    float emax = dcx ? 0.0f : e[0];
+#pragma unroll
+    for (int k = 1; k < NN; k++) {
+        if (k == Structural<N>::k[0] || k == Structural<N>::k[1] || k == Structural<N>::k[2]) continue;
+        emax = fmaxf(emax, e[k]);
+    }
+    uint32_t sf = 0;
+#pragma unroll
+    for (int s = 0; s < 3; s++) sf |= (e[Structural<N>::k[s]] >= tab->lim[Structural<N>::k[s]]) ? (1u << s) : 0u;
+    *sflags = sf;
 #pragma unroll
     for (int j = 0; j < NN / 2; j++)
         zp[j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
-    return need;
+    return emax;
 }
 
-// Replace zig-zag coefficient kz of a packed block by v (a runtime position: a select chain over
-// the words, so the block stays in registers).
-template <int NP>
-__device__ __forceinline__ void patch(uint32_t (&zp)[NP], int kz, uint32_t v) {
-    const int wsel = kz >> 1;
-    const uint32_t lo = v & 0xFFFFu, hi = v << 16;
+template <int N, int WPR>
+__device__ __forceinline__ void block_pixels(const uint32_t (&seg)[N][WPR], int b, float (&x)[N * N]) {
 #pragma unroll
-    for (int j = 0; j < NP; j++) {
-        const uint32_t w = zp[j];
-        const uint32_t nw = (kz & 1) ? ((w & 0xFFFFu) | hi) : ((w & 0xFFFF0000u) | lo);
-        zp[j] = (j == wsel) ? nw : w;
+    for (int i = 0; i < N; i++)
+#pragma unroll
+        for (int j = 0; j < N; j++) x[i * N + j] = float(pix<WPR>(seg[i], b * N + j));
+}
+
+template <int N>
+__device__ __forceinline__ void quotients(const EncTables* __restrict__ tab, float (&x)[N * N]) {
+    if constexpr (N == 4) quot4(x, tab->plan4, FloatOp());
+    else quot8(x, tab->dct, tab->g, FloatOp());
+}
+
+// The FP64 fix-up of one flagged block, all in line (a call would make the caller spill its
+// live coefficient registers around it): the same FP32 quotients rounded into the task's LDS
+// result slot, then every coefficient whose residual reaches its own lim[k] re-evaluated in the
+// reference's FP64 order and patched in place (a runtime position: LDS, not a register array).
+template <int N>
+__device__ __forceinline__ void fix_block(const EncTables* __restrict__ tab, const BlockPx<N>& px, uint32_t* res) {
+    constexpr int NN = N * N;
+    float x[NN];
+#pragma unroll
+    for (int k = 0; k < NN; k++) x[k] = float((px.w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+    quotients<N>(tab, x);
+    uint32_t yb[NN];
+    uint64_t near = 0;
+#pragma unroll
+    for (int k = 0; k < NN; k++) {
+        const float y = x[k] + kMagic;
+        const float e = fabsf(x[k] - (y - kMagic));
+        yb[k] = __float_as_uint(y);
+        if (k == 0 && tab->dc_exact) yb[0] = uint32_t(int(truncf(x[0] + copysignf(0.5f, x[0]))));
+        else near |= uint64_t(e >= tab->lim[k]) << k;
+    }
+#pragma unroll
+    for (int j = 0; j < NN / 2; j++)
+        res[j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
+    uint16_t* h = reinterpret_cast<uint16_t*>(res);
+    while (near) {
+        const int k = __ffsll((unsigned long long)near) - 1;
+        near &= near - 1;
+        h[ZigZagInv<N>::pos[k]] = uint16_t(exact_coef_inl<N>(tab, k, px));
     }
 }
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
+// Packed int16 helpers (the compiler otherwise splits them into per-half compares).
+// (Constants go in a register: an inline constant of a packed op feeds the low half only.)
+__device__ __forceinline__ uint32_t pk_min1_u16(uint32_t w) {  // per half: min(h, 1) = (h != 0)
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(w), "s"(0x00010001u));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_sign_i16(uint32_t w) {  // per half: h >> 15 (arithmetic)
+    uint32_t r;
+    asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(r) : "s"(0x000F000Fu), "v"(w));
+    return r;
+}
+
 // Zig-zag RLE sizing of one packed block (Block.cpp:186-232, :383-397), two coefficients per
-// packed-int16 instruction.  Returns bl | Lw << 8 and the record length in bits.
+// packed-int16 instruction.  Returns bl | Lw << 8 and the record length in bits.  In the RLE
+// truncation case (L == N*N, z[N*N-2] == 0: the reference drops the last coefficient,
+// Block.cpp:388-390) z[N*N-1] is cleared, so every coefficient at or past Lw is zero.
 template <int N>
-__device__ __forceinline__ uint32_t size_block(const uint32_t (&zp)[N * N / 2], int rle, uint32_t* bits) {
+__device__ __forceinline__ uint32_t size_block(uint32_t (&zp)[N * N / 2], int rle, uint32_t* bits) {
     constexpr int NN = N * N;
     constexpr int NP = NN / 2;
-    // nz: bit kz set iff z[kz] != 0 (min(u16, 1) per half, even kz in the low halves)
-    uint64_t nz = 0;
+    uint64_t nz = 0;  // bit kz set iff z[kz] != 0
     uint32_t mo = 0;  // OR of v ^ (v >> 15) per half: its bit length + 1 is the widest bits_needed
 #pragma unroll
     for (int g = 0; g < NP / 8; g++) {
@@ -204,10 +290,8 @@ __device__ __forceinline__ uint32_t size_block(const uint32_t (&zp)[N * N / 2], 
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const uint32_t w = zp[g * 8 + j];
-            const u16x2 m = __builtin_elementwise_min(__builtin_bit_cast(u16x2, w), u16x2{1, 1});
-            M |= __builtin_bit_cast(uint32_t, m) << (2 * j);
-            const s16x2 v = __builtin_bit_cast(s16x2, w);
-            mo |= __builtin_bit_cast(uint32_t, v ^ (v >> s16x2{15, 15}));
+            M |= pk_min1_u16(w) << (2 * j);
+            mo |= w ^ pk_sign_i16(w);  // one v_bitop3
         }
         const uint32_t nz16 = (M & 0x5555u) | ((M >> 15) & 0xAAAAu);
         nz |= uint64_t(nz16) << (16 * g);
@@ -223,6 +307,7 @@ __device__ __forceinline__ uint32_t size_block(const uint32_t (&zp)[N * N / 2], 
     } else if (L == NN && !((nz >> (NN - 2)) & 1ull)) {
         const uint64_t m = nz & ((1ull << (NN - 1)) - 1);  // drop the last element (Block.cpp:388-390)
         lw = m ? 64 - __clzll((long long)m) : 0;
+        zp[NP - 1] &= 0xFFFFu;
     } else {
         lw = L;
     }
@@ -230,190 +315,250 @@ __device__ __forceinline__ uint32_t size_block(const uint32_t (&zp)[N * N / 2], 
     return uint32_t(bl) | (uint32_t(lw) << 8);
 }
 
-template <int N, bool EXACT>
-__global__ __launch_bounds__(kTPB, 4) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
-    constexpr int NN = N * N;
-    constexpr int BPT = Geo<N>::BPT;
-    constexpr int WPR = BPT * N / 4;
-    constexpr int IMGW = image_words<N>();
-    __shared__ uint32_t smem[IMGW + 32];
-    uint32_t* img = smem;
-    uint32_t* misc = smem + IMGW;  // [0..3] scan, [4] ticket, [5..6] excl, [7] pred tail, [8..31] look-back
+// OR the low `len` bits of v (MSB first) into the LDS bit image at bit p (len + p%32 <= 64).
+__device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t v, uint32_t len) {
+    const uint32_t w = p >> 5, s = p & 31u;
+    const uint64_t x = uint64_t(v) << (64u - len - s);
+    atomicOr(&img[w], uint32_t(x >> 32));
+    atomicOr(&img[w + 1], uint32_t(x));
+}
 
-    const int tid = threadIdx.x;
-    // Tile order = dispatch order.  Workgroups are dispatched in increasing blockIdx per XCD, so
-    // every predecessor of a resident tile is resident or done and the look-back cannot deadlock;
-    // the bounded spins report (never hang) should that ever not hold, and the host then re-runs
-    // with an atomic ticket (a.ticket != nullptr), which orders tiles explicitly.
-    int t;
-    if (a.ticket) {
-        if (tid == 0) misc[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
-        __syncthreads();
-        t = int(misc[4]);
-        if (t >= a.ntiles) return;  // ticket desync (a failed earlier launch): never touch memory
+// The record of one sized block at bit p of the tile image (Block.cpp:372-413): bl in 4 bits,
+// [Lw in bl bits,] then the coefficients two at a time (2*bl <= 32 bits per OR pair).
+template <int N>
+__device__ __forceinline__ void emit_block(uint32_t* img, uint32_t p, const uint32_t (&zp)[N * N / 2], uint32_t blw,
+                                           int rle) {
+    const uint32_t bl = blw & 0xFFu, lw = blw >> 8;
+    const uint32_t m = (1u << bl) - 1u;
+    if (rle) {
+        scatter_bits(img, p, ((bl & 0xFu) << bl) | lw, 4u + bl);
+        p += 4u + bl;
     } else {
-        t = int(blockIdx.x);
+        scatter_bits(img, p, bl & 0xFu, 4u);
+        p += 4u;
     }
-    // Independent images interleave their tiles in ticket order (frame = t % nframes), so every
-    // frame's chain advances together; a concatenated stream keeps chain order = ticket order.
-    int frame, tif, step;
+#pragma unroll
+    for (int j = 0; j < N * N / 2; j++) {
+        if (uint32_t(2 * j) < lw) {
+            const uint32_t lo = zp[j] & m, hi = (zp[j] >> 16) & m;
+            scatter_bits(img, p, (lo << bl) | hi, 2u * bl);
+            p += 2u * bl;
+        }
+    }
+}
+
+// Where tile t sits: its chain (frame / whole batch), its position in it and this thread's
+// group of blocks.
+struct TileGeo {
+    int frame, tif, step, chain_pos;
+    int nblk, byi, bx0;  // blocks of this thread's group (nblk = 0: none)
+};
+
+template <int N>
+__device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
+    TileGeo g;
+    // Independent images interleave their tiles (frame = t % nframes), so every frame's chain
+    // advances together; a concatenated stream keeps chain order = tile order.
     if (a.segmented) {
-        frame = t % a.nframes;
-        tif = t / a.nframes;
-        step = a.nframes;
+        g.frame = t % a.nframes;
+        g.tif = t / a.nframes;
+        g.step = a.nframes;
     } else {
-        frame = t / a.tiles_per_frame;
-        tif = t - frame * a.tiles_per_frame;
-        step = 1;
+        g.frame = t / a.tiles_per_frame;
+        g.tif = t - g.frame * a.tiles_per_frame;
+        g.step = 1;
     }
-    const int chain_pos = a.segmented ? tif : t;  // tiles before this one in its chain
+    g.chain_pos = a.segmented ? g.tif : t;  // tiles before this one in its chain
+    const int gi = g.tif * kEncTPB + tid;
+    g.nblk = g.byi = g.bx0 = 0;
+    if (gi < a.groups_per_frame) {
+        g.byi = gi / a.gpr;
+        g.bx0 = (gi - g.byi * a.gpr) * Geo<N>::BPT;
+        g.nblk = min(Geo<N>::BPT, a.bx - g.bx0);
+    }
+    return g;
+}
 
-    // ---------------------------------------------------------------- 1. transform + quantise
-    const int gi = tif * kTPB + tid;
-    const bool active = gi < a.groups_per_frame;
-    int nblk = 0, byi = 0, bx0 = 0;
-    uint32_t seg[N][WPR];
-    if (active) {
-        byi = gi / a.gpr;
-        bx0 = (gi - byi * a.gpr) * BPT;
-        nblk = min(BPT, a.bx - bx0);
-        const uint8_t* base = a.y + size_t(frame) * a.frame_pitch + size_t(byi) * N * a.stride + size_t(bx0) * N;
-        load_group<N, WPR>(a, base, nblk, seg);
+template <int N, int WPR>
+__device__ __forceinline__ void load_tile(const EncArgs& a, const TileGeo& g, uint32_t (&seg)[N][WPR]) {
+    if (g.nblk) {
+        const uint8_t* base =
+            a.y + size_t(g.frame) * a.frame_pitch + size_t(g.byi) * N * a.stride + size_t(g.bx0) * N;
+        load_group<N, WPR>(a, base, g.nblk, seg);
     } else {
 #pragma unroll
         for (int r = 0; r < N; r++)
 #pragma unroll
             for (int m = 0; m < WPR; m++) seg[r][m] = 0;
     }
+}
 
+// Profiling stamps (IE_STAMPS): thread 0's s_memtime at the phase boundaries of each tile.
+#define STAMP(i)                                                                                  \
+    do {                                                                                          \
+        if (a.stamps && tid == 0) a.stamps[size_t(t) * kStamps + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
+template <int N, bool EXACT>
+__global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
+    constexpr int NN = N * N;
     constexpr int NP = NN / 2;
-    using Mask = NearMask<N>;
-    uint32_t zp[BPT][NP];  // quantised coefficients, zig-zag order, two int16 per word
-    Mask need[BPT];
+    constexpr int BPT = Geo<N>::BPT;
+    constexpr int WPR = BPT * N / 4;
+    constexpr int IMGW = image_words<N>();
+    constexpr int TPB = kEncTPB;
+    __shared__ uint32_t smem[IMGW + 32];
+    uint32_t* img = smem;
+    uint32_t* misc = smem + IMGW;  // [0..15] scan scratch (one word per wave)
+    uint32_t* ctl = misc + 16;     // [4] ticket, [5..6] exclusive prefix, [7] predecessor tail
+
+    const int tid = threadIdx.x;
+    // Tile order = dispatch order.  Workgroups are dispatched in increasing blockIdx, so every
+    // chain predecessor of a resident tile is resident or done and the look-back cannot
+    // deadlock; the bounded spins report (never hang) should that ever not hold, and the host
+    // then re-runs with an atomic ticket (a.ticket != nullptr), which orders tiles explicitly.
+    int t;
+    if (a.ticket) {
+        if (tid == 0) ctl[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+        lds_barrier();
+        t = int(ctl[4]);
+        if (t >= a.ntiles) return;  // ticket desync (a failed earlier launch): never touch memory
+    } else {
+        t = int(blockIdx.x);
+    }
+    STAMP(0);
+    const TileGeo g = tile_geo<N>(a, t, tid);
+    const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
+    const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
+    uint32_t seg[N][WPR];
+    load_tile<N, WPR>(a, g, seg);
+
+    asm volatile("; PHASE load_done" ::: "memory");
+    if (a.stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
+        uint32_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < N; r++)
+#pragma unroll
+            for (int m = 0; m < WPR; m++) acc ^= seg[r][m];
+        if (acc == 0x9E3779B9u) a.err[1] = acc;
+    }
+    STAMP(2);
+    // ---------------------------------------------------------------- 1. transform + quantise
+    uint32_t zp[BPT][NP];
+    // fix-up requests, 4 bits per block: bits 0-2 structural coefficient s, bit 3 the whole block
+    uint32_t flags = 0;
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
         __builtin_amdgcn_sched_barrier(0);  // one block at a time: keeps the live set small
-        if constexpr (!EXACT) {
-            if (a.ablate & 16) {
-                need[b] = 0;
-#pragma unroll
-                for (int j = 0; j < NP; j++) zp[b][j] = seg[j % N][(j / N) % WPR] & 0x00FF00FFu;
-            } else {
-                need[b] = quantize_block<N, WPR>(tab, seg, b, zp[b]);
-            }
-        } else {
-            need[b] = (NN == 64) ? ~Mask(0) : Mask((1ull << (NN & 63)) - 1);
-#pragma unroll
-            for (int j = 0; j < NP; j++) zp[b][j] = 0;
-        }
-        if (b >= nblk || (a.ablate & 1)) need[b] = 0;
-    }
-
-    // ---------------------------------------------------------------- 1b. FP64 re-evaluation
-    // Coefficients flagged as possible ties (FAST) or all coefficients (EXACT) take the
-    // reference's FP64 order.  FAST mode compacts a wave's flagged (lane, block, k) triples into
-    // an LDS task list so that one exact evaluation per lane serves up to 64 of them.
-    unsigned nfall = 0;
-    const int lane = tid & 63, wid = tid >> 6;
-    if constexpr (EXACT) {
-#pragma unroll
-        for (int b = 0; b < BPT; b++) {
+        if constexpr (EXACT) {
             BlockPx<N> px;
 #pragma unroll
             for (int i = 0; i < N; i++)
 #pragma unroll
                 for (int m = 0; m < N / 4; m++) px.w[i * (N / 4) + m] = seg[i][(b * N) / 4 + m];
-            Mask nd = need[b];
-            while (nd) {
-                const int k = (N == 4) ? (__ffs(uint32_t(nd)) - 1) : (__ffsll((unsigned long long)nd) - 1);
-                nd &= nd - 1;
-                patch<NP>(zp[b], ZigZagInv<N>::pos[k], uint32_t(exact_coef<N>(tab, k, px)));
-            }
-        }
-    } else {
-        uint32_t cnt = 0;
+            uint32_t yb[NN];
+            for (int k = 0; k < NN; k++) yb[k] = uint32_t(exact_coef<N>(tab, k, px));
 #pragma unroll
-        for (int b = 0; b < BPT; b++) cnt += (N == 4) ? __popc(uint32_t(need[b])) : __popcll((unsigned long long)need[b]);
-        if (__ballot(cnt != 0)) {
-            // per-wave LDS region (the tile image is not built yet): pixels, tasks, results
-            constexpr int WAVE_WORDS = (IMGW - 4) / (kTPB / 64);
-            constexpr int PIXW = N * WPR;              // pixel words per lane (16 for both N)
-            constexpr int CAP = (WAVE_WORDS - 64 * PIXW) / 2;
-            static_assert(CAP >= 128, "LDS task list too small");
-            uint32_t* wpix = img + wid * WAVE_WORDS;
-            uint32_t* wtask = wpix + 64 * PIXW;
-            int32_t* wres = reinterpret_cast<int32_t*>(wtask + CAP);
-            const uint32_t incl = wave_incl_scan(cnt);
-            const uint32_t off = incl - cnt;
-            const uint32_t T = __shfl(incl, 63, 64);
-            nfall = cnt;
+            for (int j = 0; j < NP; j++)
+                zp[b][j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
+        } else {
+            float x[NN];
+            block_pixels<N, WPR>(seg, b, x);
+            if (!(a.ablate & 16)) quotients<N>(tab, x);
+            uint32_t sf;
+            const float emax = round_block<N>(tab, x, zp[b], &sf);
+            uint32_t fb = (emax >= tab->lim_min) ? 8u : sf;  // a whole-block fix covers s
+            if (a.ablate & 32) fb &= 7u;   // profiling: drop whole-block fixes
+            if (a.ablate & 64) fb &= 8u;   // profiling: drop structural fixes
+            if (b < nblk && !(a.ablate & 1)) flags |= fb << (4 * b);
+        }
+    }
+    asm volatile("; PHASE quant_done" ::: "memory");
+    STAMP(3);
+
+    // ---------------------------------------------------------------- 1b. FP64 fix-up
+    // The tile's requests are compacted into an LDS task list (owner, block, kind) beside every
+    // thread's pixel rows, so that one thread per task serves up to RR of them in as few waves
+    // as possible (the areas alias the tile image, not yet built).  Kind s < 3: structural
+    // coefficient s alone in the reference's FP64 order (a compile-time row of P, read through the
+    // scalar cache); kind 3: fix_block (every coefficient near a tie).
+    if constexpr (!EXACT) {
+        constexpr int PIXW = N * WPR;               // pixel words per thread
+        constexpr int TCAP = TPB * BPT * 3;         // worst case: every structural coefficient
+        constexpr int RFIT = (IMGW - TPB * PIXW - TCAP) / NP;
+        constexpr int RR = RFIT < TPB ? RFIT : TPB;  // tasks per round
+        static_assert(RR >= 16, "LDS fix-up area too small");
+        uint32_t T;
+        const uint32_t off0 = block_excl_scan<TPB>(__popc(flags), misc, &T);
+        if (T) {  // uniform
+            uint32_t* wpix = img;                  // [TPB][PIXW] every thread's pixel rows
+            uint32_t* wtask = wpix + TPB * PIXW;   // [T] tid | b << 12 | kind << 16
+            uint32_t* wres = wtask + TCAP;         // [RR][NP]
 #pragma unroll
             for (int i = 0; i < N; i++)
 #pragma unroll
-                for (int m = 0; m < WPR; m++) wpix[lane * PIXW + i * WPR + m] = seg[i][m];
-            {
-                uint32_t o = off;
+                for (int m = 0; m < WPR; m++) wpix[tid * PIXW + i * WPR + m] = seg[i][m];
+            uint32_t o = off0;
 #pragma unroll
-                for (int b = 0; b < BPT; b++) {
-                    Mask nd = need[b];
-                    while (nd) {
-                        const int k = (N == 4) ? (__ffs(uint32_t(nd)) - 1) : (__ffsll((unsigned long long)nd) - 1);
-                        nd &= nd - 1;
-                        if (o < CAP) wtask[o] = uint32_t(lane) | (uint32_t(b) << 6) | (uint32_t(k) << 8);
-                        o++;
-                    }
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t TT = min(T, uint32_t(CAP));
-            for (uint32_t base = 0; base < TT; base += 64) {
-                const uint32_t i = base + lane;
-                if (i < TT) {
+            for (int b = 0; b < BPT; b++)
+#pragma unroll
+                for (int s = 0; s < 4; s++)
+                    if ((flags >> (4 * b + s)) & 1u) wtask[o++] = uint32_t(tid) | (uint32_t(b) << 12) | (uint32_t(s) << 16);
+            STAMP(10);
+            lds_barrier();
+            for (uint32_t base = 0; base < T; base += RR) {
+                const uint32_t i = base + uint32_t(tid);
+                if (tid < RR && i < T) {
                     const uint32_t task = wtask[i];
-                    const int o = int(task & 63), b = int((task >> 6) & 3), k = int(task >> 8);
+                    const uint32_t ow = task & 0xFFFu, b = (task >> 12) & 0xFu, kind = task >> 16;
                     BlockPx<N> px;
 #pragma unroll
                     for (int r = 0; r < N; r++)
 #pragma unroll
-                        for (int m = 0; m < N / 4; m++) px.w[r * (N / 4) + m] = wpix[o * PIXW + r * WPR + (b * N) / 4 + m];
-                    wres[i] = exact_coef<N>(tab, k, px);
+                        for (int m = 0; m < N / 4; m++)
+                            px.w[r * (N / 4) + m] = wpix[ow * PIXW + r * WPR + (b * N) / 4 + m];
+                    if (kind == 3) fix_block<N>(tab, px, wres + tid * NP);
+#pragma unroll
+                    for (int s = 0; s < 3; s++)
+                        if (kind == uint32_t(s))
+                            wres[tid * NP] = uint32_t(exact_coef_inl<N>(tab, Structural<N>::k[s], px)) & 0xFFFFu;
                 }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (cnt) {
-                uint32_t o = off;
+                lds_barrier();
+                if (base == 0) STAMP(11);
+                uint32_t oo = off0;
 #pragma unroll
                 for (int b = 0; b < BPT; b++) {
-                    Mask nd = need[b];
-                    if (nd) {
-                        BlockPx<N> px;
 #pragma unroll
-                        for (int i = 0; i < N; i++)
+                    for (int s = 0; s < 4; s++) {
+                        if ((flags >> (4 * b + s)) & 1u) {
+                            if (oo >= base && oo < base + RR) {
+                                const uint32_t* r = wres + (oo - base) * NP;
+                                if (s == 3) {
 #pragma unroll
-                            for (int m = 0; m < N / 4; m++) px.w[i * (N / 4) + m] = seg[i][(b * N) / 4 + m];
-                        do {
-                            const int k = (N == 4) ? (__ffs(uint32_t(nd)) - 1) : (__ffsll((unsigned long long)nd) - 1);
-                            nd &= nd - 1;
-                            // tasks beyond the list capacity are evaluated by their own lane
-                            const int v = (o < CAP) ? wres[o] : exact_coef<N>(tab, k, px);
-                            patch<NP>(zp[b], ZigZagInv<N>::pos[k], uint32_t(v));
-                            o++;
-                        } while (nd);
+                                    for (int j = 0; j < NP; j++) zp[b][j] = r[j];
+                                } else {
+                                    const int zpos = Structural<N>::zpos(s);
+                                    const uint32_t v = r[0];
+                                    zp[b][zpos >> 1] = (zpos & 1) ? ((zp[b][zpos >> 1] & 0xFFFFu) | (v << 16))
+                                                                  : ((zp[b][zpos >> 1] & 0xFFFF0000u) | v);
+                                }
+                            }
+                            oo++;
+                        }
                     }
                 }
+                lds_barrier();
+                if (base == 0) STAMP(12);
             }
-            __builtin_amdgcn_wave_barrier();
+            if (tid == 0) atomicAdd(&a.err[2 + (t & 63)], T);  // statistics: fix-up tasks, spread counters
         }
-        const unsigned wsum = unsigned(wave_sum64(nfall));  // statistics: spread counters
-        if (lane == 0 && wsum) atomicAdd(&a.err[2 + ((t * 4 + wid) & 63)], wsum);
     }
+    asm volatile("; PHASE fix_done" ::: "memory");
+    STAMP(4);
 
     // ---------------------------------------------------------------- 1c. zig-zag RLE sizing
     uint32_t blw[BPT];  // bl | Lw << 8
+    uint32_t rbits[BPT];
     uint32_t mybits = 0;
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
@@ -425,98 +570,71 @@ __global__ __launch_bounds__(kTPB, 4) void encode_kernel(EncArgs a, const EncTab
                 dst[k] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
             }
         }
-        uint32_t rb;
-        blw[b] = size_block<N>(zp[b], a.rle, &rb);
-        if (b < nblk) mybits += rb;
+        blw[b] = size_block<N>(zp[b], a.rle, &rbits[b]);
+        rbits[b] = (b < nblk) ? rbits[b] : 0u;
+        mybits += rbits[b];
     }
-    __syncthreads();  // the per-wave task areas alias the tile image
+    asm volatile("; PHASE size_done" ::: "memory");
+    STAMP(5);
+    lds_barrier();  // the fix-up areas alias the tile image
 
     // ---------------------------------------------------------------- 2. tile scan + LDS image
     uint32_t A;
-    const uint32_t off = block_excl_scan(mybits, misc, &A);
+    const uint32_t off = block_excl_scan<TPB>(mybits, misc, &A);
+    if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);  // successors may resolve now
+    Probe pr{0, 0, 0};
+    if (tid < 64 && chain_pos != 0 && !(a.ablate & 4)) pr = probe_issue(a.st, t, chain_pos, step, 0);  // in flight during emission
     const uint32_t nw = (A + 31) >> 5;
-    for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
-    __syncthreads();
-    if (mybits && !(a.ablate & 2)) {
-        BitSink sink(img, off);
+    for (uint32_t w = tid; w < nw + 2; w += TPB) img[w] = 0u;
+    lds_barrier();
+    asm volatile("; PHASE scan_done" ::: "memory");
+    STAMP(6);
+    if (!(a.ablate & 2)) {
+        uint32_t p = off;
 #pragma unroll
         for (int b = 0; b < BPT; b++) {
-            if (b < nblk) {
-                const int bl = int(blw[b] & 0xFF), lw = int(blw[b] >> 8);
-                const uint32_t m = (1u << bl) - 1u;
-                if (a.rle) sink.put(4 + bl, ((uint32_t(bl) & 0xFu) << bl) | uint32_t(lw));
-                else sink.put(4, uint32_t(bl) & 0xFu);
-                // value fields in pairs: (z[2j], z[2j+1]) as one 2*bl-bit put
-#pragma unroll
-                for (int j = 0; j < NN / 2; j++) {
-                    if (2 * j < lw) {
-                        const uint32_t lo = zp[b][j] & m, hi = (zp[b][j] >> 16) & m;
-                        if (2 * j + 1 < lw) sink.put(2 * bl, (lo << bl) | hi);
-                        else sink.put(bl, lo);
-                    }
-                }
-            }
+            if (rbits[b]) emit_block<N>(img, p, zp[b], blw[b], a.rle);
+            p += rbits[b];
         }
-        sink.finish();
     }
-    __syncthreads();
+    lds_barrier();
+    asm volatile("; PHASE emit_done" ::: "memory");
+    STAMP(7);
 
     // ---------------------------------------------------------------- 3. look-back
     const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
     uint32_t* out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
-    if (tid == 0) {
-        const uint32_t my_tail = image_tail32(img, A);
-        if (chain_pos == 0) {
-            // chain start: the bits before start_bit belong to the caller (header); keep them
-            const uint64_t P = a.start_bit;
-            const uint32_t s = uint32_t(P & 31);
-            const uint32_t ptail = s ? (bswap32(out[P >> 5]) >> (32 - s)) : 0u;
-            const uint32_t tl = (A >= 32) ? my_tail : ((A ? (ptail << A) : ptail) | my_tail);
-            st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
-            st_state(&a.st[2 * t + 1], (uint64_t(a.tag) << 56) | (uint64_t(A) & kMask56));
-            misc[5] = 0;
-            misc[6] = 0;
-            misc[7] = ptail;
-        } else if (A >= 32) {
-            st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | my_tail);
-        }
-    }
-    if (chain_pos != 0 && (a.ablate & 4)) {
+    uint64_t excl;
+    if (a.ablate & 4) {
         if (tid == 0) {
-            st_state(&a.st[2 * t + 1], (uint64_t(a.tag) << 56) | (uint64_t(A) & kMask56));
-            misc[5] = uint32_t(uint64_t(tif) * 110000u);
-            misc[6] = 0;
-            misc[7] = 0;
+            publish(a.st, t, 1, a.tag, A);
+            ctl[7] = 0;
         }
-    } else if (chain_pos != 0) {
-        uint32_t ptail;
-        const uint64_t excl = lookback_wg(a.st, t, chain_pos, step, a.tag, &ptail, a.err, misc + 8);
-        if (tid == 0) {
-            if (A < 32) {
-                // a short tile publishes its tail only now: it must carry predecessor bits
-                const uint32_t tl = (A ? (ptail << A) : ptail) | image_tail32(img, A);
-                st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
-            }
-            st_state(&a.st[2 * t + 1], (uint64_t(a.tag) << 56) | ((excl + A) & kMask56));
-            misc[5] = uint32_t(excl);
-            misc[6] = uint32_t(excl >> 32);
-            misc[7] = ptail;
-        }
+        lds_barrier();
+        excl = uint64_t(tif) * (110u * TPB);
+    } else {
+        excl = chain_resolve(a.st, t, chain_pos, step, a.tag, img, A, out, a.start_bit, a.err, ctl, pr,
+                             a.stamps ? &a.stamps[size_t(t) * kStamps + 1] : nullptr);
     }
-    __syncthreads();
-    const uint64_t excl = uint64_t(misc[5]) | (uint64_t(misc[6]) << 32);
     if (tid == 0) {
         const uint64_t P = a.start_bit + excl;
         if (tif == 0) a.frame_start[frame] = P;
         if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
     }
+    asm volatile("; PHASE lookback_done" ::: "memory");
+    STAMP(8);
 
     // ---------------------------------------------------------------- 4. store
-    if (!(a.ablate & 8)) store_image(out, img, A, a.start_bit + excl, misc[7], chain_last);
+    if (!(a.ablate & 8)) store_image<TPB>(out, img, A, a.start_bit + excl, ctl[7], chain_last);
+    STAMP(9);
 }
 
+int encode_blocks_per_thread(int n) { return n == 4 ? Geo<4>::BPT : Geo<8>::BPT; }
+
+int encode_threads_per_tile() { return kEncTPB; }
+
 void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s) {
-    const dim3 grid(a.ntiles), block(kTPB);
+    const dim3 grid(a.ntiles), block(kEncTPB);
     if (n == 4) {
         if (exact) hipLaunchKernelGGL((encode_kernel<4, true>), grid, block, 0, s, a, a.tab);
         else hipLaunchKernelGGL((encode_kernel<4, false>), grid, block, 0, s, a, a.tab);

@@ -97,6 +97,9 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
 
     uint32_t A;
     const uint32_t off = block_excl_scan(mybits, misc, &A);
+    if (tid == 0) chain_publish_count(a.st, t, t, a.tag, A);
+    Probe pr{0, 0, 0};
+    if (tid < 64 && t != 0) pr = probe_issue(a.st, t, t, 1, 0);
     const uint32_t nw = (A + 31) >> 5;
     for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
     __syncthreads();
@@ -109,39 +112,9 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     }
     __syncthreads();
 
-    // look-back (a single chain in ticket order) -- same protocol as encode_kernel
+    // one chain in tile order -- the same protocol as encode_kernel
     const bool last = (t == a.ntiles - 1);
-    if (tid == 0) {
-        const uint32_t my_tail = image_tail32(img, A);
-        if (t == 0) {
-            const uint32_t s = uint32_t(a.start_bit & 31);
-            const uint32_t ptail = s ? (bswap32(a.out[a.start_bit >> 5]) >> (32 - s)) : 0u;
-            const uint32_t tl = (A >= 32) ? my_tail : ((A ? (ptail << A) : ptail) | my_tail);
-            st_state(&a.st[0], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
-            st_state(&a.st[1], (uint64_t(a.tag) << 56) | (uint64_t(A) & kMask56));
-            misc[5] = 0;
-            misc[6] = 0;
-            misc[7] = ptail;
-        } else if (A >= 32) {
-            st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | my_tail);
-        }
-    }
-    if (t != 0) {
-        uint32_t ptail;
-        const uint64_t excl = lookback_wg(a.st, t, t, 1, a.tag, &ptail, a.err, misc + 8);
-        if (tid == 0) {
-            if (A < 32) {
-                const uint32_t tl = (A ? (ptail << A) : ptail) | image_tail32(img, A);
-                st_state(&a.st[2 * t], (uint64_t(a.tag) << 56) | (uint64_t(A) << 32) | tl);
-            }
-            st_state(&a.st[2 * t + 1], (uint64_t(a.tag) << 56) | ((excl + A) & kMask56));
-            misc[5] = uint32_t(excl);
-            misc[6] = uint32_t(excl >> 32);
-            misc[7] = ptail;
-        }
-    }
-    __syncthreads();
-    const uint64_t excl = uint64_t(misc[5]) | (uint64_t(misc[6]) << 32);
+    const uint64_t excl = chain_resolve(a.st, t, t, 1, a.tag, img, A, a.out, a.start_bit, a.err, misc, pr);
     if (tid == 0 && last) a.chain_end[0] = a.start_bit + excl + A;
     store_image(a.out, img, A, a.start_bit + excl, misc[7], last);
 }
