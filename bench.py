@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--mode", default="fast", choices=["fast", "exact"])
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-iters", type=int, default=4)
+    p.add_argument("--single-frame", action="store_true",
+                   help="also time one-image launches (the latency of a single 4K encode)")
     return p.parse_args()
 
 
@@ -215,16 +217,16 @@ def main():
             _, g2 = timer.run(enc_only, 1, args.steps)
             enc_s = g2 / args.steps
             extra["huffman_bytes_per_image"] = int(sum(hsizes) / max(len(hsizes), 1))
-        # one 4K frame per launch: the latency of the single-image configuration
-        one = outs[0][:pitch]
+        if args.single_frame:  # one 4K frame per launch: the latency of the single-image configuration
+            one = outs[0][:pitch]
 
-        def single(i):
-            f = i % R
-            codec.encode_images(frames[f:f + 1], w, h, one, out_pitch=pitch, nframes=1, start_bit=hdr_bits,
-                                mode=mode, want_sizes=False)
-        _, g1 = timer.run(single, 2, 4 * B)
-        extra["single_frame"] = {"us_per_frame": round(g1 / (4 * B) * 1e6, 2),
-                                 "Mpx_s": round(w * h / (g1 / (4 * B)) / 1e6, 1)}
+            def single(i):
+                f = i % R
+                codec.encode_images(frames[f:f + 1], w, h, one, out_pitch=pitch, nframes=1, start_bit=hdr_bits,
+                                    mode=mode, want_sizes=False)
+            _, g1 = timer.run(single, 2, 4 * B)
+            extra["single_frame"] = {"us_per_frame": round(g1 / (4 * B) * 1e6, 2),
+                                     "Mpx_s": round(w * h / (g1 / (4 * B)) / 1e6, 1)}
         workload = (f"{args.workload}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
                     f"{' +Huffman' if cfg['huffman'] else ''}, batch of {B} independent images per step, "
                     f"{R} distinct resident frames per GPU ({R * w * h / 2**20:.0f} MiB)")

@@ -35,7 +35,8 @@ struct ie_ctx {
     uint64_t* d_frame_start = nullptr;  // [cap_frames]
     uint64_t* d_chain_end = nullptr;    // [cap_frames]
     size_t cap_frames = 0;
-    unsigned* d_err = nullptr;          // [0] look-back timeouts, [2..65] fallback counters
+    unsigned* d_err = nullptr;          // [0] look-back timeouts, [2..65] fallback counters (cumulative)
+    unsigned err_seen[66] = {};         // counter values at the previous read
     bool use_ticket = false;            // order tiles with an atomic ticket (after a timeout)
 
     // staging for host-resident inputs / outputs
@@ -291,19 +292,21 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
         HIPCHK(c, hipMalloc(&c->d_chain_end, cap * sizeof(uint64_t)));
         c->cap_frames = cap;
     }
-    HIPCHK(c, hipMemsetAsync(c->d_err, 0, kErrWords * sizeof(unsigned), c->stream));
     return IE_OK;
 }
 
 // [0] look-back timeouts; sum of [2..65] = FP64 re-evaluations.  Synchronises the stream.
+// The device counters only ever grow (no per-launch reset kernel in the launch path); a read
+// reports the increments since the previous read.
 int read_errors(ie_ctx* c, unsigned* timeouts, uint64_t* fallbacks) {
     unsigned e[kErrWords];
     HIPCHK(c, hipMemcpyAsync(e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     uint64_t f = 0;
-    for (int i = 2; i < kErrWords; i++) f += e[i];
-    if (timeouts) *timeouts = e[0];
+    for (int i = 2; i < kErrWords; i++) f += unsigned(e[i] - c->err_seen[i]);
+    if (timeouts) *timeouts = e[0] - c->err_seen[0];
     if (fallbacks) *fallbacks = f;
+    std::memcpy(c->err_seen, e, sizeof(e));
     return IE_OK;
 }
 
@@ -573,6 +576,7 @@ int ie_create(int device, ie_ctx** out) {
     if (r == IE_OK) chk(hipMalloc(&c->d_ticket, sizeof(unsigned long long)), "hipMalloc(ticket)");
     if (r == IE_OK) chk(hipMemset(c->d_ticket, 0, sizeof(unsigned long long)), "hipMemset(ticket)");
     if (r == IE_OK) chk(hipMalloc(&c->d_err, kErrWords * sizeof(unsigned)), "hipMalloc(err)");
+    if (r == IE_OK) chk(hipMemset(c->d_err, 0, kErrWords * sizeof(unsigned)), "hipMemset(err)");
     if (r == IE_OK) chk(hipMalloc(&c->d_code, 2 * 256 * sizeof(uint32_t)), "hipMalloc(code)");
     if (r == IE_OK) chk(hipHostMalloc(&c->h_code, 2 * 256 * sizeof(uint32_t)), "hipHostMalloc(code)");
     if (r == IE_OK) chk(hipMalloc(&c->d_hist, 256 * sizeof(uint32_t)), "hipMalloc(hist)");
@@ -692,8 +696,10 @@ int ie_quantize_frames(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride,
 int ie_last_fallbacks(ie_ctx* c, uint64_t* count) {
     if (!c || !count) return IE_EINVAL;
     unsigned timeouts = 0;
-    int r = read_errors(c, &timeouts, &c->last_fallbacks);
+    uint64_t fresh = 0;  // requests since the last read (launches that did not read back)
+    int r = read_errors(c, &timeouts, &fresh);
     if (r) return r;
+    if (fresh) c->last_fallbacks = fresh;
     *count = c->last_fallbacks;
     if (timeouts) return fail(c, IE_EDEVICE, "tile look-back timed out");
     return IE_OK;

@@ -149,12 +149,20 @@ struct Probe {
     uint64_t gi, ga, gt;
 };
 
-__device__ __forceinline__ Probe probe_issue(const uint64_t* st, int t, int chain_pos, int step, int d0) {
+// First probe window: most tiles find an inclusive prefix among their nearest predecessors, and
+// every probed state is an uncached agent-scope load, so the first round reads only a few.
+#ifndef IE_PROBE0
+#define IE_PROBE0 8
+#endif
+constexpr int kProbe0 = IE_PROBE0;
+
+__device__ __forceinline__ Probe probe_issue(const uint64_t* st, int t, int chain_pos, int step, int d0,
+                                             int width) {
     Probe p;
     p.gi = p.ga = p.gt = 0;
     const int lane = lane_id();
     const int d = d0 + lane;
-    if (chain_pos - 1 - d >= 0) {
+    if (lane < width && chain_pos - 1 - d >= 0) {
         const int idx = t - step * (d + 1);
         p.gi = ld_state(&st[kGran * idx + 1]);
         p.ga = ld_state(&st[kGran * idx]);
@@ -163,21 +171,24 @@ __device__ __forceinline__ Probe probe_issue(const uint64_t* st, int t, int chai
     return p;
 }
 
-// Exclusive prefix of tile t, executed by ONE wave from a first probe: the sum of aggregates up
-// to the nearest inclusive value (normally inside the first window: predecessors publish their
-// aggregate as soon as their bit count is known).  Returns the prefix in every lane.
+// Exclusive prefix of tile t, executed by ONE wave from a first probe (width kProbe0): the sum of
+// aggregates up to the nearest inclusive value (predecessors publish their aggregate as soon as
+// their bit count is known).  Later windows read 64 predecessors.  Returns the prefix in every
+// lane.
 __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
                                   unsigned* err, unsigned* rounds = nullptr) {
     const int lane = lane_id();
     uint64_t excl = 0;
-    int d0 = 0;
+    int d0 = 0, width = kProbe0;
     unsigned spins = 0;
     if (rounds) *rounds = 0;
     for (;;) {
         const int d = d0 + lane;
         int status = 2;  // before the chain start: a virtual inclusive prefix of 0
         uint64_t val = 0;
-        if (chain_pos - 1 - d >= 0) {
+        if (lane >= width) {
+            status = 3;  // outside the window
+        } else if (chain_pos - 1 - d >= 0) {
             if (uint32_t(p.gi >> 56) == tag) {
                 val = p.gi & kMask56;
             } else {
@@ -186,7 +197,7 @@ __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_
             }
         }
         const uint64_t incl = __ballot(status == 2);
-        const int dP = incl ? (__ffsll((unsigned long long)incl) - 1) : 64;
+        const int dP = incl ? (__ffsll((unsigned long long)incl) - 1) : width;
         const uint64_t before = (dP < 64) ? ((1ull << dP) - 1ull) : ~0ull;
         if (__ballot(status == 0) & before) {
             if (++spins > kSpinLimit) {
@@ -194,14 +205,15 @@ __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_
                 return excl;
             }
             __builtin_amdgcn_s_sleep(1);
-            p = probe_issue(st, t, chain_pos, step, d0);
+            p = probe_issue(st, t, chain_pos, step, d0, width);
             if (rounds) *rounds += 1;
             continue;
         }
-        excl += wave_sum64((lane <= dP) ? val : 0ull);
-        if (dP < 64) return excl;
-        d0 += 64;
-        p = probe_issue(st, t, chain_pos, step, d0);
+        excl += wave_sum64((lane <= dP && lane < width) ? val : 0ull);
+        if (dP < width) return excl;
+        d0 += width;
+        width = 64;
+        p = probe_issue(st, t, chain_pos, step, d0, width);
         if (rounds) *rounds += 0x10000;
     }
 }

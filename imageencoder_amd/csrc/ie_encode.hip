@@ -115,6 +115,23 @@ __device__ __forceinline__ int exact_coef_inl(const EncTables* __restrict__ tab,
     return int(r);
 }
 
+// The same evaluation with the coefficient's row of P and its scalars taken from an LDS copy.
+template <int N>
+__device__ __forceinline__ int exact_coef_row(const double* P, double S, double rq, double qd, const BlockPx<N>& px) {
+    constexpr int NN = N * N;
+    double acc = 0.0;
+#pragma unroll
+    for (int ij = 0; ij < NN; ij++) {
+        const double x = double(int((px.w[ij >> 2] >> (8 * (ij & 3))) & 0xFFu)) + (-128.0);
+        acc = acc + P[ij] * x;
+    }
+    const double D = acc * S;
+    const double t = (rq != 0.0) ? D * rq : D / qd;
+    double r = trunc(t);
+    if (fabs(t - r) >= 0.5) r += copysign(1.0, t);
+    return int(r);
+}
+
 // Out-of-line copy for the EXACT mode's per-coefficient loop.
 template <int N>
 __device__ __noinline__ int exact_coef(const EncTables* __restrict__ tab, int k, BlockPx<N> px) {
@@ -250,11 +267,13 @@ __device__ __forceinline__ void fix_block(const EncTables* __restrict__ tab, con
 #pragma unroll
     for (int j = 0; j < NN / 2; j++)
         res[j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
-    uint16_t* h = reinterpret_cast<uint16_t*>(res);
     while (near) {
         const int k = __ffsll((unsigned long long)near) - 1;
         near &= near - 1;
-        h[ZigZagInv<N>::pos[k]] = uint16_t(exact_coef_inl<N>(tab, k, px));
+        const int kz = ZigZagInv<N>::pos[k];
+        const uint32_t v = uint32_t(exact_coef_inl<N>(tab, k, px)) & 0xFFFFu;
+        const uint32_t w = res[kz >> 1];  // same-type read-modify-write (no uint16 aliasing)
+        res[kz >> 1] = (kz & 1) ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
     }
 }
 
@@ -408,6 +427,8 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     constexpr int IMGW = image_words<N>();
     constexpr int TPB = kEncTPB;
     __shared__ uint32_t smem[IMGW + 32];
+    // FAST mode: the structural coefficients' FP64 rows (P[3][NN], then S[3], rq[3], qd[3])
+    __shared__ double srow[3 * NN + 9];
     uint32_t* img = smem;
     uint32_t* misc = smem + IMGW;  // [0..15] scan scratch (one word per wave)
     uint32_t* ctl = misc + 16;     // [4] ticket, [5..6] exclusive prefix, [7] predecessor tail
@@ -427,11 +448,23 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
         t = int(blockIdx.x);
     }
     STAMP(0);
+    if constexpr (!EXACT) {
+        // issued before the pixel loads, so waiting for it does not wait for them
+        for (int i = tid; i < 3 * NN + 9; i += TPB) {
+            double v;
+            if (i < 3 * NN) v = tab->P[Structural<N>::k[i / NN] * NN + i % NN];
+            else if (i < 3 * NN + 3) v = tab->S[Structural<N>::k[i - 3 * NN]];
+            else if (i < 3 * NN + 6) v = tab->rq[Structural<N>::k[i - 3 * NN - 3]];
+            else v = tab->qd[Structural<N>::k[i - 3 * NN - 6]];
+            srow[i] = v;
+        }
+    }
     const TileGeo g = tile_geo<N>(a, t, tid);
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
     uint32_t seg[N][WPR];
     load_tile<N, WPR>(a, g, seg);
+    if constexpr (!EXACT) lds_barrier();  // srow visible (the pixel loads stay in flight)
 
     asm volatile("; PHASE load_done" ::: "memory");
     if (a.stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
@@ -477,81 +510,68 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     STAMP(3);
 
     // ---------------------------------------------------------------- 1b. FP64 fix-up
-    // The tile's requests are compacted into an LDS task list (owner, block, kind) beside every
-    // thread's pixel rows, so that one thread per task serves up to RR of them in as few waves
-    // as possible (the areas alias the tile image, not yet built).  Kind s < 3: structural
-    // coefficient s alone in the reference's FP64 order (a compile-time row of P, read through the
-    // scalar cache); kind 3: fix_block (every coefficient near a tie).
+    // Every lane re-evaluates its own requests in the reference's FP64 order -- no compaction,
+    // no barrier: a wave loops as long as any lane still has one.  Structural coefficient s of
+    // block b: its P row comes from the LDS copy; a whole-block request (rare): fix_block, with
+    // its per-lane result slot in the (not yet built) tile image.
     if constexpr (!EXACT) {
-        constexpr int PIXW = N * WPR;               // pixel words per thread
-        constexpr int TCAP = TPB * BPT * 3;         // worst case: every structural coefficient
-        constexpr int RFIT = (IMGW - TPB * PIXW - TCAP) / NP;
-        constexpr int RR = RFIT < TPB ? RFIT : TPB;  // tasks per round
-        static_assert(RR >= 16, "LDS fix-up area too small");
-        uint32_t T;
-        const uint32_t off0 = block_excl_scan<TPB>(__popc(flags), misc, &T);
-        if (T) {  // uniform
-            uint32_t* wpix = img;                  // [TPB][PIXW] every thread's pixel rows
-            uint32_t* wtask = wpix + TPB * PIXW;   // [T] tid | b << 12 | kind << 16
-            uint32_t* wres = wtask + TCAP;         // [RR][NP]
+        uint32_t sf = flags & (0x77777777u >> (32 - 4 * BPT));
+        while (__ballot(sf != 0)) {
+            if (sf) {
+                const int bit = __ffs(sf) - 1;
+                sf &= sf - 1;
+                const int b = bit >> 2, s = bit & 3;
+                BlockPx<N> px;
 #pragma unroll
-            for (int i = 0; i < N; i++)
+                for (int r = 0; r < N; r++)
 #pragma unroll
-                for (int m = 0; m < WPR; m++) wpix[tid * PIXW + i * WPR + m] = seg[i][m];
-            uint32_t o = off0;
+                    for (int m = 0; m < N / 4; m++) {
+                        uint32_t v = seg[r][m];
 #pragma unroll
-            for (int b = 0; b < BPT; b++)
-#pragma unroll
-                for (int s = 0; s < 4; s++)
-                    if ((flags >> (4 * b + s)) & 1u) wtask[o++] = uint32_t(tid) | (uint32_t(b) << 12) | (uint32_t(s) << 16);
-            STAMP(10);
-            lds_barrier();
-            for (uint32_t base = 0; base < T; base += RR) {
-                const uint32_t i = base + uint32_t(tid);
-                if (tid < RR && i < T) {
-                    const uint32_t task = wtask[i];
-                    const uint32_t ow = task & 0xFFFu, b = (task >> 12) & 0xFu, kind = task >> 16;
-                    BlockPx<N> px;
-#pragma unroll
-                    for (int r = 0; r < N; r++)
-#pragma unroll
-                        for (int m = 0; m < N / 4; m++)
-                            px.w[r * (N / 4) + m] = wpix[ow * PIXW + r * WPR + (b * N) / 4 + m];
-                    if (kind == 3) fix_block<N>(tab, px, wres + tid * NP);
-#pragma unroll
-                    for (int s = 0; s < 3; s++)
-                        if (kind == uint32_t(s))
-                            wres[tid * NP] = uint32_t(exact_coef_inl<N>(tab, Structural<N>::k[s], px)) & 0xFFFFu;
-                }
-                lds_barrier();
-                if (base == 0) STAMP(11);
-                uint32_t oo = off0;
-#pragma unroll
-                for (int b = 0; b < BPT; b++) {
-#pragma unroll
-                    for (int s = 0; s < 4; s++) {
-                        if ((flags >> (4 * b + s)) & 1u) {
-                            if (oo >= base && oo < base + RR) {
-                                const uint32_t* r = wres + (oo - base) * NP;
-                                if (s == 3) {
-#pragma unroll
-                                    for (int j = 0; j < NP; j++) zp[b][j] = r[j];
-                                } else {
-                                    const int zpos = Structural<N>::zpos(s);
-                                    const uint32_t v = r[0];
-                                    zp[b][zpos >> 1] = (zpos & 1) ? ((zp[b][zpos >> 1] & 0xFFFFu) | (v << 16))
-                                                                  : ((zp[b][zpos >> 1] & 0xFFFF0000u) | v);
-                                }
-                            }
-                            oo++;
-                        }
+                        for (int bb = 1; bb < BPT; bb++) v = (b == bb) ? seg[r][(bb * N) / 4 + m] : v;
+                        px.w[r * (N / 4) + m] = v;
                     }
-                }
-                lds_barrier();
-                if (base == 0) STAMP(12);
+                const uint32_t v = uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
+                                                              srow[3 * NN + 6 + s], px)) & 0xFFFFu;
+#pragma unroll
+                for (int bb = 0; bb < BPT; bb++)
+#pragma unroll
+                    for (int ss = 0; ss < 3; ss++) {
+                        const int zpos = Structural<N>::zpos(ss);
+                        if (b == bb && s == ss)
+                            zp[bb][zpos >> 1] = (zpos & 1) ? ((zp[bb][zpos >> 1] & 0xFFFFu) | (v << 16))
+                                                           : ((zp[bb][zpos >> 1] & 0xFFFF0000u) | v);
+                    }
             }
-            if (tid == 0) atomicAdd(&a.err[2 + (t & 63)], T);  // statistics: fix-up tasks, spread counters
         }
+        uint32_t wf = flags & (0x88888888u >> (32 - 4 * BPT));
+        unsigned nfix = __popc(flags);
+        while (__ballot(wf != 0)) {
+            if (wf) {
+                const int b = (__ffs(wf) - 1) >> 2;
+                wf &= wf - 1;
+                BlockPx<N> px;
+#pragma unroll
+                for (int r = 0; r < N; r++)
+#pragma unroll
+                    for (int m = 0; m < N / 4; m++) {
+                        uint32_t v = seg[r][m];
+#pragma unroll
+                        for (int bb = 1; bb < BPT; bb++) v = (b == bb) ? seg[r][(bb * N) / 4 + m] : v;
+                        px.w[r * (N / 4) + m] = v;
+                    }
+                uint32_t* res = img + tid * NP;  // this lane's slot (the image is built later)
+                fix_block<N>(tab, px, res);
+#pragma unroll
+                for (int bb = 0; bb < BPT; bb++)
+                    if (b == bb) {
+#pragma unroll
+                        for (int j = 0; j < NP; j++) zp[bb][j] = res[j];
+                    }
+            }
+        }
+        const unsigned wsum = unsigned(wave_sum64(nfix));  // statistics: fix-up requests, spread counters
+        if ((tid & 63) == 0 && wsum) atomicAdd(&a.err[2 + ((t * 4 + (tid >> 6)) & 63)], wsum);
     }
     asm volatile("; PHASE fix_done" ::: "memory");
     STAMP(4);
@@ -576,14 +596,15 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     }
     asm volatile("; PHASE size_done" ::: "memory");
     STAMP(5);
-    lds_barrier();  // the fix-up areas alias the tile image
+    // (the fix-up slots alias the tile image: the scan's barrier below orders them before the
+    // image is zeroed)
 
     // ---------------------------------------------------------------- 2. tile scan + LDS image
     uint32_t A;
     const uint32_t off = block_excl_scan<TPB>(mybits, misc, &A);
     if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);  // successors may resolve now
     Probe pr{0, 0, 0};
-    if (tid < 64 && chain_pos != 0 && !(a.ablate & 4)) pr = probe_issue(a.st, t, chain_pos, step, 0);  // in flight during emission
+    if (tid < 64 && chain_pos != 0 && !(a.ablate & 4)) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);  // in flight during emission
     const uint32_t nw = (A + 31) >> 5;
     for (uint32_t w = tid; w < nw + 2; w += TPB) img[w] = 0u;
     lds_barrier();

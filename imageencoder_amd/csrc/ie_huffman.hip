@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     const uint32_t off = block_excl_scan(mybits, misc, &A);
     if (tid == 0) chain_publish_count(a.st, t, t, a.tag, A);
     Probe pr{0, 0, 0};
-    if (tid < 64 && t != 0) pr = probe_issue(a.st, t, t, 1, 0);
+    if (tid < 64 && t != 0) pr = probe_issue(a.st, t, t, 1, 0, kProbe0);
     const uint32_t nw = (A + 31) >> 5;
     for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
     __syncthreads();
