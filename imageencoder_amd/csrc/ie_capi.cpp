@@ -35,7 +35,9 @@ struct ie_ctx {
     uint64_t* d_frame_start = nullptr;  // [cap_frames]
     uint64_t* d_chain_end = nullptr;    // [cap_frames]
     size_t cap_frames = 0;
-    unsigned* d_err = nullptr;          // [0] look-back timeouts, [2..65] fallback counters (cumulative)
+    unsigned* d_err = nullptr;          // [0] look-back timeouts (cumulative)
+    uint32_t* d_wave_fix = nullptr;     // [cap_tiles * waves per tile] fix-up requests of the last launch
+    int last_fix_words = 0;
     unsigned err_seen[66] = {};         // counter values at the previous read
     bool use_ticket = false;            // order tiles with an atomic ticket (after a timeout)
 
@@ -272,6 +274,8 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
         }
         const size_t cap = std::max<size_t>(ntiles, c->cap_tiles * 2);
         HIPCHK(c, hipMalloc(&c->d_state, 3 * cap * sizeof(uint64_t)));
+        if (c->d_wave_fix) HIPCHK(c, hipFree(c->d_wave_fix));
+        HIPCHK(c, hipMalloc(&c->d_wave_fix, cap * 16 * sizeof(uint32_t)));
         HIPCHK(c, hipMemsetAsync(c->d_state, 0, 3 * cap * sizeof(uint64_t), c->stream));
         c->cap_tiles = cap;
         c->tag = 0;
@@ -303,7 +307,11 @@ int read_errors(ie_ctx* c, unsigned* timeouts, uint64_t* fallbacks) {
     HIPCHK(c, hipMemcpyAsync(e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     uint64_t f = 0;
-    for (int i = 2; i < kErrWords; i++) f += unsigned(e[i] - c->err_seen[i]);
+    if (fallbacks && c->last_fix_words) {
+        std::vector<uint32_t> w(size_t(c->last_fix_words));
+        HIPCHK(c, hipMemcpy(w.data(), c->d_wave_fix, w.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (uint32_t v : w) f += v;
+    }
     if (timeouts) *timeouts = e[0] - c->err_seen[0];
     if (fallbacks) *fallbacks = f;
     std::memcpy(c->err_seen, e, sizeof(e));
@@ -419,6 +427,8 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.frame_start = c->d_frame_start;
     a.chain_end = c->d_chain_end;
     a.err = c->d_err;
+    a.wave_fix = c->d_wave_fix;
+    c->last_fix_words = (mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
     a.tab = c->d_tab;
     a.coef = coef;
     static const int ablate = getenv("IE_ABLATE") ? atoi(getenv("IE_ABLATE")) : 0;  // profiling only
@@ -603,6 +613,7 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_frame_start);
     (void)hipFree(c->d_chain_end);
     (void)hipFree(c->d_err);
+    (void)hipFree(c->d_wave_fix);
     (void)hipFree(c->d_in);
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_scratch);
@@ -696,10 +707,8 @@ int ie_quantize_frames(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride,
 int ie_last_fallbacks(ie_ctx* c, uint64_t* count) {
     if (!c || !count) return IE_EINVAL;
     unsigned timeouts = 0;
-    uint64_t fresh = 0;  // requests since the last read (launches that did not read back)
-    int r = read_errors(c, &timeouts, &fresh);
+    int r = read_errors(c, &timeouts, &c->last_fallbacks);  // the last encode launch's requests
     if (r) return r;
-    if (fresh) c->last_fallbacks = fresh;
     *count = c->last_fallbacks;
     if (timeouts) return fail(c, IE_EDEVICE, "tile look-back timed out");
     return IE_OK;

@@ -55,7 +55,8 @@ struct EncArgs {
     uint32_t tag;            // epoch tag 1..255
     uint64_t* frame_start;   // [nframes] absolute start bit of each frame's payload
     uint64_t* chain_end;     // [nchains] absolute end bit
-    unsigned* err;           // [0] look-back timeouts, [2..65] fallback coefficient counters
+    unsigned* err;           // [0] look-back timeouts (atomic, only ever on a timeout)
+    uint32_t* wave_fix;      // [ntiles * kTPB/64] FP64 fix-up requests per wave (plain stores, statistics)
     const EncTables* tab;
     int16_t* coef;           // optional: quantised coefficients, natural order, [nframes*bx*by][N*N]
     int ablate;              // profiling only (IE_ABLATE): 1 no FP64, 2 no emission, 4 no look-back, 8 no store, 16 no DCT

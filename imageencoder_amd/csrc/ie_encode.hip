@@ -418,6 +418,47 @@ __device__ __forceinline__ void load_tile(const EncArgs& a, const TileGeo& g, ui
         if (a.stamps && tid == 0) a.stamps[size_t(t) * kStamps + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
+// Emission through a per-lane 64-bit accumulator: whole words are ORed into the (zeroed) image
+// as they complete, so a lane issues ~one LDS operation per 32 output bits instead of two per field.
+#ifndef IE_EMIT_SINK
+#define IE_EMIT_SINK 0
+#endif
+struct WordSink {
+    uint32_t* img;
+    uint64_t acc;
+    uint32_t n;   // bits in acc not yet written (< 32)
+    uint32_t wi;  // word index of the next word
+    __device__ __forceinline__ WordSink(uint32_t* l, uint32_t p) : img(l), acc(0), n(p & 31u), wi(p >> 5) {}
+    __device__ __forceinline__ void put(uint32_t len, uint32_t v) {  // len in [1, 32], v < 2^len
+        acc = (acc << len) | v;
+        n += len;
+        if (n >= 32) {
+            n -= 32;
+            atomicOr(&img[wi], uint32_t(acc >> n));
+            wi++;
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if (n) atomicOr(&img[wi], uint32_t(acc << (32 - n)));
+    }
+};
+
+template <int N>
+__device__ __forceinline__ void emit_block_sink(WordSink& k, const uint32_t (&zp)[N * N / 2], uint32_t blw, int rle) {
+    const uint32_t bl = blw & 0xFFu, lw = blw >> 8;
+    const uint32_t m = (1u << bl) - 1u;
+    if (rle) k.put(4u + bl, ((bl & 0xFu) << bl) | lw);
+    else k.put(4u, bl & 0xFu);
+#pragma unroll
+    for (int j = 0; j < N * N / 2; j++) {
+        if (uint32_t(2 * j) < lw) {
+            const uint32_t lo = zp[j] & m, hi = (zp[j] >> 16) & m;
+            if (uint32_t(2 * j + 1) < lw) k.put(2u * bl, (lo << bl) | hi);
+            else k.put(bl, lo);
+        }
+    }
+}
+
 template <int N, bool EXACT>
 __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     constexpr int NN = N * N;
@@ -570,8 +611,9 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
                     }
             }
         }
-        const unsigned wsum = unsigned(wave_sum64(nfix));  // statistics: fix-up requests, spread counters
-        if ((tid & 63) == 0 && wsum) atomicAdd(&a.err[2 + ((t * 4 + (tid >> 6)) & 63)], wsum);
+        // statistics: one plain store per wave (a shared atomic counter would serialise the waves)
+        const unsigned wsum = unsigned(wave_sum64(nfix));
+        if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
     }
     asm volatile("; PHASE fix_done" ::: "memory");
     STAMP(4);
@@ -611,11 +653,21 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     asm volatile("; PHASE scan_done" ::: "memory");
     STAMP(6);
     if (!(a.ablate & 2)) {
-        uint32_t p = off;
+        if (IE_EMIT_SINK) {
+            if (mybits) {
+                WordSink k(img, off);
 #pragma unroll
-        for (int b = 0; b < BPT; b++) {
-            if (rbits[b]) emit_block<N>(img, p, zp[b], blw[b], a.rle);
-            p += rbits[b];
+                for (int b = 0; b < BPT; b++)
+                    if (rbits[b]) emit_block_sink<N>(k, zp[b], blw[b], a.rle);
+                k.finish();
+            }
+        } else {
+            uint32_t p = off;
+#pragma unroll
+            for (int b = 0; b < BPT; b++) {
+                if (rbits[b]) emit_block<N>(img, p, zp[b], blw[b], a.rle);
+                p += rbits[b];
+            }
         }
     }
     lds_barrier();

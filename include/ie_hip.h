@@ -98,9 +98,8 @@ int ie_encode_images(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride,
 int ie_quantize_frames(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch,
                        int nframes, int mode, int16_t* coef);
 
-/* Fallback statistics of the last FAST-mode encode that read its results back (or of the
- * asynchronous launches since): FP64 re-evaluation requests (one per structural coefficient at a
- * tie, one per block with another coefficient near a tie). */
+/* Fallback statistics of the last FAST-mode encode launch: FP64 re-evaluation requests (one per
+ * structural coefficient at a tie, one per block with another coefficient near a tie). */
 int ie_last_fallbacks(ie_ctx* ctx, uint64_t* count);
 
 /* ---- Device memory on the context's stream (for hosts that keep streams device-resident
