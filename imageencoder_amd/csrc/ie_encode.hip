@@ -229,6 +229,33 @@ __device__ __forceinline__ float round_block(const EncTables* __restrict__ tab, 
     return emax;
 }
 
+// 8x8: round as above, but flag every coefficient on its own (bit k of the returned mask: its
+// residual reaches lim[k]).  The fix-up then re-evaluates single coefficients and never
+// recomputes a whole 8x8 block, whose 64 live quotients would spill next to the 32 packed words.
+template <int N>
+__device__ __forceinline__ uint64_t round_block_mask(const EncTables* __restrict__ tab, const float (&t)[N * N],
+                                                     uint32_t (&zp)[N * N / 2]) {
+    constexpr int NN = N * N;
+    static_assert(NN <= 64, "one mask bit per coefficient");
+    uint32_t yb[NN];
+    uint64_t near = 0;
+#pragma unroll
+    for (int k = 0; k < NN; k++) {
+        const float y = t[k] + kMagic;
+        const float e = fabsf(t[k] - (y - kMagic));
+        yb[k] = __float_as_uint(y);
+        near |= uint64_t(e >= tab->lim[k]) << k;
+    }
+    if (tab->dc_exact) {
+        yb[0] = uint32_t(int(truncf(t[0] + copysignf(0.5f, t[0]))));
+        near &= ~1ull;
+    }
+#pragma unroll
+    for (int j = 0; j < NN / 2; j++)
+        zp[j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
+    return near;
+}
+
 template <int N, int WPR>
 __device__ __forceinline__ void block_pixels(const uint32_t (&seg)[N][WPR], int b, float (&x)[N * N]) {
 #pragma unroll
@@ -489,7 +516,7 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
         t = int(blockIdx.x);
     }
     STAMP(0);
-    if constexpr (!EXACT) {
+    if constexpr (!EXACT && N == 4) {
         // issued before the pixel loads, so waiting for it does not wait for them
         for (int i = tid; i < 3 * NN + 9; i += TPB) {
             double v;
@@ -505,7 +532,7 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
     uint32_t seg[N][WPR];
     load_tile<N, WPR>(a, g, seg);
-    if constexpr (!EXACT) lds_barrier();  // srow visible (the pixel loads stay in flight)
+    if constexpr (!EXACT && N == 4) lds_barrier();  // srow visible (the pixel loads stay in flight)
 
     asm volatile("; PHASE load_done" ::: "memory");
     if (a.stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
@@ -521,6 +548,7 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     uint32_t zp[BPT][NP];
     // fix-up requests, 4 bits per block: bits 0-2 structural coefficient s, bit 3 the whole block
     uint32_t flags = 0;
+    uint64_t near8 = 0;  // 8x8: per-coefficient requests of the lane's one block
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
         __builtin_amdgcn_sched_barrier(0);  // one block at a time: keeps the live set small
@@ -539,6 +567,12 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
             float x[NN];
             block_pixels<N, WPR>(seg, b, x);
             if (!(a.ablate & 16)) quotients<N>(tab, x);
+            if constexpr (N == 8) {
+                static_assert(BPT == 1, "8x8: one block per lane");
+                near8 = round_block_mask<N>(tab, x, zp[b]);
+                if (b >= nblk || (a.ablate & 1)) near8 = 0;
+                continue;
+            }
             uint32_t sf;
             const float emax = round_block<N>(tab, x, zp[b], &sf);
             uint32_t fb = (emax >= tab->lim_min) ? 8u : sf;  // a whole-block fix covers s
@@ -555,7 +589,30 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     // no barrier: a wave loops as long as any lane still has one.  Structural coefficient s of
     // block b: its P row comes from the LDS copy; a whole-block request (rare): fix_block, with
     // its per-lane result slot in the (not yet built) tile image.
-    if constexpr (!EXACT) {
+    if constexpr (!EXACT && N == 8) {
+        // 8x8: one coefficient per request, its FP64 row from the (L2-resident) table
+        uint64_t nr = near8;
+        const unsigned nfix = unsigned(__popcll(near8));
+        while (__ballot(nr != 0)) {
+            if (nr) {
+                const int k = __ffsll((unsigned long long)nr) - 1;
+                nr &= nr - 1;
+                BlockPx<N> px;
+#pragma unroll
+                for (int r = 0; r < N; r++)
+#pragma unroll
+                    for (int m = 0; m < N / 4; m++) px.w[r * (N / 4) + m] = seg[r][m];
+                const uint32_t v = uint32_t(exact_coef_inl<N>(tab, k, px)) & 0xFFFFu;
+                const int kz = ZigZagInv<N>::pos[k];
+#pragma unroll
+                for (int j = 0; j < NP; j++)
+                    if ((kz >> 1) == j)
+                        zp[0][j] = (kz & 1) ? ((zp[0][j] & 0xFFFFu) | (v << 16)) : ((zp[0][j] & 0xFFFF0000u) | v);
+            }
+        }
+        const unsigned wsum = unsigned(wave_sum64(nfix));
+        if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
+    } else if constexpr (!EXACT) {
         uint32_t sf = flags & (0x77777777u >> (32 - 4 * BPT));
         while (__ballot(sf != 0)) {
             if (sf) {
