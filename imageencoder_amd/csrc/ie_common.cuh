@@ -249,7 +249,7 @@ __device__ __forceinline__ void chain_publish_count(uint64_t* st, int t, int cha
 __device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
                                                   const uint32_t* img, uint32_t A, const uint32_t* out,
                                                   uint64_t start, unsigned* err, uint32_t* misc, const Probe& pr,
-                                                  uint64_t* dbg = nullptr) {
+                                                  uint64_t* dbg = nullptr, bool defer_tail = false) {
     const int tid = threadIdx.x;
     if (tid == 0) {
         const uint32_t my_tail = image_tail32(img, A);
@@ -262,6 +262,7 @@ __device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain
             misc[5] = 0;
             misc[6] = 0;
             misc[7] = ptail;
+            misc[8] = 0;
         } else if (A >= 32) {
             publish(st, t, 2, tag, my_tail);
         }
@@ -271,8 +272,12 @@ __device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain
         const uint64_t excl = lookback_wave(pr, st, t, chain_pos, step, tag, err, dbg ? &rounds : nullptr);
         if (tid == 0) {
             publish(st, t, 1, tag, excl + A);
-            const uint32_t ptail = (uint32_t(pr.gt >> 56) == tag) ? uint32_t(pr.gt)
-                                                                  : wait_tail(st, t - step, tag, err, &polls);
+            const bool have = uint32_t(pr.gt >> 56) == tag;
+            // deferred: only the tile's first output word needs the predecessor's tail, and only
+            // when the tile starts inside a word; store_tile() fetches it after the bulk store
+            const bool later = defer_tail && !have && A >= 32 && ((start + excl) & 31) != 0;
+            const uint32_t ptail = have ? uint32_t(pr.gt) : later ? 0u : wait_tail(st, t - step, tag, err, &polls);
+            misc[8] = later ? 1u : 0u;
             if (dbg) *dbg = (uint64_t(rounds) << 32) | polls;
             if (A < 32) {
                 // a short tile's tail carries predecessor bits
@@ -291,36 +296,67 @@ __device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain
 // array out.  Word floor(P/32) is completed with `prev` (the 32 bits that precede bit P,
 // right-aligned).  The last partial word is left to the successor unless `last`.  Aligned runs of
 // four words go out as one 16-byte store per thread (TPB threads).
+#ifndef IE_NT_STORE
+#define IE_NT_STORE 1
+#endif
 template <int TPB = kTPB>
 __device__ __forceinline__ void store_image(uint32_t* out, const uint32_t* L, uint32_t bits, uint64_t P,
-                                            uint32_t prev, bool last) {
+                                            uint32_t prev, bool last, bool skip0 = false) {
+    // Output word r (r = 0 at word floor(P/32)) is the funnel shift of image words r-1 and r:
+    // alignbit(L[r-1], L[r], s), with L[-1] = prev and s = 0 giving L[r] itself.  The caller's
+    // image is zero through word ceil(bits/32), so L[r] needs no bound check.
     const uint64_t w0 = P >> 5;
     const uint32_t s = uint32_t(P & 31);
     const uint64_t end = P + bits;
     const uint64_t w1 = last ? ((end + 31) >> 5) : (end >> 5);
-    const uint32_t nL = (bits + 31) >> 5;
     const uint32_t nw = uint32_t(w1 - w0);
-    auto word = [&](uint32_t r) -> uint32_t {
-        const uint32_t cur = (r < nL) ? L[r] : 0u;
-        const uint32_t pw = (r == 0) ? prev : L[r - 1];
-        return bswap32(s ? ((pw << (32 - s)) | (cur >> s)) : cur);
-    };
     const uint32_t tid = threadIdx.x;
-    const uint32_t head = min(nw, uint32_t((4u - uint32_t(w0 & 3u)) & 3u));
-    if (tid < head) out[w0 + tid] = word(tid);
+    auto word = [&](uint32_t r) -> uint32_t {
+        const uint32_t pw = (r == 0) ? prev : L[r - 1];
+        return bswap32(__builtin_amdgcn_alignbit(pw, L[r], s));
+    };
+    // skip0: word 0 is written later by the caller (its predecessor bits are not known yet)
+    const uint32_t head0 = min(nw, uint32_t((4u - uint32_t(w0 & 3u)) & 3u));
+    const uint32_t head = (skip0 && head0 == 0) ? min(nw, 4u) : head0;
+    if (tid < head && !(skip0 && tid == 0)) out[w0 + tid] = word(tid);
     const uint32_t nq = (nw - head) >> 2;
-#pragma unroll 4
+#pragma unroll 2
     for (uint32_t q = tid; q < nq; q += TPB) {
         const uint32_t r = head + 4u * q;
+        const uint32_t* l = L + r;
+        const uint32_t am = L[max(r, 1u) - 1u];  // branch-free: read a valid word, then select
+        const uint32_t a0 = (r == 0) ? prev : am;
+        const uint32_t b0 = l[0], b1 = l[1], b2 = l[2], b3 = l[3];
         uint4 v;
-        v.x = word(r);
-        v.y = word(r + 1);
-        v.z = word(r + 2);
-        v.w = word(r + 3);
+        v.x = bswap32(__builtin_amdgcn_alignbit(a0, b0, s));
+        v.y = bswap32(__builtin_amdgcn_alignbit(b0, b1, s));
+        v.z = bswap32(__builtin_amdgcn_alignbit(b1, b2, s));
+        v.w = bswap32(__builtin_amdgcn_alignbit(b2, b3, s));
+#if IE_NT_STORE
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u vv = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(vv, reinterpret_cast<v4u*>(out + w0 + r));
+#else
         *reinterpret_cast<uint4*>(out + w0 + r) = v;
+#endif
     }
     const uint32_t t0 = head + 4u * nq;
     if (tid < nw - t0) out[w0 + t0 + tid] = word(t0 + tid);
+}
+
+// The tile store after chain_resolve(..., defer_tail = true): the bulk of the words first, then
+// (misc[8] set) thread 0 fetches the predecessor's tail and completes the first word.
+template <int TPB = kTPB>
+__device__ __forceinline__ void store_tile(uint32_t* out, const uint32_t* L, uint32_t bits, uint64_t P,
+                                           const uint32_t* misc, bool last, const uint64_t* st, int pred,
+                                           uint32_t tag, unsigned* err) {
+    const bool pend = misc[8] != 0u;
+    store_image<TPB>(out, L, bits, P, misc[7], last, pend);
+    if (pend && threadIdx.x == 0) {
+        const uint32_t pt = wait_tail(st, pred, tag, err);
+        const uint32_t s = uint32_t(P & 31);
+        out[P >> 5] = bswap32((pt << (32 - s)) | (L[0] >> s));
+    }
 }
 
 }  // namespace ie

@@ -739,12 +739,13 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
         if (tid == 0) {
             publish(a.st, t, 1, a.tag, A);
             ctl[7] = 0;
+            ctl[8] = 0;
         }
         lds_barrier();
         excl = uint64_t(tif) * (110u * TPB);
     } else {
         excl = chain_resolve(a.st, t, chain_pos, step, a.tag, img, A, out, a.start_bit, a.err, ctl, pr,
-                             a.stamps ? &a.stamps[size_t(t) * kStamps + 1] : nullptr);
+                             a.stamps ? &a.stamps[size_t(t) * kStamps + 1] : nullptr, true);
     }
     if (tid == 0) {
         const uint64_t P = a.start_bit + excl;
@@ -755,7 +756,8 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     STAMP(8);
 
     // ---------------------------------------------------------------- 4. store
-    if (!(a.ablate & 8)) store_image<TPB>(out, img, A, a.start_bit + excl, ctl[7], chain_last);
+    if (!(a.ablate & 8))
+        store_tile<TPB>(out, img, A, a.start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err);
     STAMP(9);
 }
 
