@@ -199,11 +199,8 @@ def main():
                 out = outs[i % len(outs)]
                 ends = codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, out, out_pitch=pitch,
                                            nframes=B, start_bit=hdr_bits, mode=mode)
-                hsizes.clear()
-                for k in range(B):
-                    nb = (int(ends[k]) + 7) // 8
-                    hsizes.append(codec.huffman_encode_device(out[k * pitch:], nb,
-                                                              houts[k * hpitch:(k + 1) * hpitch]))
+                # the batch's Huffman pass: one histogram launch, host tree builds, one pack launch
+                hsizes[:] = codec.huffman_encode_batch(out, pitch, [(int(e) + 7) // 8 for e in ends], houts, hpitch)
         wall, gpu_s = timer.run(step, args.warmup, args.steps)
         px_total = world * args.steps * B * w * h
         in_bytes_per_launch = B * w * h

@@ -74,6 +74,12 @@ def load_library(path: str | None = None) -> C.CDLL:
         L.ie_huffman_hist.argtypes = [vp, u8p, C.c_size_t, u32p, u64p]
         L.ie_huffman_pack.argtypes = [vp, u8p, C.c_size_t, u32p, u8p, u8p, C.c_size_t, C.c_uint64, u64p]
         L.ie_bitcopy.argtypes = [vp, u8p, C.c_size_t, u8p, C.c_size_t, C.c_uint64]
+    if hasattr(L, "ie_huffman_hist_batch"):
+        L.ie_huffman_hist_batch.restype = C.c_int
+        L.ie_huffman_hist_batch.argtypes = [vp, u8p, C.c_size_t, u64p, C.c_int, u32p, u64p]
+        L.ie_huffman_pack_batch.restype = C.c_int
+        L.ie_huffman_pack_batch.argtypes = [vp, u8p, C.c_size_t, u64p, C.c_int, u32p, u8p, u8p, C.c_size_t, u8p,
+                                            C.c_size_t, u64p, u64p]
     if hasattr(L, "ie_decode_frames"):
         L.ie_decode_frames.argtypes = [vp, u8p, C.c_size_t, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
                                        u8p, C.c_size_t, C.c_size_t, u64p]
@@ -108,6 +114,8 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
     H.ieh_write_header.restype = C.c_int64
     H.ieh_huffman_encode_device.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t]
     H.ieh_huffman_encode_device.restype = C.c_int64
+    H.ieh_huffman_encode_device_batch.argtypes = [vp, vp, C.c_size_t, vp, C.c_int, vp, C.c_size_t, vp]
+    H.ieh_huffman_encode_device_batch.restype = C.c_int
     H.ieh_release.argtypes = [vp]
     H.ieh_release.restype = None
     for f in ("ieh_encode_image", "ieh_encode_video", "ieh_decode_image", "ieh_decode_video", "ieh_huffman_encode"):
@@ -331,6 +339,18 @@ class Codec:
         """Huffman pass from device ``data[:nbytes]`` into device ``out``; returns output bytes."""
         H = load_host_library()
         return self._host_chk(H.ieh_huffman_encode_device(self.h, _ptr(data), nbytes, _ptr(out), _nbytes(out)))
+
+    def huffman_encode_batch(self, data, in_pitch: int, sizes, out, out_pitch: int) -> list[int]:
+        """Huffman pass over a batch of device strings (string k: ``sizes[k]`` bytes at
+        ``data + k*in_pitch``) into device ``out + k*out_pitch``: one histogram launch, host tree
+        builds, one pack launch (asynchronous on the context's stream).  Returns output bytes."""
+        H = load_host_library()
+        k = len(sizes)
+        n = np.asarray(sizes, dtype=np.uint64)
+        nb = np.zeros(k, dtype=np.int64)
+        self._host_chk(H.ieh_huffman_encode_device_batch(self.h, _ptr(data), in_pitch, n.ctypes.data, k, _ptr(out),
+                                                         out_pitch, nb.ctypes.data))
+        return [int(v) for v in nb]
 
     def huffman_encode(self, data) -> bytes:
         """The Huffman post-pass alone (host or device input)."""

@@ -397,6 +397,14 @@ int64_t ieh_huffman_encode_device(ie_ctx* c, const uint8_t* din, size_t n, uint8
     return algo::huffman_device(c, din, n, out, err);
 }
 
+int ieh_huffman_encode_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count,
+                                    uint8_t* dout, size_t out_pitch, int64_t* bytes) {
+    if (!c || !din || !n || count <= 0 || !dout || !bytes) return IE_EINVAL;
+    if (!dc::is_device(c, din) || !dc::is_device(c, dout)) return IE_EINVAL;
+    std::string err;
+    return algo::huffman_device_batch(c, din, in_pitch, n, count, dout, out_pitch, bytes, err);
+}
+
 void ieh_release(ie_ctx* c) {
     std::lock_guard<std::mutex> lk(dc::g_mu);
     dc::g_scratch.erase(c);

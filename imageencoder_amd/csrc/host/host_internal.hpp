@@ -49,6 +49,8 @@ namespace algo {
 bool build_code(const uint32_t* hist, const uint64_t* first, util::BitStreamWriter& hdr, uint32_t* code,
                 uint8_t* len, uint64_t& data_bits, std::string& err);
 int64_t huffman_device(ie_ctx* c, const uint8_t* din, size_t n, dc::DeviceBuffer& out, std::string& err);
+int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count, uint8_t* dout,
+                         size_t out_pitch, int64_t* bytes, std::string& err);
 }  // namespace algo
 
 namespace dc {

@@ -14,6 +14,7 @@
 #include <memory>
 #include <queue>
 #include <stdexcept>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -158,6 +159,76 @@ int64_t huffman_device(ie_ctx* c, const uint8_t* din, size_t n, dc::DeviceBuffer
     if ((r = ie_huffman_pack(c, din, n, code, len, out.p, out.cap, dict_bits, &end))) return (err = ie_last_error(c), r);
     if (end != dict_bits + data_bits) return (err = "Huffman pack length mismatch", IE_EDEVICE);
     return int64_t(total);
+}
+
+// A batch of device-resident strings (string k: n[k] bytes at din + k*in_pitch) into
+// dout + k*out_pitch: one histogram launch, the tree builds on host threads, one pack launch.
+// bytes[k] = output length of string k.  Asynchronous after the histogram read-back.
+int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count, uint8_t* dout,
+                         size_t out_pitch, int64_t* bytes, std::string& err) {
+    const size_t K = size_t(count);
+    std::vector<uint32_t> hist(256 * K), code(256 * K);
+    std::vector<uint64_t> first(256 * K), start(K);
+    std::vector<uint8_t> len(256 * K);
+    int r;
+    if ((r = ie_huffman_hist_batch(c, din, in_pitch, n, count, hist.data(), first.data())))
+        return (err = ie_last_error(c), r);
+    std::vector<std::vector<uint8_t>> dict(K);
+    std::vector<std::string> errs(K);
+    std::vector<char> ok(K, 1);
+    auto build = [&](size_t k) {
+        uint32_t* cd = &code[256 * k];
+        uint8_t* ln = &len[256 * k];
+        if (n[k] == 0) {  // the reference pops an empty queue: the bare stop bit
+            dict[k].assign(1, 0);
+            start[k] = 1;
+            bytes[k] = 1;
+            return;
+        }
+        util::BitStreamWriter hdr(64);
+        uint64_t data_bits = 0;
+        if (!build_code(&hist[256 * k], &first[256 * k], hdr, cd, ln, data_bits, errs[k])) {
+            ok[k] = 0;
+            return;
+        }
+        const uint64_t dict_bits = hdr.get_position();
+        const uint64_t total = (dict_bits + data_bits + 7) / 8;
+        if (n[k] < total) {  // no gain: '0' + the input bytes (Huffman.cpp:329-341)
+            for (int b = 0; b < 256; b++) {
+                cd[b] = uint32_t(b);
+                ln[b] = 8;
+            }
+            dict[k].assign(1, 0);
+            start[k] = 1;
+            bytes[k] = int64_t(n[k] + 1);
+            return;
+        }
+        const size_t hb = size_t((dict_bits + 7) / 8);
+        dict[k].assign(hdr.get_buffer(), hdr.get_buffer() + hb);
+        start[k] = dict_bits;
+        bytes[k] = int64_t(total);
+    };
+    const size_t T = std::min<size_t>(K, std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+    if (T <= 1) {
+        for (size_t k = 0; k < K; k++) build(k);
+    } else {
+        std::vector<std::thread> pool;
+        for (size_t i = 0; i < T; i++)
+            pool.emplace_back([&, i] {
+                for (size_t k = i; k < K; k += T) build(k);
+            });
+        for (auto& th : pool) th.join();
+    }
+    for (size_t k = 0; k < K; k++)
+        if (!ok[k]) return (err = errs[k], IE_EINVAL);
+    size_t pp = 4;
+    for (const auto& d : dict) pp = std::max(pp, d.size());
+    std::vector<uint8_t> prefix(pp * K, 0);
+    for (size_t k = 0; k < K; k++) std::memcpy(&prefix[pp * k], dict[k].data(), dict[k].size());
+    if ((r = ie_huffman_pack_batch(c, din, in_pitch, n, count, code.data(), len.data(), prefix.data(), pp, dout,
+                                   out_pitch, start.data(), nullptr)))
+        return (err = ie_last_error(c), r);
+    return IE_OK;
 }
 
 int Huffman::encode(ie_ctx* c, const uint8_t* in, size_t n, std::vector<uint8_t>& out) {

@@ -57,6 +57,11 @@ struct ie_ctx {
     uint32_t* d_code = nullptr;        // [256] codes, then [256/4] packed lengths (one block)
     uint32_t* h_code = nullptr;        // pinned mirror
     uint32_t* d_hist = nullptr;        // [256]
+    // batched Huffman: device + pinned staging (hist/first of every string, then the pack tables)
+    uint8_t* d_batch = nullptr;
+    size_t cap_batch = 0;
+    uint8_t* h_batch = nullptr;
+    size_t cap_hbatch = 0;
     // decoder scratch
     uint8_t* d_dec = nullptr;          // staged stream + padding
     size_t cap_dec = 0;
@@ -113,6 +118,20 @@ int ensure(ie_ctx* c, T*& p, size_t& cap, size_t need_elems) {
     return IE_OK;
 }
 
+
+// pinned host staging (the stream is synchronised before an existing buffer is replaced)
+int ensure_pinned(ie_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
+    if (cap >= need && p) return IE_OK;
+    if (p) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipHostFree(p));
+        p = nullptr;
+    }
+    const size_t n = std::max(need, cap + cap / 2);
+    HIPCHK(c, hipHostMalloc(&p, n));
+    cap = n;
+    return IE_OK;
+}
 
 // ---- rigorous error bound of the FP32 fast path -----------------------------------------
 // Trk = an exact real affine form c0 + sum_k a_k x_k of the block's RAW pixels x_k in [0, 255]
@@ -620,6 +639,8 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_code);
     (void)hipHostFree(c->h_code);
     (void)hipFree(c->d_hist);
+    (void)hipFree(c->d_batch);
+    (void)hipHostFree(c->h_batch);
     (void)hipFree(c->d_first);
     (void)hipFree(c->d_dec);
     (void)hipFree(c->d_walk);
@@ -798,6 +819,141 @@ int ie_bitcopy(ie_ctx* c, const uint8_t* bytes, size_t n, uint8_t* out, size_t o
     }
     uint64_t end = 0;
     return pack(c, bytes, n, code, len, out, out_cap, start_bit, &end);
+}
+
+int ie_huffman_hist_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
+                          uint32_t* hist, uint64_t* first_pos) {
+    if (!c || !in || !n || count <= 0 || !hist || !first_pos) return IE_EINVAL;
+    if (!is_device_ptr(in)) return fail(c, IE_EINVAL, "batched Huffman input must be device memory");
+    HIPCHK(c, hipSetDevice(c->device));
+    uint64_t maxn = 0;
+    for (int k = 0; k < count; k++) {
+        if (k + 1 < count && n[k] > in_pitch) return fail(c, IE_EINVAL, "string longer than the input pitch");
+        maxn = std::max(maxn, n[k]);
+    }
+    const size_t hb = size_t(count) * 256 * sizeof(uint32_t), fb = size_t(count) * 256 * sizeof(uint64_t);
+    const size_t nb = size_t(count) * sizeof(uint64_t);
+    int r;
+    if ((r = ensure(c, c->d_batch, c->cap_batch, hb + fb + nb))) return r;
+    if ((r = ensure_pinned(c, c->h_batch, c->cap_hbatch, nb))) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the pinned staging may still feed a copy
+    std::memcpy(c->h_batch, n, nb);
+    uint32_t* dh = reinterpret_cast<uint32_t*>(c->d_batch);
+    auto* df = reinterpret_cast<unsigned long long*>(c->d_batch + hb);
+    auto* dn = reinterpret_cast<uint64_t*>(c->d_batch + hb + fb);
+    HIPCHK(c, hipMemcpyAsync(dn, c->h_batch, nb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(dh, 0, hb, c->stream));
+    HIPCHK(c, hipMemsetAsync(df, 0xFF, fb, c->stream));
+    ie::launch_hist_batch(in, in_pitch, dn, maxn, count, dh, df, c->stream);
+    HIPCHK(c, hipGetLastError());
+    const hipMemcpyKind k1 = is_device_ptr(hist) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    const hipMemcpyKind k2 = is_device_ptr(first_pos) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    HIPCHK(c, hipMemcpyAsync(hist, dh, hb, k1, c->stream));
+    HIPCHK(c, hipMemcpyAsync(first_pos, df, fb, k2, c->stream));
+    if (k1 == hipMemcpyDeviceToHost || k2 == hipMemcpyDeviceToHost) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return IE_OK;
+}
+
+int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
+                          const uint32_t* code, const uint8_t* len, const uint8_t* prefix, size_t prefix_pitch,
+                          uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit) {
+    if (!c || !in || !n || count <= 0 || !code || !len || !out || !start_bit || (!prefix && prefix_pitch))
+        return IE_EINVAL;
+    if (!is_device_ptr(in) || !is_device_ptr(out))
+        return fail(c, IE_EINVAL, "batched Huffman input and output must be device memory");
+    if (reinterpret_cast<uintptr_t>(out) % 4 || out_pitch % 4)
+        return fail(c, IE_EINVAL, "output and its pitch must be 4-byte aligned");
+    HIPCHK(c, hipSetDevice(c->device));
+    // layout of the staged tables: tile_start[count+1] n[count] start[count] code[count*256]
+    // prefix[count][pw] (words) len[count*256]
+    uint64_t pw = 1, ntiles = 0;
+    std::vector<uint64_t> ts(size_t(count) + 1);
+    for (int k = 0; k < count; k++) {
+        if (k + 1 < count && n[k] > in_pitch) return fail(c, IE_EINVAL, "string longer than the input pitch");
+        unsigned maxlen = 0;
+        for (int b = 0; b < 256; b++) {
+            if (len[256 * k + b] > 32) return fail(c, IE_EINVAL, "code length above 32 bits");
+            maxlen = std::max<unsigned>(maxlen, len[256 * k + b]);
+        }
+        const uint64_t end_bound = start_bit[k] + uint64_t(maxlen) * n[k];
+        if (out_pitch < size_t((end_bound + 31) / 32) * 4)
+            return fail(c, IE_ECAP, "output pitch below start_bit + max_len * n bits");
+        if (start_bit[k] && !prefix) return fail(c, IE_EINVAL, "start_bit > 0 needs a prefix");
+        if ((start_bit[k] + 7) / 8 > prefix_pitch && start_bit[k]) return fail(c, IE_EINVAL, "prefix pitch too small");
+        pw = std::max<uint64_t>(pw, start_bit[k] / 32 + 1);
+        ts[size_t(k)] = ntiles;
+        ntiles += (n[k] + ie::kPackTileBytes - 1) / ie::kPackTileBytes;
+    }
+    ts[size_t(count)] = ntiles;
+    if (ntiles > uint64_t(INT32_MAX)) return fail(c, IE_EINVAL, "batch too large");
+    const size_t K = size_t(count);
+    const size_t o_ts = 0, o_n = o_ts + 8 * (K + 1), o_st = o_n + 8 * K, o_code = o_st + 8 * K;
+    const size_t o_pre = o_code + 4 * 256 * K, o_len = o_pre + 4 * size_t(pw) * K, total = o_len + 256 * K;
+    int r;
+    if ((r = ensure(c, c->d_batch, c->cap_batch, total))) return r;
+    if ((r = ensure_pinned(c, c->h_batch, c->cap_hbatch, total))) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the pinned staging may still feed a copy
+    uint8_t* h = c->h_batch;
+    std::memcpy(h + o_ts, ts.data(), 8 * (K + 1));
+    std::memcpy(h + o_n, n, 8 * K);
+    std::memcpy(h + o_st, start_bit, 8 * K);
+    std::memcpy(h + o_code, code, 4 * 256 * K);
+    std::memcpy(h + o_len, len, 256 * K);
+    std::memset(h + o_pre, 0, 4 * size_t(pw) * K);
+    for (size_t k = 0; k < K; k++) {
+        const uint64_t sb = start_bit[k];
+        if (!sb) continue;
+        uint8_t* d = h + o_pre + 4 * size_t(pw) * k;
+        const size_t nbytes = size_t((sb + 7) / 8);
+        std::memcpy(d, prefix + k * prefix_pitch, nbytes);
+        if (sb % 8) d[nbytes - 1] &= uint8_t(0xFF00u >> (sb % 8));  // bits from start_bit on are the packer's
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_batch, h, total, hipMemcpyHostToDevice, c->stream));
+    const uint8_t* d = c->d_batch;
+    // strings without bytes: the prefix alone
+    for (size_t k = 0; k < K; k++)
+        if (n[k] == 0)
+            HIPCHK(c, hipMemcpyAsync(out + k * out_pitch, d + o_pre + 4 * size_t(pw) * k, 4 * size_t(start_bit[k] / 32 + 1),
+                                     hipMemcpyDeviceToDevice, c->stream));
+    if (ntiles) {
+        if ((r = prepare_state(c, int(ntiles), count))) return r;
+        ie::PackArgs a{};
+        a.in = in;
+        a.code = reinterpret_cast<const uint32_t*>(d + o_code);
+        a.len = d + o_len;
+        a.ntiles = int(ntiles);
+        a.out = reinterpret_cast<uint32_t*>(out);
+        a.st = c->d_state;
+        a.ticket = c->use_ticket ? c->d_ticket : nullptr;
+        a.ticket_base = c->ticket_base;
+        a.tag = c->tag;
+        a.chain_end = c->d_chain_end;
+        a.err = c->d_err;
+        a.count = count;
+        a.tile_start = reinterpret_cast<const uint64_t*>(d + o_ts);
+        a.bn = reinterpret_cast<const uint64_t*>(d + o_n);
+        a.bstart = reinterpret_cast<const uint64_t*>(d + o_st);
+        a.in_pitch = in_pitch;
+        a.out_pitch_words = out_pitch / 4;
+        a.prefix_pitch_words = pw;
+        a.prefix = reinterpret_cast<const uint32_t*>(d + o_pre);
+        ie::launch_pack(a, c->stream);
+        HIPCHK(c, hipGetLastError());
+        if (c->use_ticket) c->ticket_base += ntiles;
+    }
+    if (!end_bit) return IE_OK;
+    std::vector<uint64_t> ends(K);
+    if (ntiles) HIPCHK(c, hipMemcpyAsync(ends.data(), c->d_chain_end, 8 * K, hipMemcpyDeviceToHost, c->stream));
+    unsigned timeouts = 0;
+    if ((r = read_errors(c, &timeouts, nullptr))) return r;
+    if (timeouts) {
+        if (c->use_ticket) return fail(c, IE_EDEVICE, "tile look-back timed out");
+        c->use_ticket = true;
+        return ie_huffman_pack_batch(c, in, in_pitch, n, count, code, len, prefix, prefix_pitch, out, out_pitch,
+                                     start_bit, end_bit);
+    }
+    for (size_t k = 0; k < K; k++) end_bit[k] = n[k] ? ends[k] : start_bit[k];
+    return IE_OK;
 }
 
 int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,

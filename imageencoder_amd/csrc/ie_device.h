@@ -82,10 +82,25 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
     uint32_t tag;
     uint64_t* chain_end;
     unsigned* err;
+    // batch mode (count > 0): string k owns tiles [tile_start[k], tile_start[k+1]), one chain
+    // each; its bytes at in + k*in_pitch (n[k] of them), its code table at code/len + 256*k, its
+    // output at out + k*out_pitch_words from bit start[k], the words before that from
+    // prefix + k*prefix_pitch_words (e.g. the Huffman dictionary), its end bit in chain_end[k]
+    int count;
+    const uint64_t* tile_start;  // [count + 1]
+    const uint64_t* bn;          // [count]
+    const uint64_t* bstart;      // [count]
+    uint64_t in_pitch, out_pitch_words, prefix_pitch_words;
+    const uint32_t* prefix;
 };
 constexpr int kPackBytesPerThread = 16;
+constexpr int kPackTileBytes = 256 * kPackBytesPerThread;
 void launch_pack(const PackArgs& a, hipStream_t s);
 void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, hipStream_t s);
+// count strings at in + k*pitch, n[k] (device array) bytes each, maxn >= every n[k]:
+// hist/first + 256*k
+void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count, uint32_t* hist,
+                       unsigned long long* first, hipStream_t s);
 
 struct DecArgs {
     const uint64_t* block_bit;  // [nblocks] start bit of every block record (from the walk index)

@@ -19,8 +19,10 @@ namespace ie {
 
 constexpr int kHistTile = kTPB * 16;  // bytes per workgroup pass
 
-__global__ __launch_bounds__(kTPB) void hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t* hist,
-                                                     unsigned long long* first) {
+// Histogram + first occurrence of bytes [0, n) of `in`, grid-strided over workgroups
+// blockIdx.x of gridDim.x; merged into hist / first with global atomics.
+__device__ __forceinline__ void hist_body(const uint8_t* __restrict__ in, uint64_t n, uint32_t* hist,
+                                          unsigned long long* first) {
     __shared__ uint32_t h[256];
     __shared__ unsigned long long f[256];
     const int tid = threadIdx.x;
@@ -54,10 +56,31 @@ __global__ __launch_bounds__(kTPB) void hist_kernel(const uint8_t* __restrict__ 
     }
 }
 
+__global__ __launch_bounds__(kTPB) void hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t* hist,
+                                                     unsigned long long* first) {
+    hist_body(in, n, hist, first);
+}
+
+// string blockIdx.y of a batch
+__global__ __launch_bounds__(kTPB) void hist_batch_kernel(const uint8_t* __restrict__ in, uint64_t pitch,
+                                                           const uint64_t* __restrict__ n, uint32_t* hist,
+                                                           unsigned long long* first) {
+    const int k = blockIdx.y;
+    hist_body(in + uint64_t(k) * pitch, n[k], hist + 256 * k, first + 256 * k);
+}
+
 void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, hipStream_t s) {
     const uint64_t tiles = (n + kHistTile - 1) / kHistTile;
     const int grid = int(tiles < 2048 ? (tiles ? tiles : 1) : 2048);
     hipLaunchKernelGGL(hist_kernel, dim3(grid), dim3(kTPB), 0, s, in, n, hist, first);
+}
+
+void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count, uint32_t* hist,
+                       unsigned long long* first, hipStream_t s) {
+    const uint64_t tiles = (maxn + kHistTile - 1) / kHistTile;
+    const uint64_t per = (4096 + count - 1) / count;  // ~4096 workgroups over the batch
+    const int gx = int(tiles < per ? (tiles ? tiles : 1) : per);
+    hipLaunchKernelGGL(hist_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist, first);
 }
 
 // One tile = kTPB threads x kPackBytesPerThread input bytes, codes of up to 32 bits.
@@ -72,24 +95,50 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     const int tid = threadIdx.x;
     // tile order = dispatch order (see encode_kernel); the atomic ticket is the fallback
     if (a.ticket && tid == 0) misc[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
-    s_code[tid] = a.code[tid];
-    s_len[tid] = a.len[tid];
-    __syncthreads();
+    if (a.ticket) __syncthreads();
     const int t = a.ticket ? int(misc[4]) : int(blockIdx.x);
     if (t >= a.ntiles) return;
+    // the tile's string: its chain, bytes, code table and output
+    int k = 0, chain_pos = t;
+    const uint8_t* in = a.in;
+    uint64_t n = a.n, start = a.start_bit;
+    uint32_t* out = a.out;
+    const uint32_t* hdr = a.out;  // words holding the bits before `start`
+    bool last = (t == a.ntiles - 1);
+    if (a.count) {
+        int lo = 0, hi = a.count - 1;  // largest k with tile_start[k] <= t
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (a.tile_start[mid] <= uint64_t(t)) lo = mid;
+            else hi = mid - 1;
+        }
+        k = lo;
+        chain_pos = t - int(a.tile_start[k]);
+        last = uint64_t(t) + 1 == a.tile_start[k + 1];
+        in = a.in + uint64_t(k) * a.in_pitch;
+        n = a.bn[k];
+        start = a.bstart[k];
+        out = a.out + uint64_t(k) * a.out_pitch_words;
+        hdr = a.prefix + uint64_t(k) * a.prefix_pitch_words;
+        if (chain_pos == 0)  // the prefix words (the chain's bits before `start` live in hdr)
+            for (uint32_t w = tid; w < uint32_t(start >> 5); w += kTPB) out[w] = hdr[w];
+    }
+    s_code[tid] = a.code[256 * k + tid];
+    s_len[tid] = a.len[256 * k + tid];
+    __syncthreads();
 
-    const uint64_t p = uint64_t(t) * (kTPB * kPackBytesPerThread) + uint64_t(tid) * kPackBytesPerThread;
+    const uint64_t p = uint64_t(chain_pos) * (kTPB * kPackBytesPerThread) + uint64_t(tid) * kPackBytesPerThread;
     uint8_t b[kPackBytesPerThread];
     int nb = 0;
-    if (p < a.n) nb = int(min<uint64_t>(kPackBytesPerThread, a.n - p));
-    if (nb == kPackBytesPerThread && ((reinterpret_cast<uintptr_t>(a.in) & 15) == 0)) {
-        const uint4 v = *reinterpret_cast<const uint4*>(a.in + p);
+    if (p < n) nb = int(min<uint64_t>(kPackBytesPerThread, n - p));
+    if (nb == kPackBytesPerThread && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
+        const uint4 v = *reinterpret_cast<const uint4*>(in + p);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 16; e++) b[e] = uint8_t(w[e >> 2] >> (8 * (e & 3)));
     } else {
 #pragma unroll
-        for (int e = 0; e < kPackBytesPerThread; e++) b[e] = (e < nb) ? a.in[p + e] : 0;
+        for (int e = 0; e < kPackBytesPerThread; e++) b[e] = (e < nb) ? in[p + e] : 0;
     }
     uint32_t mybits = 0;
 #pragma unroll
@@ -97,9 +146,9 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
 
     uint32_t A;
     const uint32_t off = block_excl_scan(mybits, misc, &A);
-    if (tid == 0) chain_publish_count(a.st, t, t, a.tag, A);
+    if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);
     Probe pr{0, 0, 0};
-    if (tid < 64 && t != 0) pr = probe_issue(a.st, t, t, 1, 0, kProbe0);
+    if (tid < 64 && chain_pos != 0) pr = probe_issue(a.st, t, chain_pos, 1, 0, kProbe0);
     const uint32_t nw = (A + 31) >> 5;
     for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
     __syncthreads();
@@ -112,11 +161,10 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     }
     __syncthreads();
 
-    // one chain in tile order -- the same protocol as encode_kernel
-    const bool last = (t == a.ntiles - 1);
-    const uint64_t excl = chain_resolve(a.st, t, t, 1, a.tag, img, A, a.out, a.start_bit, a.err, misc, pr);
-    if (tid == 0 && last) a.chain_end[0] = a.start_bit + excl + A;
-    store_image(a.out, img, A, a.start_bit + excl, misc[7], last);
+    // one chain per string in tile order -- the same protocol as encode_kernel
+    const uint64_t excl = chain_resolve(a.st, t, chain_pos, 1, a.tag, img, A, hdr, start, a.err, misc, pr);
+    if (tid == 0 && last) a.chain_end[k] = start + excl + A;
+    store_image(out, img, A, start + excl, misc[7], last);
 }
 
 void launch_pack(const PackArgs& a, hipStream_t s) {

@@ -123,6 +123,25 @@ int ie_huffman_hist(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint32_t* hist,
 int ie_huffman_pack(ie_ctx* ctx, const uint8_t* bytes, size_t n, const uint32_t* code, const uint8_t* len,
                     uint8_t* out, size_t out_cap, uint64_t start_bit, uint64_t* end_bit);
 
+/* Batched Huffman post-pass over `count` device-resident byte strings (one encoded image each):
+ * string k is n[k] bytes at in + k*in_pitch (n: host array).  Replaces the per-image
+ * Huffman.cpp:237-243 histogram loop; hist/first_pos hold count*256 entries (string k at 256*k),
+ * host or device memory.  One launch for the whole batch. */
+int ie_huffman_hist_batch(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
+                          uint32_t* hist, uint64_t* first_pos);
+
+/* Batched re-encode (Huffman.cpp:314-319 for every string of the batch in one launch): string k
+ * with the code table code/len[256*k ...] into out + k*out_pitch from bit start_bit[k].  The
+ * bits before start_bit[k] (the dictionary, Huffman.cpp:283-311, or the '0' bit of the "no gain"
+ * copy) come from prefix + k*prefix_pitch, so `out` needs no preparation; bits of the prefix
+ * from start_bit[k] on are ignored.  in/out: device memory, out and out_pitch 4-byte aligned,
+ * out_pitch >= (start_bit[k] + max_len_k * n[k] + 31) / 32 * 4.  Host arrays n, code, len,
+ * prefix, start_bit are copied before the call returns.  end_bit (host, count entries) optional:
+ * asking for it synchronises; without it the call is asynchronous on the context's stream. */
+int ie_huffman_pack_batch(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
+                          const uint32_t* code, const uint8_t* len, const uint8_t* prefix, size_t prefix_pitch,
+                          uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit);
+
 /* Copy n bytes into out starting at bit start_bit, i.e. shifted by start_bit % 8 (the "no gain"
  * path of Huffman.cpp:329-341 writes '0' + the input: start_bit = 1). */
 int ie_bitcopy(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint8_t* out, size_t out_cap, uint64_t start_bit);

@@ -240,6 +240,11 @@ int64_t ieh_decode_video(ie_ctx* ctx, const uint8_t* enc, size_t len, int n, uin
 // Huffman post-pass entirely between device buffers (in, out device memory; out needs
 // ~n + 4 KiB).  Returns output bytes; only the 256-entry histogram and code table cross PCIe.
 int64_t ieh_huffman_encode_device(ie_ctx* ctx, const uint8_t* din, size_t n, uint8_t* dout, size_t cap);
+/* Batched device Huffman pass: string k = n[k] bytes at din + k*in_pitch -> dout + k*out_pitch
+ * (device memory; out_pitch 4-byte aligned and >= the loose bound (dict + max_len * n[k]) / 8).
+ * bytes[k] receives each output length.  The outputs are complete when the context's stream is. */
+int ieh_huffman_encode_device_batch(ie_ctx* ctx, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count,
+                                    uint8_t* dout, size_t out_pitch, int64_t* bytes);
 // Free the host library's device scratch for ctx (call before ie_destroy).
 void ieh_release(ie_ctx* ctx);
 // Huffman post-pass of n bytes (host or device) into out (host).  Returns output bytes.

@@ -115,6 +115,31 @@ def test_huffman_encode_device_input(codec):
     assert codec.huffman_encode(t) == O.load().huffman_encode(data)
 
 
+def test_huffman_encode_batch(codec):
+    """One histogram launch + one pack launch over a batch of strings (every byte set above, an
+    empty one, a no-gain one) equals the per-string reference Huffman pass; the output pitch
+    starts out as garbage (the batch writes every byte it returns, dictionary included)."""
+    torch = pytest.importorskip("torch")
+    datas = [d for _, d in BYTE_SETS] + [b""]
+    pitch = (max(len(d) for d in datas) + 255) // 256 * 256
+    src = torch.zeros(pitch * len(datas), dtype=torch.uint8)
+    for k, d in enumerate(datas):
+        if d:
+            src[k * pitch:k * pitch + len(d)] = torch.from_numpy(np.frombuffer(d, np.uint8).copy())
+    src = src.cuda()
+    opitch = (4 * pitch + 4096 + 255) // 256 * 256
+    out = torch.full((opitch * len(datas),), 0xAB, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the codec runs on its own stream
+    sizes = codec.huffman_encode_batch(src, pitch, [len(d) for d in datas], out, opitch)
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    oracle = O.load()
+    for k, d in enumerate(datas):
+        got = host[k * opitch:k * opitch + sizes[k]].tobytes()
+        want = oracle.huffman_encode(d) if d else b"\x00"  # empty: the bare stop bit
+        assert got == want, (k, len(d))
+
+
 def test_huffman_no_gain_revert(codec):
     """Uniform bytes do not compress: '0' + the input (Huffman.cpp:329-341), n + 1 bytes."""
     data = BYTE_SETS[0][1]
