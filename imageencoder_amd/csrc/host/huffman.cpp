@@ -24,16 +24,12 @@
 namespace algo {
 namespace {
 
+// Tree nodes live in one pool (no per-node allocation); children by pointer as in the reference.
 struct Node {
     uint8_t data;
     size_t freq;
     Node* left = nullptr;
     Node* right = nullptr;
-    Node(uint8_t d, size_t f, Node* l = nullptr, Node* r = nullptr) : data(d), freq(f), left(l), right(r) {}
-    ~Node() {
-        delete left;
-        delete right;
-    }
     bool leaf() const { return !left && !right; }
 };
 struct ByFreq {  // Node::comparator (Huffman.hpp:63-67): lower frequency = higher priority
@@ -43,19 +39,16 @@ struct Codeword {
     uint32_t word, len;
 };
 
-void walk(const Node* nd, std::vector<bool> path, std::unordered_map<uint8_t, Codeword>& dict) {
+// Depth-first, left before right (Huffman.cpp:93-118): the order of the dictionary insertions.
+// The path travels as (bits, depth); a depth past 32 is reported by the caller.
+void walk(const Node* nd, uint64_t bits, uint32_t depth, std::unordered_map<uint8_t, Codeword>& dict) {
     if (!nd) return;
     if (nd->leaf()) {
-        uint32_t w = 0;
-        for (bool b : path) w = (w << 1) | uint32_t(b);
-        dict[nd->data] = Codeword{w, uint32_t(path.size())};
+        dict[nd->data] = Codeword{uint32_t(bits), depth};
         return;
     }
-    std::vector<bool> lp(path);
-    lp.push_back(false);
-    path.push_back(true);
-    walk(nd->left, lp, dict);
-    walk(nd->right, path, dict);
+    walk(nd->left, bits << 1, depth + 1, dict);
+    walk(nd->right, (bits << 1) | 1u, depth + 1, dict);
 }
 
 }  // namespace
@@ -70,18 +63,26 @@ bool build_code(const uint32_t* hist, const uint64_t* first, util::BitStreamWrit
     std::unordered_map<uint8_t, uint32_t> freqs;
     for (int b : order) freqs[uint8_t(b)] = hist[b];
 
-    std::priority_queue<Node*, std::vector<Node*>, ByFreq> pq;
-    for (const auto& pr : freqs) pq.push(new Node(pr.first, pr.second));
+    std::vector<Node> pool;
+    pool.reserve(2 * freqs.size());  // leaves + internal nodes: pointers stay valid
+    std::vector<Node*> heap;
+    heap.reserve(freqs.size());
+    std::priority_queue<Node*, std::vector<Node*>, ByFreq> pq(ByFreq(), std::move(heap));
+    for (const auto& pr : freqs) {
+        pool.push_back(Node{pr.first, pr.second});
+        pq.push(&pool.back());
+    }
     while (pq.size() > 1) {
         Node* l = pq.top();
         pq.pop();
         Node* r = pq.top();
         pq.pop();
-        pq.push(new Node(uint8_t(-1), l->freq + r->freq, l, r));
+        pool.push_back(Node{uint8_t(-1), l->freq + r->freq, l, r});
+        pq.push(&pool.back());
     }
-    std::unique_ptr<Node> root(pq.top());
+    const Node* root = pq.top();
     std::unordered_map<uint8_t, Codeword> dict;
-    walk(root.get(), std::vector<bool>(), dict);
+    walk(root, 0, 0, dict);
 
     std::vector<std::pair<uint8_t, Codeword>> sorted(dict.begin(), dict.end());
     std::sort(sorted.begin(), sorted.end(),
