@@ -253,6 +253,20 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
     TrkOp op{nn};
     if (n == 4) ie::quot4(b.data(), T->plan4, op);
     else ie::quot8(b.data(), T->dct, T->g, op);
+    // Largest record: |Q_k| <= 128 * sum_ij |S_k P_k[ij]| / q_k (|x| <= 128), so bl <= the widest
+    // bits_needed over k (utils.hpp:226-243; int16 caps it at 16) and >= ffs(N*N) (the L field);
+    // an RLE record is 4 + bl * (1 + N*N) bits at most (Block.cpp:372-413).
+    {
+        int bl = 32 - __builtin_clz(unsigned(nn));
+        for (int k = 0; k < nn; k++) {
+            double m = 0.0;
+            for (int ij = 0; ij < nn; ij++) m += std::fabs(T->S[k] * T->P[k * nn + ij]);
+            const double qmax = std::ceil(128.0 * m / T->qd[k]) + 1.0;
+            const int b = (qmax >= 32768.0) ? 16 : std::min(16, (32 - __builtin_clz(unsigned(qmax))) + 1);
+            bl = std::max(bl, b);
+        }
+        T->rec_bits = 4 + bl * (1 + nn);
+    }
     bool ok = true;
     T->dc_exact = 0;
     T->lim_min = 0.5f;
@@ -449,9 +463,13 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.wave_fix = c->d_wave_fix;
     c->last_fix_words = (mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
     a.tab = c->d_tab;
+    a.rec_bits = c->h_tab->rec_bits;
     a.coef = coef;
     static const int ablate = getenv("IE_ABLATE") ? atoi(getenv("IE_ABLATE")) : 0;  // profiling only
-    a.ablate = ablate;
+#ifndef IE_ABLATE_FORCE
+#define IE_ABLATE_FORCE 0
+#endif
+    a.ablate = ablate | IE_ABLATE_FORCE;  // IE_ABLATE_FORCE: A/B builds of an ablation
     static const char* stamp_file = getenv("IE_STAMPS");  // profiling only: per-tile phase stamps
     uint64_t* d_stamps = nullptr;
     if (stamp_file) {

@@ -21,6 +21,7 @@ struct EncTables {
     Dct4Plan plan4; // 4x4 folded quotient transform (quot4)
     float lim_min;  // min of lim[k] over the non-structural coefficients: one compare per block
     int dc_exact;   // t[0] is exact in FP32 (q[0] a power of two): round it directly
+    int rec_bits;   // largest record (bits) any block can produce with this matrix: sizes the tile image
     // FP64 reference order (algo.cpp:309-331, Block.cpp:149-152)
     double S[64];   // C(u)*C(v)
     double qd[64];  // double(q[uv])
@@ -59,8 +60,10 @@ struct EncArgs {
     uint32_t* wave_fix;      // [ntiles * kTPB/64] FP64 fix-up requests per wave (plain stores, statistics)
     const EncTables* tab;
     int16_t* coef;           // optional: quantised coefficients, natural order, [nframes*bx*by][N*N]
-    int ablate;              // profiling only (IE_ABLATE): 1 no FP64, 2 no emission, 4 no look-back, 8 no store, 16 no DCT
+    int ablate;              // profiling only (IE_ABLATE): 1 no FP64, 2 no emission, 4 no look-back, 8 no store, 16 no DCT, 128 no pixel loads
     uint64_t* stamps;        // profiling only (IE_STAMPS): [tile][kStamps] s_memtime per phase, thread 0
+    int rec_bits;            // = tab->rec_bits (host copy): launch_encode sizes the LDS tile image from it
+    int img_words;           // set by launch_encode
 };
 
 constexpr int kStamps = 16;

@@ -73,11 +73,25 @@ template <> struct Geo<8> {  // one block: 8 bytes per pixel row per lane
     static constexpr int WAVES = 2;
 };
 
-// bits-in-tile upper bound: 4 + 16 * (N*N + 1) bits per block, plus slack for the zero bits the
-// pair emission may OR in past the last record (<= 2 * 16 bits) and the store's look-ahead word
-template <int N> constexpr int image_words() {
-    return ((kEncTPB * Geo<N>::BPT * (4 + 16 * (N * N + 1)) + 31) / 32 + 4 + 3) / 4 * 4;  // keeps misc 16-B aligned
+// The tile's LDS bit image: kEncTPB * BPT records of at most rec_bits bits (the matrix's bound,
+// ie_capi.cpp build_tables), plus slack for the zero bits the pair emission may OR in past the
+// last record (<= 2 * 16 bits) and the store's look-ahead word; at least the fix-up's scratch.
+// Sized per launch (dynamic LDS): a smaller image measured faster at equal occupancy.
+constexpr int image_words_for(int n, int bpt, int rec_bits) {
+    return ((kEncTPB * bpt * rec_bits + 31) / 32 + 4 + 3) / 4 * 4;  // keeps misc 16-B aligned
 }
+
+// Structural fix-up compaction (FAST 4x4): per-wave LDS task slots in the (not yet built) tile
+// image, after the per-lane whole-block result slots [0, kEncTPB * 8).
+#ifndef IE_FIX_COMPACT
+#define IE_FIX_COMPACT 1
+#endif
+#ifndef IE_FIX_UNROLL
+#define IE_FIX_UNROLL 16
+#endif
+constexpr int kFixPix = 0;                               // [BPT][TPB] x 4 words: the pixels
+constexpr int kFixTasks = kFixPix + IE_BPT4 * kEncTPB * 4;  // per wave: [64] tasks, [64] results
+constexpr int kFixWords = kFixTasks + (kEncTPB / 64) * 128;   // the image is never smaller
 
 template <int WPR>
 __device__ __forceinline__ uint32_t pix(const uint32_t (&row)[WPR], int byte) {
@@ -116,11 +130,13 @@ __device__ __forceinline__ int exact_coef_inl(const EncTables* __restrict__ tab,
 }
 
 // The same evaluation with the coefficient's row of P and its scalars taken from an LDS copy.
+// (The row is walked four terms at a time so the compiler does not hoist all NN LDS loads and
+// conversions at once: the caller's packed coefficients stay live around it.)
 template <int N>
 __device__ __forceinline__ int exact_coef_row(const double* P, double S, double rq, double qd, const BlockPx<N>& px) {
     constexpr int NN = N * N;
     double acc = 0.0;
-#pragma unroll
+#pragma unroll IE_FIX_UNROLL
     for (int ij = 0; ij < NN; ij++) {
         const double x = double(int((px.w[ij >> 2] >> (8 * (ij & 3))) & 0xFFu)) + (-128.0);
         acc = acc + P[ij] * x;
@@ -486,19 +502,32 @@ __device__ __forceinline__ void emit_block_sink(WordSink& k, const uint32_t (&zp
     }
 }
 
+// Occupancy hint: __launch_bounds__'s second argument (Geo<N>::WAVES).  IE_LB_ATTR=1 states it
+// as amdgpu_waves_per_eu instead (A/B aid: measured slower).
+#ifndef IE_LB_ATTR
+#define IE_LB_ATTR 0
+#endif
+#if IE_LB_ATTR
+#define IE_ENC_BOUNDS(N) __launch_bounds__(kEncTPB) __attribute__((amdgpu_waves_per_eu(Geo<N>::WAVES, 8)))
+#else
+#define IE_ENC_BOUNDS(N) __launch_bounds__(kEncTPB, Geo<N>::WAVES)
+#endif
 template <int N, bool EXACT>
-__global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
+__global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     constexpr int NN = N * N;
     constexpr int NP = NN / 2;
     constexpr int BPT = Geo<N>::BPT;
     constexpr int WPR = BPT * N / 4;
-    constexpr int IMGW = image_words<N>();
     constexpr int TPB = kEncTPB;
-    __shared__ uint32_t smem[IMGW + 32];
+#ifdef IE_STATIC_IMG4  // A/B aid: a static image of this many bits per block (4x4 only)
+    __shared__ __attribute__((aligned(16))) uint32_t smem[image_words_for(4, 4, IE_STATIC_IMG4) + 32];
+#else
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // [a.img_words + 32]
+#endif
     // FAST mode: the structural coefficients' FP64 rows (P[3][NN], then S[3], rq[3], qd[3])
     __shared__ double srow[3 * NN + 9];
     uint32_t* img = smem;
-    uint32_t* misc = smem + IMGW;  // [0..15] scan scratch (one word per wave)
+    uint32_t* misc = smem + a.img_words;  // [0..15] scan scratch (one word per wave)
     uint32_t* ctl = misc + 16;     // [4] ticket, [5..6] exclusive prefix, [7] predecessor tail
 
     const int tid = threadIdx.x;
@@ -531,7 +560,14 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
     uint32_t seg[N][WPR];
-    load_tile<N, WPR>(a, g, seg);
+    if (a.ablate & 128) {  // profiling: no pixel loads (synthetic pixels from the thread id)
+#pragma unroll
+        for (int r = 0; r < N; r++)
+#pragma unroll
+            for (int m = 0; m < WPR; m++) seg[r][m] = (uint32_t(tid) * 0x9E3779B1u + uint32_t(t) * 0x85EBCA77u) ^ (r * 0x27D4EB2Fu + m);
+    } else {
+        load_tile<N, WPR>(a, g, seg);
+    }
     if constexpr (!EXACT && N == 4) lds_barrier();  // srow visible (the pixel loads stay in flight)
 
     asm volatile("; PHASE load_done" ::: "memory");
@@ -611,6 +647,126 @@ __global__ __launch_bounds__(kEncTPB, Geo<N>::WAVES) void encode_kernel(EncArgs 
             }
         }
         const unsigned wsum = unsigned(wave_sum64(nfix));
+        if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
+    } else if constexpr (!EXACT && IE_FIX_COMPACT) {
+        // Structural requests, compacted per wave: the wave's pixels go to LDS (so the pixel
+        // registers die here), every request gets a task number (a 4-plane ballot prefix), lane i
+        // evaluates task i in FP64 and the owners patch their results in.  One FP64 evaluation
+        // per 64 requests instead of one per lane per request.
+        if (__ballot(flags != 0)) {
+            uint32_t* pxl = img + kFixPix;  // [BPT][TPB] x 16 bytes: block b of thread tid
+#pragma unroll
+            for (int bb = 0; bb < BPT; bb++) {
+                u32x4 v;
+                v.x = seg[0][(bb * N) / 4]; v.y = seg[1][(bb * N) / 4];
+                v.z = seg[2][(bb * N) / 4]; v.w = seg[3][(bb * N) / 4];
+                *reinterpret_cast<u32x4*>(pxl + 4 * (bb * TPB + tid)) = v;
+            }
+            const uint32_t sf = flags & (0x77777777u >> (32 - 4 * BPT));
+            const uint32_t cnt = __popc(sf);
+            uint32_t pre = 0, total = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {  // cnt <= 3 * BPT <= 12
+                const uint64_t bm = __ballot((cnt >> k) & 1u);
+                pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+                total += uint32_t(__popcll(bm)) << k;
+            }
+            const int lane = tid & 63;
+            uint32_t* task = img + kFixTasks + (tid >> 6) * 128;  // [64] tasks, then [64] results
+            uint32_t* res = task + 64;
+            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+                uint32_t m = sf, i = pre - r0;
+                while (m) {
+                    const int bit = __ffs(m) - 1;
+                    m &= m - 1;
+                    if (i < 64u) task[i] = (uint32_t(tid) << 4) | uint32_t(bit);
+                    i++;
+                }
+                wave_sync();
+                if (uint32_t(lane) < total - r0) {
+                    const uint32_t tk = task[lane];
+                    const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
+                    BlockPx<N> px;
+                    px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
+                    res[lane] = uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
+                                                           srow[3 * NN + 6 + s], px)) & 0xFFFFu;
+                }
+                wave_sync();
+                m = sf;
+                i = pre - r0;
+                while (m) {
+                    const int bit = __ffs(m) - 1;
+                    m &= m - 1;
+                    if (i < 64u) {
+                        const uint32_t v = res[i];
+                        const int b = bit >> 2, s = bit & 3;
+#pragma unroll
+                        for (int bb = 0; bb < BPT; bb++)
+#pragma unroll
+                            for (int ss = 0; ss < 3; ss++) {
+                                const int zpos = Structural<N>::zpos(ss);
+                                if (b == bb && s == ss)
+                                    zp[bb][zpos >> 1] = (zpos & 1) ? ((zp[bb][zpos >> 1] & 0xFFFFu) | (v << 16))
+                                                                   : ((zp[bb][zpos >> 1] & 0xFFFF0000u) | v);
+                            }
+                    }
+                    i++;
+                }
+                wave_sync();  // the next round rewrites the task list
+            }
+            // Whole-block requests (rare: an ordinary coefficient near a tie): all NN coefficients
+            // of the block are re-evaluated in FP64, one per lane, four blocks per round.
+            const uint32_t wf = flags & (0x88888888u >> (32 - 4 * BPT));
+            if (__ballot(wf != 0)) {
+                const uint32_t nb = __popc(wf);
+                uint32_t pb = 0, tb = 0;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {  // nb <= BPT <= 4
+                    const uint64_t bm = __ballot((nb >> k) & 1u);
+                    pb += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+                    tb += uint32_t(__popcll(bm)) << k;
+                }
+                for (uint32_t r0 = 0; r0 < tb; r0 += 4) {
+                    uint32_t m = wf, j = pb - r0;
+                    while (m) {
+                        const int b = (__ffs(m) - 1) >> 2;
+                        m &= m - 1;
+                        if (j < 4u) task[j] = (uint32_t(tid) << 4) | uint32_t(b);
+                        j++;
+                    }
+                    wave_sync();
+                    if (uint32_t(lane >> 4) < tb - r0) {
+                        const uint32_t tk = task[lane >> 4];
+                        const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
+                        BlockPx<N> px;
+                        px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
+                        res[lane] = uint32_t(exact_coef_row<N>(tab->P + k * NN, tab->S[k], tab->rq[k], tab->qd[k], px)) &
+                                    0xFFFFu;
+                    }
+                    wave_sync();
+                    m = wf;
+                    j = pb - r0;
+                    while (m) {
+                        const int b = (__ffs(m) - 1) >> 2;
+                        m &= m - 1;
+                        if (j < 4u) {
+                            const uint32_t* rr = res + 16 * j;
+#pragma unroll
+                            for (int jj = 0; jj < NP; jj++) {
+                                const uint32_t w = rr[ZigZag<N>::idx[2 * jj]] | (rr[ZigZag<N>::idx[2 * jj + 1]] << 16);
+#pragma unroll
+                                for (int bb = 0; bb < BPT; bb++) zp[bb][jj] = (b == bb) ? w : zp[bb][jj];
+                            }
+                        }
+                        j++;
+                    }
+                    wave_sync();
+                }
+            }
+        }
+        const unsigned wsum = unsigned(wave_sum64(__popc(flags)));
         if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
     } else if constexpr (!EXACT) {
         uint32_t sf = flags & (0x77777777u >> (32 - 4 * BPT));
@@ -765,14 +921,24 @@ int encode_blocks_per_thread(int n) { return n == 4 ? Geo<4>::BPT : Geo<8>::BPT;
 
 int encode_threads_per_tile() { return kEncTPB; }
 
-void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s) {
+void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s) {
+    EncArgs a = a0;
+    const int bpt = encode_blocks_per_thread(n);
+    a.img_words = image_words_for(n, bpt, a.rec_bits);
+    if (n == 4 && a.img_words < kFixWords) a.img_words = kFixWords;
+#ifdef IE_STATIC_IMG4
+    a.img_words = image_words_for(4, 4, IE_STATIC_IMG4);
+    const size_t lds = 0;
+#else
+    const size_t lds = (size_t(a.img_words) + 32) * sizeof(uint32_t);
+#endif
     const dim3 grid(a.ntiles), block(kEncTPB);
     if (n == 4) {
-        if (exact) hipLaunchKernelGGL((encode_kernel<4, true>), grid, block, 0, s, a, a.tab);
-        else hipLaunchKernelGGL((encode_kernel<4, false>), grid, block, 0, s, a, a.tab);
+        if (exact) hipLaunchKernelGGL((encode_kernel<4, true>), grid, block, lds, s, a, a.tab);
+        else hipLaunchKernelGGL((encode_kernel<4, false>), grid, block, lds, s, a, a.tab);
     } else {
-        if (exact) hipLaunchKernelGGL((encode_kernel<8, true>), grid, block, 0, s, a, a.tab);
-        else hipLaunchKernelGGL((encode_kernel<8, false>), grid, block, 0, s, a, a.tab);
+        if (exact) hipLaunchKernelGGL((encode_kernel<8, true>), grid, block, lds, s, a, a.tab);
+        else hipLaunchKernelGGL((encode_kernel<8, false>), grid, block, lds, s, a, a.tab);
     }
 }
 

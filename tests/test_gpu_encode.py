@@ -178,3 +178,30 @@ def test_random_noise_stress(codec, oracle):
         exp, eend, efb = oracle.encode_blocks(y, n, q, True, 0)
         assert end == eend and np.array_equal(fb, efb)
         assert out[: (end + 7) // 8].tobytes() == exp[: (end + 7) // 8].tobytes()
+
+
+@pytest.mark.parametrize("n", [4, 8])
+@pytest.mark.parametrize("qfill", [1, 3, 255])
+def test_extreme_matrices_fill_the_tile_image(codec, oracle, n, qfill):
+    """The LDS tile image is sized per matrix (the largest record any block can produce):
+    all-ones / small / large constant matrices with extreme 0/255 pixels (the widest records) and
+    with flat frames (the narrowest), RLE on and off, GPU vs oracle bit for bit."""
+    from imageencoder_amd import stream_bound
+    rng = np.random.default_rng(7 + qfill)
+    q = np.full(n * n, qfill, dtype=np.uint16)
+    codec.set_quant(q, n)
+    w, h = 64 * n, 24 * n
+    frames = [
+        (rng.integers(0, 2, size=(h, w)) * 255).astype(np.uint8),           # 0/255 noise
+        np.indices((h, w)).sum(axis=0).astype(np.uint8) % 2 * 255,            # checkerboard
+        np.full((h, w), 128, dtype=np.uint8),                                  # all-zero blocks
+    ]
+    for rle in (True, False):
+        for y in frames:
+            y = np.ascontiguousarray(y, dtype=np.uint8)
+            out = np.zeros(stream_bound(w, h, n, 1, 5), dtype=np.uint8)
+            fb, end = codec.encode_frames(y, w, h, out, start_bit=5, rle=rle)
+            exp, eend, efb = oracle.encode_blocks(y, n, q, rle, 5)
+            assert end == eend and np.array_equal(fb, efb)
+            nb = (end + 7) // 8
+            assert out[:nb].tobytes() == exp[:nb].tobytes()

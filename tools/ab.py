@@ -1,0 +1,99 @@
+"""Interleaved A/B timing of libie_hip.so variants in ONE process (cdna_hip_programming.md rule 24).
+
+usage: python tools/ab.py [--n 4|8] [--frames 16] [--rounds 7] lib1.so lib2.so ...
+Each variant gets its own ie_ctx on torch's current stream; every round times every variant
+(10 launches each, HIP events) in turn; prints the median / min us per launch, and whether the
+variant's output for the batch matches the first variant's byte for byte.
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from imageencoder_amd import synth  # noqa: E402
+from tests import oracle_lib as O  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=4)
+ap.add_argument("--frames", type=int, default=16)
+ap.add_argument("--rounds", type=int, default=7)
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--kind", default="U")
+ap.add_argument("libs", nargs="+")
+args = ap.parse_args()
+
+n = args.n
+q = np.ascontiguousarray(np.asarray(O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n), dtype=np.uint16).ravel())
+w, h, nf = 3840, 2160, args.frames
+y = torch.from_numpy(synth.frames(args.kind, w, h, nf, seed=3)).cuda()
+stream = torch.cuda.Stream()  # a real stream handle (the default stream's handle is 0 = the ctx's own)
+torch.cuda.set_stream(stream)
+variants = []
+shared_out = None
+for path in args.libs:
+    L = C.CDLL(os.path.abspath(path), mode=C.RTLD_LOCAL)
+    vp = C.c_void_p
+    L.ie_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    L.ie_set_stream.argtypes = [vp, vp]
+    L.ie_set_quant.argtypes = [vp, vp, C.c_int]
+    L.ie_stream_bound.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
+    L.ie_stream_bound.restype = C.c_size_t
+    L.ie_encode_images.argtypes = [vp, vp, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                   vp, C.c_size_t, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.ie_last_error.argtypes = [vp]
+    L.ie_last_error.restype = C.c_char_p
+    hnd = C.c_void_p()
+    assert L.ie_create(0, C.byref(hnd)) == 0
+    assert L.ie_set_stream(hnd, C.c_void_p(stream.cuda_stream)) == 0
+    assert L.ie_set_quant(hnd, q.ctypes.data, n) == 0
+    pitch = (int(L.ie_stream_bound(w, h, n, 1, 165)) + 255) // 256 * 256
+    if shared_out is None:  # one output buffer for every variant (placement effects cancel)
+        shared_out = torch.zeros(pitch * nf, dtype=torch.uint8, device="cuda")
+    out = shared_out
+    out.zero_()
+    eb = np.zeros(nf, dtype=np.uint64)
+
+    def run(L=L, hnd=hnd, out=out, pitch=pitch, eb=eb, sizes=False):
+        r = L.ie_encode_images(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, nf, 1, 0, C.c_void_p(out.data_ptr()),
+                               pitch, 165, eb.ctypes.data_as(C.POINTER(C.c_uint64)) if sizes else None)
+        if r != 0:
+            raise RuntimeError(L.ie_last_error(hnd))
+
+    run(sizes=True)
+    torch.cuda.synchronize()
+    variants.append({"name": os.path.basename(os.path.dirname(path)) or path, "run": run, "out": out.clone(),
+                     "pitch": pitch, "eb": eb.copy(), "t": []})
+
+ref = variants[0]
+for v in variants:
+    ok = np.array_equal(v["eb"], ref["eb"])
+    if ok:
+        for f in range(nf):
+            nb = (int(v["eb"][f]) + 7) // 8
+            a = v["out"][f * v["pitch"]: f * v["pitch"] + nb]
+            b = ref["out"][f * ref["pitch"]: f * ref["pitch"] + nb]
+            if not torch.equal(a, b):
+                ok = False
+                break
+    v["same"] = ok
+
+order_rng = np.random.default_rng(0)
+for r in range(args.rounds):
+    for vi in order_rng.permutation(len(variants)):
+        v = variants[vi]
+        v["run"]()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            v["run"]()
+        e1.record()
+        e1.synchronize()
+        v["t"].append(e0.elapsed_time(e1) * 1000.0 / args.iters)
+for v in variants:
+    t = np.array(v["t"])
+    print(f"{v['name']:24s} median {np.median(t):8.2f} us  min {t.min():8.2f} us  same_as_first={v['same']}")
