@@ -74,11 +74,11 @@ template <> struct Geo<8> {  // one block: 8 bytes per pixel row per lane
 };
 
 // The tile's LDS bit image: kEncTPB * BPT records of at most rec_bits bits (the matrix's bound,
-// ie_capi.cpp build_tables), plus slack for the zero bits the pair emission may OR in past the
-// last record (<= 2 * 16 bits) and the store's look-ahead word; at least the fix-up's scratch.
+// ie_capi.cpp build_tables), plus slack for the zero pairs emit_block2 may OR in past the last
+// record (<= 16 * N*N bits) and the store's look-ahead word; at least the fix-up's scratch.
 // Sized per launch (dynamic LDS): a smaller image measured faster at equal occupancy.
 constexpr int image_words_for(int n, int bpt, int rec_bits) {
-    return ((kEncTPB * bpt * rec_bits + 31) / 32 + 4 + 3) / 4 * 4;  // keeps misc 16-B aligned
+    return ((kEncTPB * bpt * rec_bits + 31) / 32 + 4 + (n * n + 3) + 3) / 4 * 4;  // keeps misc 16-B aligned
 }
 
 // Structural fix-up compaction (FAST 4x4): per-wave LDS task slots in the (not yet built) tile
@@ -92,6 +92,13 @@ constexpr int image_words_for(int n, int bpt, int rec_bits) {
 constexpr int kFixPix = 0;                               // [BPT][TPB] x 4 words: the pixels
 constexpr int kFixTasks = kFixPix + IE_BPT4 * kEncTPB * 4;  // per wave: [64] tasks, [64] results
 constexpr int kFixWords = kFixTasks + (kEncTPB / 64) * 128;   // the image is never smaller
+// 8x8: one 16-word block per lane at a 20-word stride (16-byte writes land on distinct banks)
+#ifndef IE_FIX_COMPACT8
+#define IE_FIX_COMPACT8 1
+#endif
+constexpr int kFix8Stride = 20;
+constexpr int kFix8Tasks = kFix8Stride * kEncTPB;
+constexpr int kFix8Words = kFix8Tasks + (kEncTPB / 64) * 128;
 
 template <int WPR>
 __device__ __forceinline__ uint32_t pix(const uint32_t (&row)[WPR], int byte) {
@@ -385,6 +392,34 @@ __device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t
     atomicOr(&img[w + 1], uint32_t(x));
 }
 
+// Branch-free variant: every pair is written (past Lw the packed coefficients are zero, so
+// those ORs are no-ops) and the wave leaves the loop once no lane has a pair left: no per-lane
+// exec-mask juggling per pair.  The zero pairs may land up to 2 * 16 * N*N/2 bits past the
+// record: the image keeps that much slack.
+#ifndef IE_EMIT2
+#define IE_EMIT2 1
+#endif
+template <int N>
+__device__ __forceinline__ void emit_block2(uint32_t* img, uint32_t p, const uint32_t (&zp)[N * N / 2], uint32_t blw,
+                                            int rle) {
+    const uint32_t bl = blw & 0xFFu, lw = blw >> 8;
+    if (rle) {
+        scatter_bits(img, p, ((bl & 0xFu) << bl) | lw, 4u + bl);
+        p += 4u + bl;
+    } else {
+        scatter_bits(img, p, bl & 0xFu, 4u);
+        p += 4u;
+    }
+    const uint32_t m = (1u << bl) - 1u;
+#pragma unroll
+    for (int j = 0; j < N * N / 2; j++) {
+        if (j > 0 && !__ballot(uint32_t(2 * j) < lw)) break;  // no lane has pair j
+        const uint32_t v = ((zp[j] & m) << bl) | __builtin_amdgcn_ubfe(zp[j], 16u, bl);
+        scatter_bits(img, p, v, 2u * bl);
+        p += 2u * bl;
+    }
+}
+
 // The record of one sized block at bit p of the tile image (Block.cpp:372-413): bl in 4 bits,
 // [Lw in bl bits,] then the coefficients two at a time (2*bl <= 32 bits per OR pair).
 template <int N>
@@ -545,7 +580,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
         t = int(blockIdx.x);
     }
     STAMP(0);
-    if constexpr (!EXACT && N == 4) {
+    if constexpr (!EXACT) {
         // issued before the pixel loads, so waiting for it does not wait for them
         for (int i = tid; i < 3 * NN + 9; i += TPB) {
             double v;
@@ -568,7 +603,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     } else {
         load_tile<N, WPR>(a, g, seg);
     }
-    if constexpr (!EXACT && N == 4) lds_barrier();  // srow visible (the pixel loads stay in flight)
+    if constexpr (!EXACT) lds_barrier();  // srow visible (the pixel loads stay in flight)
 
     asm volatile("; PHASE load_done" ::: "memory");
     if (a.stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
@@ -625,7 +660,82 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     // no barrier: a wave loops as long as any lane still has one.  Structural coefficient s of
     // block b: its P row comes from the LDS copy; a whole-block request (rare): fix_block, with
     // its per-lane result slot in the (not yet built) tile image.
-    if constexpr (!EXACT && N == 8) {
+    if constexpr (!EXACT && N == 8 && IE_FIX_COMPACT8) {
+        // 8x8: one task per flagged coefficient, compacted per wave as for 4x4: the lane's block
+        // (16 words) goes to an LDS slot, lane i evaluates task i in FP64 -- the structural
+        // coefficients' rows from the LDS copy, any other row from the (L2-resident) table --
+        // and the owners patch their results in.
+        const unsigned nfix = unsigned(__popcll(near8));
+        if (__ballot(near8 != 0)) {
+            uint32_t* pxl = img;  // [TPB] x kFix8Stride words
+#pragma unroll
+            for (int q4 = 0; q4 < 4; q4++) {
+                u32x4 v;
+                v.x = seg[2 * q4][0]; v.y = seg[2 * q4][1]; v.z = seg[2 * q4 + 1][0]; v.w = seg[2 * q4 + 1][1];
+                *reinterpret_cast<u32x4*>(pxl + kFix8Stride * tid + 4 * q4) = v;
+            }
+            const uint32_t cnt = nfix;
+            uint32_t pre = 0, total = 0;
+#pragma unroll
+            for (int k = 0; k < 7; k++) {  // cnt <= 64
+                const uint64_t bm = __ballot((cnt >> k) & 1u);
+                pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+                total += uint32_t(__popcll(bm)) << k;
+            }
+            const int lane = tid & 63;
+            uint32_t* task = img + kFix8Tasks + (tid >> 6) * 128;  // [64] tasks, then [64] results
+            uint32_t* res = task + 64;
+            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+                uint64_t m = near8;
+                uint32_t i = pre - r0;
+                while (m) {
+                    const int k = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    if (i < 64u) task[i] = (uint32_t(tid) << 6) | uint32_t(k);
+                    i++;
+                }
+                wave_sync();
+                if (uint32_t(lane) < total - r0) {
+                    const uint32_t tk = task[lane];
+                    const int k = int(tk & 63u), owner = int(tk >> 6);
+                    BlockPx<N> px;
+#pragma unroll
+                    for (int q4 = 0; q4 < 4; q4++) {
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + kFix8Stride * owner + 4 * q4);
+                        px.w[4 * q4] = v.x; px.w[4 * q4 + 1] = v.y; px.w[4 * q4 + 2] = v.z; px.w[4 * q4 + 3] = v.w;
+                    }
+                    const int s = (k == Structural<N>::k[0]) ? 0 : (k == Structural<N>::k[1]) ? 1
+                                : (k == Structural<N>::k[2]) ? 2 : -1;
+                    uint32_t v;
+                    if (s >= 0)
+                        v = uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
+                                                       srow[3 * NN + 6 + s], px));
+                    else
+                        v = uint32_t(exact_coef_inl<N>(tab, k, px));
+                    res[lane] = v & 0xFFFFu;
+                }
+                wave_sync();
+                m = near8;
+                i = pre - r0;
+                while (m) {
+                    const int k = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    if (i < 64u) {
+                        const uint32_t v = res[i];
+                        const int kz = ZigZagInv<N>::pos[k];
+#pragma unroll
+                        for (int j = 0; j < NP; j++)
+                            if ((kz >> 1) == j)
+                                zp[0][j] = (kz & 1) ? ((zp[0][j] & 0xFFFFu) | (v << 16)) : ((zp[0][j] & 0xFFFF0000u) | v);
+                    }
+                    i++;
+                }
+                wave_sync();  // the next round rewrites the task list
+            }
+        }
+        const unsigned wsum = unsigned(wave_sum64(nfix));
+        if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
+    } else if constexpr (!EXACT && N == 8) {
         // 8x8: one coefficient per request, its FP64 row from the (L2-resident) table
         uint64_t nr = near8;
         const unsigned nfix = unsigned(__popcll(near8));
@@ -689,8 +799,10 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                     const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
                     BlockPx<N> px;
                     px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
-                    res[lane] = uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
-                                                           srow[3 * NN + 6 + s], px)) & 0xFFFFu;
+                    res[lane] = (a.ablate & 256) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
+                                                 : uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s],
+                                                                              srow[3 * NN + 3 + s], srow[3 * NN + 6 + s],
+                                                                              px)) & 0xFFFFu;
                 }
                 wave_sync();
                 m = sf;
@@ -878,7 +990,11 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
             uint32_t p = off;
 #pragma unroll
             for (int b = 0; b < BPT; b++) {
-                if (rbits[b]) emit_block<N>(img, p, zp[b], blw[b], a.rle);
+                if (IE_EMIT2) {
+                    if (rbits[b]) emit_block2<N>(img, p, zp[b], blw[b], a.rle);
+                } else {
+                    if (rbits[b]) emit_block<N>(img, p, zp[b], blw[b], a.rle);
+                }
                 p += rbits[b];
             }
         }
@@ -926,6 +1042,7 @@ void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s) {
     const int bpt = encode_blocks_per_thread(n);
     a.img_words = image_words_for(n, bpt, a.rec_bits);
     if (n == 4 && a.img_words < kFixWords) a.img_words = kFixWords;
+    if (n == 8 && a.img_words < kFix8Words) a.img_words = kFix8Words;
 #ifdef IE_STATIC_IMG4
     a.img_words = image_words_for(4, 4, IE_STATIC_IMG4);
     const size_t lds = 0;
