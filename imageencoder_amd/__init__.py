@@ -109,6 +109,7 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
     H.ieh_decode_image.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip]
     H.ieh_decode_video.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip, ip]
     H.ieh_huffman_encode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t]
+    H.ieh_huffman_decode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, ip]
     H.ieh_write_header.argtypes = [vp, C.c_size_t, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, C.c_int, C.c_int]
     H.ieh_write_header.restype = C.c_int64
@@ -118,7 +119,8 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
     H.ieh_huffman_encode_device_batch.restype = C.c_int
     H.ieh_release.argtypes = [vp]
     H.ieh_release.restype = None
-    for f in ("ieh_encode_image", "ieh_encode_video", "ieh_decode_image", "ieh_decode_video", "ieh_huffman_encode"):
+    for f in ("ieh_encode_image", "ieh_encode_video", "ieh_decode_image", "ieh_decode_video", "ieh_huffman_encode",
+              "ieh_huffman_decode"):
         getattr(H, f).restype = C.c_int64
     _host = H
     return H
@@ -351,6 +353,16 @@ class Codec:
         self._host_chk(H.ieh_huffman_encode_device_batch(self.h, _ptr(data), in_pitch, n.ctypes.data, k, _ptr(out),
                                                          out_pitch, nb.ctypes.data))
         return [int(v) for v in nb]
+
+    def huffman_decode(self, data: bytes):
+        """The Huffman decode alone (device bit walk): (decoded bytes, passthrough)."""
+        H = load_host_library()
+        src = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+        cap = 8 * src.size + 16
+        out = np.zeros(cap, dtype=np.uint8)
+        pt = C.c_int(0)
+        r = self._host_chk(H.ieh_huffman_decode(self.h, src.ctypes.data, src.size, out.ctypes.data, cap, C.byref(pt)))
+        return out[:r].tobytes(), bool(pt.value)
 
     def huffman_encode(self, data) -> bytes:
         """The Huffman post-pass alone (host or device input)."""

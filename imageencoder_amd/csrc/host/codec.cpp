@@ -155,7 +155,8 @@ static int decode_file(ie_ctx* c, const uint8_t* enc, size_t len, int n, bool vi
     std::vector<uint8_t> dec;
     bool pass = false;
     size_t start = 0;
-    if (!algo::Huffman::decode(enc, len, dec, pass, start)) return (err = "malformed Huffman stream", IE_EFORMAT);
+    if (int r = algo::Huffman::decode(c, enc, len, dec, pass, start))
+        return (err = (r == IE_EFORMAT ? std::string("malformed Huffman stream") : std::string(ie_last_error(c))), r);
     const uint8_t* src = pass ? enc : dec.data();
     const size_t srclen = pass ? len : dec.size();
     if (!parse_header(src, srclen, start, n, video, sh)) return (err = "stream shorter than its header", IE_EFORMAT);
@@ -408,6 +409,21 @@ int ieh_huffman_encode_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pit
 void ieh_release(ie_ctx* c) {
     std::lock_guard<std::mutex> lk(dc::g_mu);
     dc::g_scratch.erase(c);
+}
+
+// The Huffman decode alone (Huffman.cpp:354-402): returns the decoded byte count, or 0 with
+// *passthrough = 1 for a stream without a dictionary; IE_ECAP if cap is too small.
+int64_t ieh_huffman_decode(ie_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap, int* passthrough) {
+    if (!c || (!in && n) || !out) return IE_EINVAL;
+    std::vector<uint8_t> v;
+    bool pass = false;
+    size_t start = 0;
+    const int r = algo::Huffman::decode(c, in, n, v, pass, start);
+    if (r) return r;
+    if (passthrough) *passthrough = pass ? 1 : 0;
+    if (v.size() > cap) return IE_ECAP;
+    if (!v.empty()) std::memcpy(out, v.data(), v.size());
+    return int64_t(v.size());
 }
 
 int64_t ieh_huffman_encode(ie_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap) {

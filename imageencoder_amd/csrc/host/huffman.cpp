@@ -249,11 +249,12 @@ int Huffman::encode(ie_ctx* c, const uint8_t* in, size_t n, std::vector<uint8_t>
 }
 
 // ----------------------------------------------------------------------------------- decode
-// Huffman<uint8_t>::decode (Huffman.cpp:120-204, 354-402): the dictionary rebuilds the tree
-// leaf by leaf; no dictionary entry = passthrough (the stream continues after the stop bit).
-// The bit walk uses a 12-bit lookup table over the tree instead of one pointer hop per bit.
-bool Huffman::decode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
-                     size_t& start_bit) {
+// Huffman<uint8_t>::decode (Huffman.cpp:120-204, 354-402): the dictionary rebuilds the tree leaf
+// by leaf on the host (<= 256 leaves); no dictionary entry = passthrough (the stream continues
+// after the stop bit).  The bit walk -- O(stream bits), serial in the reference -- runs on the
+// device (ie_huffman_decode) over a 15-bit prefix table built from the tree.
+int Huffman::decode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
+                    size_t& start_bit) {
     util::BitStreamReader rd(in, n);
     struct T {
         int child[2] = {-1, -1};
@@ -284,54 +285,41 @@ bool Huffman::decode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, boo
     if (!any) {
         passthrough = true;
         start_bit = rd.get_position();
-        return true;
+        return IE_OK;
     }
     passthrough = false;
     start_bit = 0;
-    constexpr int K = 12;
-    // table[prefix of K bits] = {symbol, bits consumed} when a leaf is reached within K bits
-    std::vector<int32_t> tab(size_t(1) << K);
-    for (uint32_t p = 0; p < (1u << K); p++) {
-        int cur = 0, used = 0;
-        while (used < K && (tree[cur].child[0] >= 0 || tree[cur].child[1] >= 0)) {
-            cur = tree[cur].child[(p >> (K - 1 - used)) & 1u];
-            used++;
-            if (cur < 0) break;
-        }
-        if (cur >= 0 && tree[cur].child[0] < 0 && tree[cur].child[1] < 0)
-            tab[p] = (tree[cur].sym << 8) | used;
-        else
-            tab[p] = -1;
-    }
-    const uint64_t raw_bits = uint64_t(n) * 8;
-    out.clear();
-    out.reserve(n * 2);
-    uint64_t pos = rd.get_position();
-    auto peek = [&](uint64_t at) -> uint32_t {  // K bits from `at`, zeros past the end
-        uint32_t v = 0;
-        for (int b = 0; b < 3; b++) {
-            const uint64_t byte = (at >> 3) + uint64_t(b);
-            v = (v << 8) | (byte < n ? in[byte] : 0u);
-        }
-        return (v >> (24 - K - (at & 7))) & ((1u << K) - 1u);
-    };
-    while (pos < raw_bits) {
-        const int32_t e = tab[peek(pos)];
-        if (e >= 0) {
-            out.push_back(uint8_t(e >> 8));
-            pos += uint64_t(e & 0xFF);
+    // lut[p] = sym | len << 8 for the leaf reached by the 15-bit string p (codes are <= 15 bits:
+    // 4-bit lengths in the dictionary); 0 where the walk falls off the tree or needs more bits
+    constexpr int K = 15;
+    std::vector<uint16_t> lut(size_t(1) << K, 0);
+    std::vector<std::pair<int, int>> stack{{0, 0}};  // (node, depth); prefix filled per leaf
+    std::vector<uint32_t> path(tree.size(), 0);
+    while (!stack.empty()) {
+        const auto [nd, depth] = stack.back();
+        stack.pop_back();
+        const T& t = tree[size_t(nd)];
+        const bool leaf = t.child[0] < 0 && t.child[1] < 0;
+        if (leaf) {
+            if (depth == 0 || depth > K || t.sym < 0) continue;  // a lone root / over-long code: no entry
+            const uint32_t lo = path[size_t(nd)] << (K - depth), span = 1u << (K - depth);
+            for (uint32_t q = 0; q < span; q++) lut[lo + q] = uint16_t(uint32_t(t.sym) | (uint32_t(depth) << 8));
             continue;
         }
-        int cur = 0;  // code longer than K bits (or invalid): walk the tree
-        while (tree[cur].child[0] >= 0 || tree[cur].child[1] >= 0) {
-            const uint32_t bit = pos < raw_bits ? (in[pos >> 3] >> (7 - (pos & 7))) & 1u : 0u;
-            pos++;
-            cur = tree[cur].child[bit];
-            if (cur < 0) return false;
-        }
-        out.push_back(uint8_t(tree[cur].sym));
+        for (int d = 0; d < 2; d++)
+            if (t.child[d] >= 0) {
+                path[size_t(t.child[d])] = (path[size_t(nd)] << 1) | uint32_t(d);
+                stack.push_back({t.child[d], depth + 1});
+            }
     }
-    return true;
+    // the walk ends at the end of the buffer (padding bits included), so at most one symbol per bit
+    const uint64_t nbits = uint64_t(n) * 8, from = rd.get_position();
+    out.resize(size_t(nbits - from) + 1);
+    size_t got = 0;
+    const int r = ie_huffman_decode(ctx, in, n, from, lut.data(), out.data(), out.size(), &got);
+    if (r) return r;
+    out.resize(got);
+    return IE_OK;
 }
 
 }  // namespace algo

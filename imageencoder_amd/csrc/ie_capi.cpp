@@ -71,7 +71,11 @@ struct ie_ctx {
     size_t cap_count = 0;
     uint64_t* d_bb = nullptr;          // block start bits
     size_t cap_bb = 0;
-    uint64_t* d_misc = nullptr;        // [0] end bit, [1] changed flag
+    uint64_t* d_misc = nullptr;        // [0] end bit, [1] changed / invalid flags, [2] symbol count
+    uint16_t* d_hlut = nullptr;        // Huffman decode prefix table (32768 entries)
+    size_t cap_hlut = 0;
+    uint8_t* d_hout = nullptr;         // Huffman decode output staging (host destinations)
+    size_t cap_hout = 0;
     uint8_t* d_pix = nullptr;
     size_t cap_pix = 0;
     int last_rounds = 0;
@@ -665,6 +669,8 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_count);
     (void)hipFree(c->d_bb);
     (void)hipFree(c->d_misc);
+    (void)hipFree(c->d_hlut);
+    (void)hipFree(c->d_hout);
     (void)hipFree(c->d_pix);
     (void)hipFree(c->d_coef);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -971,6 +977,60 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
                                      start_bit, end_bit);
     }
     for (size_t k = 0; k < K; k++) end_bit[k] = n[k] ? ends[k] : start_bit[k];
+    return IE_OK;
+}
+
+int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, const uint16_t* lut,
+                      uint8_t* out, size_t out_cap, size_t* nout) {
+    if (!c || !in || !lut || !nout) return IE_EINVAL;
+    *nout = 0;
+    if (start_bit > uint64_t(len) * 8) return fail(c, IE_EINVAL, "start_bit beyond the stream");
+    HIPCHK(c, hipSetDevice(c->device));
+    int r;
+    const size_t padded = (len + 3) / 4 * 4 + 16;  // two zero words past the end for the bit reader
+    if ((r = ensure(c, c->d_dec, c->cap_dec, padded))) return r;
+    HIPCHK(c, hipMemsetAsync(c->d_dec + (len / 4) * 4, 0, padded - (len / 4) * 4, c->stream));
+    if (len)
+        HIPCHK(c, hipMemcpyAsync(c->d_dec, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                 c->stream));
+    if ((r = ensure(c, c->d_hlut, c->cap_hlut, size_t(32768)))) return r;
+    HIPCHK(c, hipMemcpyAsync(c->d_hlut, lut, 32768 * sizeof(uint16_t),
+                             is_device_ptr(lut) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    const uint64_t nbits = uint64_t(len) * 8;
+    const uint64_t chunk_bits = 2048;
+    const size_t nchunks = size_t((nbits - start_bit + chunk_bits - 1) / chunk_bits);
+    if (!nchunks) return IE_OK;
+    if ((r = ensure(c, c->d_walk, c->cap_walk, 4 * nchunks))) return r;
+    if ((r = ensure(c, c->d_count, c->cap_count, nchunks))) return r;
+    uint64_t* wk = c->d_walk;
+    const size_t cap = c->cap_walk / 4;
+    unsigned* flags = reinterpret_cast<unsigned*>(c->d_misc + 1);
+    HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 4 * sizeof(uint64_t), c->stream));
+    const uint32_t* W = reinterpret_cast<const uint32_t*>(c->d_dec);
+    const int rounds = ie::huffman_decode_device(W, nbits, start_bit, c->d_hlut, chunk_bits, wk, wk + cap,
+                                                 wk + 2 * cap, c->d_count, wk + 3 * cap, flags, c->d_misc + 2,
+                                                 nullptr, false, c->stream, int(nchunks) + 2);
+    if (rounds < 0) return fail(c, IE_EHIP, "Huffman decode walk failed");
+    HIPCHK(c, hipGetLastError());
+    uint64_t total = 0;
+    HIPCHK(c, hipMemcpyAsync(&total, c->d_misc + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *nout = size_t(total);
+    if (total > out_cap) return fail(c, IE_ECAP, "output capacity below the decoded symbol count");
+    const bool out_dev = is_device_ptr(out);
+    uint8_t* dout = out;
+    if (!out_dev) {
+        if ((r = ensure(c, c->d_hout, c->cap_hout, size_t(total) + 1))) return r;
+        dout = c->d_hout;
+    }
+    ie::huffman_decode_device(W, nbits, start_bit, c->d_hlut, chunk_bits, wk, wk + cap, wk + 2 * cap, c->d_count,
+                              wk + 3 * cap, flags, c->d_misc + 2, dout, true, c->stream, 0);
+    HIPCHK(c, hipGetLastError());
+    unsigned f[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(f, flags, sizeof(f), hipMemcpyDeviceToHost, c->stream));
+    if (!out_dev && total) HIPCHK(c, hipMemcpyAsync(out, dout, size_t(total), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (f[1]) return fail(c, IE_EFORMAT, "Huffman stream holds a bit string no code prefixes");
     return IE_OK;
 }
 

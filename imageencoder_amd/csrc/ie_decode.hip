@@ -200,6 +200,159 @@ __global__ __launch_bounds__(kTPB) void decode_kernel(DecArgs a, const uint32_t*
     }
 }
 
+// ---- Huffman decode (Huffman.cpp:354-402; the per-bit tree walk of :190-204) -------------------
+// Same chunked speculation as the record walk: one lane per chunk of bits decodes symbols with a
+// prefix table until it leaves the chunk; fix-up rounds re-walk chunks whose entry differs from the
+// predecessor's exit (prefix codes resynchronise within a few symbols); a scan of the per-chunk
+// symbol counts places every chunk's output; a last walk writes the symbols.  The reference walks
+// to the end of the buffer, padding bits of the last byte included (a code may run past it with
+// zero bits), and so does this walk.
+//   lut   [2^15]: sym | len << 8 for every 15-bit prefix, len 0 = no code (codes are <= 15 bits:
+//         the dictionary stores lengths in 4 bits, Huffman.cpp:41-42)
+//   LDS   the 2^kHufL1 first-level entries (codes of <= kHufL1 bits resolve there)
+constexpr int kHufL1 = 11;
+struct HufArgs {
+    const uint32_t* words;
+    uint64_t nbits, start_bit, chunk_bits;
+    int nchunks;
+    const uint16_t* lut;
+    uint64_t* entry;
+    const uint64_t* exit_in;
+    uint64_t* exit_out;
+    uint32_t* count;
+    unsigned* changed;  // [0] a round changed an entry, [1] invalid code on the exact walk
+    int first;
+    const uint64_t* base;
+    uint8_t* out;
+};
+
+__device__ __forceinline__ void huf_l1(const uint16_t* lut, uint16_t* l1) {
+    for (int q = threadIdx.x; q < (1 << kHufL1); q += blockDim.x) {
+        const uint16_t e = lut[uint32_t(q) << (15 - kHufL1)];
+        l1[q] = ((e >> 8) != 0 && (e >> 8) <= kHufL1) ? e : uint16_t(0);  // 0: look in lut
+    }
+    __syncthreads();
+}
+
+// Walk [pos, end): returns the exit position; *cnt symbols; out (optional) receives them.
+__device__ __forceinline__ uint64_t huf_walk(const HufArgs& a, const uint16_t* l1, uint64_t pos, uint64_t end,
+                                             uint32_t* cnt, uint8_t* out, bool exact) {
+    uint32_t c = 0;
+    while (pos < end && pos < a.nbits) {
+        const uint32_t p15 = getbits(a.words, pos, 15);
+        uint32_t e = l1[p15 >> (15 - kHufL1)];
+        if (!e) e = a.lut[p15];
+        const uint32_t len = e >> 8;
+        if (!len) {  // no code starts here: a speculative walk slides; the exact walk reports
+            if (exact) {
+                atomicOr(&a.changed[1], 1u);
+                break;
+            }
+            pos += 1;
+            continue;
+        }
+        if (out) out[c] = uint8_t(e);
+        c++;
+        pos += len;
+    }
+    *cnt = c;
+    return pos;
+}
+
+__global__ __launch_bounds__(kTPB) void huf_walk_kernel(HufArgs a) {
+    __shared__ uint16_t l1[1 << kHufL1];
+    huf_l1(a.lut, l1);
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.nchunks) return;
+    const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
+    uint64_t e;
+    if (a.first) {
+        e = cstart;
+    } else {
+        if (k == 0) {
+            a.exit_out[0] = a.exit_in[0];
+            return;
+        }
+        e = a.exit_in[k - 1];
+        if (e == a.entry[k]) {
+            a.exit_out[k] = a.exit_in[k];
+            return;
+        }
+        atomicOr(a.changed, 1u);
+    }
+    a.entry[k] = e;
+    uint32_t c;
+    a.exit_out[k] = huf_walk(a, l1, e, cstart + a.chunk_bits, &c, nullptr, false);
+    a.count[k] = c;
+}
+
+__global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
+    __shared__ uint16_t l1[1 << kHufL1];
+    huf_l1(a.lut, l1);
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.nchunks) return;
+    const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
+    uint32_t c;
+    huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, a.out + a.base[k], true);
+}
+
+// Returns the number of fix-up rounds (>= 0), -1 on a HIP error, -2 if the rounds did not settle.
+// total receives the symbol count (device, 1 word) = base[last] + count[last].
+__global__ void huf_total_kernel(const uint64_t* base, const uint32_t* count, int n, uint64_t* total) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *total = base[n - 1] + count[n - 1];
+}
+
+int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
+                          uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,
+                          uint64_t* base, unsigned* changed, uint64_t* total, uint8_t* out, bool write,
+                          hipStream_t s, int max_rounds) {
+    const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
+    const int nchunks = int((span + chunk_bits - 1) / chunk_bits);
+    if (nchunks == 0) return 0;
+    HufArgs a{};
+    a.words = W;
+    a.nbits = nbits;
+    a.start_bit = start_bit;
+    a.chunk_bits = chunk_bits;
+    a.nchunks = nchunks;
+    a.lut = lut;
+    a.entry = entry;
+    a.count = count;
+    a.changed = changed;
+    a.base = base;
+    a.out = out;
+    const dim3 g((nchunks + kTPB - 1) / kTPB), blk(kTPB);
+    if (!write) {
+        a.first = 1;
+        a.exit_in = exA;
+        a.exit_out = exA;
+        hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
+        uint64_t* cur = exA;
+        uint64_t* nxt = exB;
+        int rounds = 0;
+        for (; rounds < max_rounds; rounds++) {
+            unsigned h = 0;
+            if (hipMemsetAsync(changed, 0, sizeof(unsigned), s) != hipSuccess) return -1;
+            a.first = 0;
+            a.exit_in = cur;
+            a.exit_out = nxt;
+            hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
+            if (hipMemcpyAsync(&h, changed, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+            if (hipStreamSynchronize(s) != hipSuccess) return -1;
+            uint64_t* t = cur;
+            cur = nxt;
+            nxt = t;
+            if (!h) break;
+        }
+        if (rounds == max_rounds) return -2;
+        hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
+        hipLaunchKernelGGL(huf_total_kernel, dim3(1), dim3(1), 0, s, base, count, nchunks, total);
+        return rounds;
+    }
+    hipLaunchKernelGGL(huf_emit_kernel, g, blk, 0, s, a);
+    return 0;
+}
+
 // Host-driven decode sequence (ie_capi.cpp::decode calls this).
 int decode_frames_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& da, int n,
                          uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,

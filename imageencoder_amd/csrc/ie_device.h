@@ -119,4 +119,11 @@ int decode_frames_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, 
                          uint64_t* base, uint64_t* block_bit, unsigned* changed, uint64_t* end_out, hipStream_t s,
                          int max_rounds);
 
+// Huffman decode (ie_decode.hip): write = false runs the walk + fix-up rounds + scan and leaves the
+// symbol count in *total (device); write = true then emits the symbols into out.
+int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
+                          uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,
+                          uint64_t* base, unsigned* changed, uint64_t* total, uint8_t* out, bool write,
+                          hipStream_t s, int max_rounds);
+
 }  // namespace ie

@@ -146,6 +146,17 @@ int ie_huffman_pack_batch(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const
  * path of Huffman.cpp:329-341 writes '0' + the input: start_bit = 1). */
 int ie_bitcopy(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint8_t* out, size_t out_cap, uint64_t start_bit);
 
+/* Huffman decode on the device (algo::Huffman<uint8_t>::decode, Huffman.cpp:354-402, replacing the
+ * per-bit tree walk of Huffman.cpp:190-204): the symbols of the code stream `in` (len bytes, host or
+ * device) from start_bit (just past the dictionary) to the END OF THE BUFFER -- the reference also
+ * decodes the padding bits of the last byte, a code running past the end reads zero bits.  lut
+ * (host or device): 32768 uint16 entries, lut[p] = sym | len << 8 for the code that prefixes the
+ * 15-bit string p (len 0: none; codes are <= 15 bits, Huffman.cpp:41-42), built by the caller from
+ * the dictionary.  out (host or device, out_cap bytes) receives the symbols; *nout their count
+ * (also when IE_ECAP is returned).  IE_EFORMAT: a bit string that no code prefixes. */
+int ie_huffman_decode(ie_ctx* ctx, const uint8_t* in, size_t len, uint64_t start_bit, const uint16_t* lut,
+                      uint8_t* out, size_t out_cap, size_t* nout);
+
 /* ---- Inverse path (ImageDecoder.cpp:55-122, Block.cpp:100-107,163-177,442-472) ------------
  * Decode nframes frames of block records starting at bit start_bit of `in` (len bytes) into
  * pixels (frame f row r at out + f*frame_pitch + r*stride).  Uses the quant matrix of

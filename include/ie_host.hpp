@@ -115,16 +115,17 @@ namespace algo {
 
 // Huffman<uint8_t> (Huffman.cpp:233-402).  encode(): device histogram + first occurrence, the
 // tree / dictionary replayed on the host with the reference's own libstdc++ containers, device
-// re-encode.  decode(): dictionary and tree on the host, then the bit walk.
+// re-encode.  decode(): dictionary and tree on the host, the bit walk on the device.
 class Huffman {
 public:
     // Encode `n` bytes at `in` (host or device).  Returns the output bytes (host).  `ctx` runs
     // the device stages.
     static int encode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_t>& out);
     // Decode a stream that starts with the Huffman flag bit.  passthrough = true: no table, the
-    // payload starts at *start_bit of `in` itself; else `out` receives the decoded bytes.
-    static bool decode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
-                       size_t& start_bit);
+    // payload starts at *start_bit of `in` itself; else `out` receives the decoded bytes (the bit
+    // walk runs on ctx's device, ie_huffman_decode).  Returns IE_OK or an ie_hip.h error code.
+    static int decode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
+                      size_t& start_bit);
 };
 
 }  // namespace algo
@@ -249,4 +250,7 @@ int ieh_huffman_encode_device_batch(ie_ctx* ctx, const uint8_t* din, size_t in_p
 void ieh_release(ie_ctx* ctx);
 // Huffman post-pass of n bytes (host or device) into out (host).  Returns output bytes.
 int64_t ieh_huffman_encode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap);
+// Huffman<uint8_t>::decode alone (Huffman.cpp:354-402; the bit walk on the device): decoded byte
+// count, or 0 with *passthrough = 1 when the stream has no dictionary.
+int64_t ieh_huffman_decode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap, int* passthrough);
 }

@@ -323,6 +323,9 @@ bool huffman_decode(const uint8_t* in, size_t len, std::vector<uint8_t>& outv, u
         return true;
     }
     passthrough = false;
+    // a lone 0-bit code leaves the root a leaf: the reference's treeAddLeaf is undefined there
+    // (Huffman.cpp:155-172) and its walk would emit forever; report it as malformed
+    if (tree[0].child[0] < 0 && tree[0].child[1] < 0) return false;
     const uint64_t raw_bits = uint64_t(len) * 8;
     outv.clear();
     while (rd.pos < raw_bits) {
@@ -439,6 +442,19 @@ int64_t ieo_encode_video(const uint8_t* yuv, size_t yuv_len, int w, int h, int n
     const int64_t end = encode_frames(yuv, w, h, size_t(w), pitch, frames, n, q, rle, buf.data(), bound, uint64_t(hb), nullptr);
     if (end < 0) return end;
     return finish(buf, uint64_t(end), huffman, out, cap);
+}
+
+// Huffman<uint8_t>::decode alone (Huffman.cpp:354-402): the decoded bytes (passthrough = 0) or,
+// without a dictionary, nothing (passthrough = 1).  -3: a bit string no code prefixes.
+int64_t ieo_huffman_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, int* passthrough) {
+    std::vector<uint8_t> dec;
+    uint64_t pos = 0;
+    bool pass = false;
+    if (!huffman_decode(in, n, dec, pos, pass)) return -3;
+    if (passthrough) *passthrough = pass ? 1 : 0;
+    if (dec.size() > cap) return -2;
+    if (!dec.empty()) std::memcpy(out, dec.data(), dec.size());
+    return int64_t(dec.size());
 }
 
 int64_t ieo_huffman_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap) {

@@ -56,6 +56,9 @@ int64_t ieo_encode_video(const uint8_t* yuv, size_t yuv_len, int w, int h, int n
 
 /* Huffman post-pass over whole bytes (Huffman.cpp:233-344).  Returns output bytes. */
 int64_t ieo_huffman_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap);
+/* Huffman<uint8_t>::decode (Huffman.cpp:354-402): decoded bytes, or 0 with *passthrough = 1 when
+ * the stream carries no dictionary. */
+int64_t ieo_huffman_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, int* passthrough);
 
 /* Histogram + first occurrence of each byte value (the inputs the host tree build needs). */
 void ieo_byte_histogram(const uint8_t* in, size_t n, uint32_t* hist, uint64_t* first_pos);

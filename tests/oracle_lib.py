@@ -43,6 +43,8 @@ class Oracle:
         L.ieo_encode_video.restype = C.c_int64
         L.ieo_huffman_encode.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t]
         L.ieo_huffman_encode.restype = C.c_int64
+        L.ieo_huffman_decode.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t, C.POINTER(C.c_int)]
+        L.ieo_huffman_decode.restype = C.c_int64
         L.ieo_byte_histogram.argtypes = [_u8p, C.c_size_t, C.POINTER(C.c_uint32), _u64p]
         L.ieo_decode_image.argtypes = [_u8p, C.c_size_t, C.c_int, _u8p, C.c_size_t, C.POINTER(C.c_int),
                                        C.POINTER(C.c_int)]
@@ -125,6 +127,18 @@ class Oracle:
         r = self.lib.ieo_huffman_encode(self._p(a), a.size, self._p(out), cap)
         assert r >= 0
         return out[:r].tobytes()
+
+    def huffman_decode(self, data: bytes):
+        """(decoded bytes, passthrough) of Huffman<uint8_t>::decode; None for an invalid stream."""
+        a = np.frombuffer(data, dtype=np.uint8)
+        cap = len(data) * 8 + 16
+        out = np.zeros(cap, dtype=np.uint8)
+        pt = C.c_int(0)
+        r = self.lib.ieo_huffman_decode(self._p(a), a.size, self._p(out), cap, C.byref(pt))
+        if r == -3:
+            return None
+        assert r >= 0
+        return out[:r].tobytes(), bool(pt.value)
 
     def histogram(self, data: bytes):
         a = np.frombuffer(data, dtype=np.uint8)
