@@ -50,11 +50,17 @@ template <> struct ZigZagInv<8> {
                                     21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 };
 
+#ifndef IE_PROFILE
+#define IE_PROFILE 0
+#endif
 #ifndef IE_BPT4
 #define IE_BPT4 4
 #endif
 #ifndef IE_WAVES4
 #define IE_WAVES4 4
+#endif
+#ifndef IE_WAVES8
+#define IE_WAVES8 2
 #endif
 // Threads per tile (= per workgroup).  256 (four waves, 1024 4x4 blocks); 64 makes every wave an
 // independent tile (no workgroup barriers, 16 tiles per CU) but quadruples the look-backs, which
@@ -70,7 +76,7 @@ template <> struct Geo<4> {  // IE_BPT4 blocks side by side: 4 * IE_BPT4 bytes p
 };
 template <> struct Geo<8> {  // one block: 8 bytes per pixel row per lane
     static constexpr int BPT = 1;
-    static constexpr int WAVES = 2;
+    static constexpr int WAVES = IE_WAVES8;  // 4: <= 128 registers
 };
 
 // The tile's LDS bit image: kEncTPB * BPT records of at most rec_bits bits (the matrix's bound,
@@ -147,6 +153,32 @@ __device__ __forceinline__ int exact_coef_row(const double* P, double S, double 
     for (int ij = 0; ij < NN; ij++) {
         const double x = double(int((px.w[ij >> 2] >> (8 * (ij & 3))) & 0xFFu)) + (-128.0);
         acc = acc + P[ij] * x;
+    }
+    const double D = acc * S;
+    const double t = (rq != 0.0) ? D * rq : D / qd;
+    double r = trunc(t);
+    if (fabs(t - r) >= 0.5) r += copysign(1.0, t);
+    return int(r);
+}
+
+// exact_coef_row for a fix-up task: the block's pixel words are read from their LDS slot pw
+// (4 pixels per word) and the row through a generic pointer P (the LDS copy of a structural row or
+// the table in global memory), one pixel word per step of a loop the compiler need not unroll --
+// a register copy of the pixels indexed by a loop counter would live in scratch memory.
+template <int N>
+__device__ __forceinline__ int exact_coef_task(const double* P, double S, double rq, double qd, const uint32_t* pw) {
+    constexpr int NN = N * N;
+    double acc = 0.0;
+    for (int w = 0; w < NN / 4; w++) {
+        const uint32_t px4 = pw[w];
+        double pr[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) pr[e] = P[4 * w + e];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const double x = double(int((px4 >> (8 * e)) & 0xFFu)) + (-128.0);
+            acc = acc + pr[e] * x;
+        }
     }
     const double D = acc * S;
     const double t = (rq != 0.0) ? D * rq : D / qd;
@@ -493,7 +525,7 @@ __device__ __forceinline__ void load_tile(const EncArgs& a, const TileGeo& g, ui
 // Profiling stamps (IE_STAMPS): thread 0's s_memtime at the phase boundaries of each tile.
 #define STAMP(i)                                                                                  \
     do {                                                                                          \
-        if (a.stamps && tid == 0) a.stamps[size_t(t) * kStamps + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (stamps && tid == 0) stamps[size_t(t) * kStamps + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
 // Emission through a per-lane 64-bit accumulator: whole words are ORed into the (zeroed) image
@@ -566,6 +598,12 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     uint32_t* ctl = misc + 16;     // [4] ticket, [5..6] exclusive prefix, [7] predecessor tail
 
     const int tid = threadIdx.x;
+    // Profiling hooks (IE_ABLATE / IE_STAMPS) exist only in IE_PROFILE builds (tools/variants.sh):
+    // in the product build they are constants, so they hold no scalar registers.
+    // (The 8x8 kernel keeps them: its register allocation measured best with them live.)
+    constexpr bool kProf = IE_PROFILE || N == 8;
+    const int ablate = kProf ? a.ablate : 0;
+    uint64_t* const stamps = kProf ? a.stamps : nullptr;
     // Tile order = dispatch order.  Workgroups are dispatched in increasing blockIdx, so every
     // chain predecessor of a resident tile is resident or done and the look-back cannot
     // deadlock; the bounded spins report (never hang) should that ever not hold, and the host
@@ -595,7 +633,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
     uint32_t seg[N][WPR];
-    if (a.ablate & 128) {  // profiling: no pixel loads (synthetic pixels from the thread id)
+    if (ablate & 128) {  // profiling: no pixel loads (synthetic pixels from the thread id)
 #pragma unroll
         for (int r = 0; r < N; r++)
 #pragma unroll
@@ -606,7 +644,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     if constexpr (!EXACT) lds_barrier();  // srow visible (the pixel loads stay in flight)
 
     asm volatile("; PHASE load_done" ::: "memory");
-    if (a.stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
+    if (stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
         uint32_t acc = 0;
 #pragma unroll
         for (int r = 0; r < N; r++)
@@ -637,19 +675,19 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
         } else {
             float x[NN];
             block_pixels<N, WPR>(seg, b, x);
-            if (!(a.ablate & 16)) quotients<N>(tab, x);
+            if (!(ablate & 16)) quotients<N>(tab, x);
             if constexpr (N == 8) {
                 static_assert(BPT == 1, "8x8: one block per lane");
                 near8 = round_block_mask<N>(tab, x, zp[b]);
-                if (b >= nblk || (a.ablate & 1)) near8 = 0;
+                if (b >= nblk || (ablate & 1)) near8 = 0;
                 continue;
             }
             uint32_t sf;
             const float emax = round_block<N>(tab, x, zp[b], &sf);
             uint32_t fb = (emax >= tab->lim_min) ? 8u : sf;  // a whole-block fix covers s
-            if (a.ablate & 32) fb &= 7u;   // profiling: drop whole-block fixes
-            if (a.ablate & 64) fb &= 8u;   // profiling: drop structural fixes
-            if (b < nblk && !(a.ablate & 1)) flags |= fb << (4 * b);
+            if (ablate & 32) fb &= 7u;   // profiling: drop whole-block fixes
+            if (ablate & 64) fb &= 8u;   // profiling: drop structural fixes
+            if (b < nblk && !(ablate & 1)) flags |= fb << (4 * b);
         }
     }
     asm volatile("; PHASE quant_done" ::: "memory");
@@ -698,14 +736,16 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                 if (uint32_t(lane) < total - r0) {
                     const uint32_t tk = task[lane];
                     const int k = int(tk & 63u), owner = int(tk >> 6);
+                    const int s = (k == Structural<N>::k[0]) ? 0 : (k == Structural<N>::k[1]) ? 1
+                                : (k == Structural<N>::k[2]) ? 2 : -1;
+                    // one code path for both kinds of task: a structural row from its LDS copy,
+                    // any other from the table in global memory (rare), through a generic pointer
                     BlockPx<N> px;
 #pragma unroll
                     for (int q4 = 0; q4 < 4; q4++) {
-                        const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + kFix8Stride * owner + 4 * q4);
-                        px.w[4 * q4] = v.x; px.w[4 * q4 + 1] = v.y; px.w[4 * q4 + 2] = v.z; px.w[4 * q4 + 3] = v.w;
+                        const u32x4 w4 = *reinterpret_cast<const u32x4*>(pxl + kFix8Stride * owner + 4 * q4);
+                        px.w[4 * q4] = w4.x; px.w[4 * q4 + 1] = w4.y; px.w[4 * q4 + 2] = w4.z; px.w[4 * q4 + 3] = w4.w;
                     }
-                    const int s = (k == Structural<N>::k[0]) ? 0 : (k == Structural<N>::k[1]) ? 1
-                                : (k == Structural<N>::k[2]) ? 2 : -1;
                     uint32_t v;
                     if (s >= 0)
                         v = uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
@@ -799,7 +839,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                     const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
                     BlockPx<N> px;
                     px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
-                    res[lane] = (a.ablate & 256) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
+                    res[lane] = (ablate & 256) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
                                                  : uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s],
                                                                               srow[3 * NN + 3 + s], srow[3 * NN + 6 + s],
                                                                               px)) & 0xFFFFu;
@@ -971,13 +1011,13 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     const uint32_t off = block_excl_scan<TPB>(mybits, misc, &A);
     if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);  // successors may resolve now
     Probe pr{0, 0, 0};
-    if (tid < 64 && chain_pos != 0 && !(a.ablate & 4)) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);  // in flight during emission
+    if (tid < 64 && chain_pos != 0 && !(ablate & 4)) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);  // in flight during emission
     const uint32_t nw = (A + 31) >> 5;
     for (uint32_t w = tid; w < nw + 2; w += TPB) img[w] = 0u;
     lds_barrier();
     asm volatile("; PHASE scan_done" ::: "memory");
     STAMP(6);
-    if (!(a.ablate & 2)) {
+    if (!(ablate & 2)) {
         if (IE_EMIT_SINK) {
             if (mybits) {
                 WordSink k(img, off);
@@ -1007,7 +1047,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
     uint32_t* out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
     uint64_t excl;
-    if (a.ablate & 4) {
+    if (ablate & 4) {
         if (tid == 0) {
             publish(a.st, t, 1, a.tag, A);
             ctl[7] = 0;
@@ -1017,7 +1057,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
         excl = uint64_t(tif) * (110u * TPB);
     } else {
         excl = chain_resolve(a.st, t, chain_pos, step, a.tag, img, A, out, a.start_bit, a.err, ctl, pr,
-                             a.stamps ? &a.stamps[size_t(t) * kStamps + 1] : nullptr, true);
+                             stamps ? &stamps[size_t(t) * kStamps + 1] : nullptr, true);
     }
     if (tid == 0) {
         const uint64_t P = a.start_bit + excl;
@@ -1028,7 +1068,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     STAMP(8);
 
     // ---------------------------------------------------------------- 4. store
-    if (!(a.ablate & 8))
+    if (!(ablate & 8))
         store_tile<TPB>(out, img, A, a.start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err);
     STAMP(9);
 }

@@ -1,4 +1,5 @@
 #!/bin/bash
+# NOTE: stamps/ablations need an IE_PROFILE build: tools/variants.sh prof "-DIE_PROFILE=1", then IE_LIB=imageencoder_amd/lib/var_prof/libie_hip.so
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out; mkdir -p $O; cd $R
 for ab in ${ABS:-0}; do
