@@ -88,6 +88,9 @@ def cpu_baseline(cfg, frame: np.ndarray) -> dict | None:
                             sample=f"{iters} x {w}x{h} {cfg['gen']} frame, reference ImageEncoder::process "
                                    f"(OpenMP{', Huffman' if cfg['huffman'] else ''}) via oracle/_ref/ref_harness, "
                                    f"{threads} threads, mean {res['mean_ms']:.1f} ms/frame")
+    if cfg["n"] != 4:
+        why = ("the reference fixes its block size at compile time (Block.hpp:13, BlockSize = 4u): an 8x8 "
+               "reference build would mean editing its sources, so the 8x8 baseline is the oracle port")
     # port: the oracle restatement (single image encode, OpenMP transform, serial emission)
     oracle = O.load()
     q = O.read_matrix(cfg["matrix"], cfg["n"])
