@@ -271,6 +271,15 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
         }
         T->rec_bits = 4 + bl * (1 + nn);
     }
+    {  // the fix-up's structural rows, contiguous (encode_kernel copies them to LDS)
+        const int h = n / 2, ks[3] = {h, h * n, h * n + h};
+        for (int si = 0; si < 3; si++) {
+            for (int ij = 0; ij < nn; ij++) T->srow[si * nn + ij] = T->P[ks[si] * nn + ij];
+            T->srow[3 * nn + si] = T->S[ks[si]];
+            T->srow[3 * nn + 3 + si] = T->rq[ks[si]];
+            T->srow[3 * nn + 6 + si] = T->qd[ks[si]];
+        }
+    }
     bool ok = true;
     T->dc_exact = 0;
     T->lim_min = 0.5f;
@@ -448,6 +457,7 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.bx = g.bx;
     a.by = g.by;
     a.gpr = g.gpr;
+    a.gpr_magic = (g.gpr > 1) ? uint32_t(((uint64_t(1) << 32) + uint64_t(g.gpr) - 1) / uint64_t(g.gpr)) : 0u;
     a.groups_per_frame = g.gpf;
     a.tiles_per_frame = g.tpf;
     a.ntiles = g.ntiles;
@@ -888,7 +898,7 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
     if (reinterpret_cast<uintptr_t>(out) % 4 || out_pitch % 4)
         return fail(c, IE_EINVAL, "output and its pitch must be 4-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
-    // layout of the staged tables: tile_start[count+1] n[count] start[count] code[count*256]
+    // layout of the staged tables: tiles[count (+1 unused)] n[count] start[count] code[count*256]
     // prefix[count][pw] (words) len[count*256]
     uint64_t pw = 1, ntiles = 0;
     std::vector<uint64_t> ts(size_t(count) + 1);
@@ -905,10 +915,11 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         if (start_bit[k] && !prefix) return fail(c, IE_EINVAL, "start_bit > 0 needs a prefix");
         if ((start_bit[k] + 7) / 8 > prefix_pitch && start_bit[k]) return fail(c, IE_EINVAL, "prefix pitch too small");
         pw = std::max<uint64_t>(pw, start_bit[k] / 32 + 1);
-        ts[size_t(k)] = ntiles;
-        ntiles += (n[k] + ie::kPackTileBytes - 1) / ie::kPackTileBytes;
+        ts[size_t(k)] = (n[k] + ie::kPackTileBytes - 1) / ie::kPackTileBytes;  // tiles of string k
+        ntiles = std::max<uint64_t>(ntiles, ts[size_t(k)]);
     }
-    ts[size_t(count)] = ntiles;
+    ntiles *= uint64_t(count);  // interleaved: tile t -> string t % count (pack_kernel)
+    ts[size_t(count)] = 0;
     if (ntiles > uint64_t(INT32_MAX)) return fail(c, IE_EINVAL, "batch too large");
     const size_t K = size_t(count);
     const size_t o_ts = 0, o_n = o_ts + 8 * (K + 1), o_st = o_n + 8 * K, o_code = o_st + 8 * K;
@@ -954,7 +965,7 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         a.chain_end = c->d_chain_end;
         a.err = c->d_err;
         a.count = count;
-        a.tile_start = reinterpret_cast<const uint64_t*>(d + o_ts);
+        a.tiles = reinterpret_cast<const uint64_t*>(d + o_ts);
         a.bn = reinterpret_cast<const uint64_t*>(d + o_n);
         a.bstart = reinterpret_cast<const uint64_t*>(d + o_st);
         a.in_pitch = in_pitch;

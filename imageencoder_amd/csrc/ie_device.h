@@ -22,6 +22,9 @@ struct EncTables {
     float lim_min;  // min of lim[k] over the non-structural coefficients: one compare per block
     int dc_exact;   // t[0] is exact in FP32 (q[0] a power of two): round it directly
     int rec_bits;   // largest record (bits) any block can produce with this matrix: sizes the tile image
+    // the structural coefficients' rows P[k_s][*] (s = 0..2), then S, rq, qd of the three: the
+    // fix-up's LDS copy, one contiguous block (3*NN + 9 doubles)
+    double srow[3 * 64 + 9];
     // FP64 reference order (algo.cpp:309-331, Block.cpp:149-152)
     double S[64];   // C(u)*C(v)
     double qd[64];  // double(q[uv])
@@ -41,6 +44,7 @@ struct EncArgs {
     int w, h, nframes;
     int bx, by;              // blocks per row / column
     int gpr;                 // thread groups per block row = ceil(bx / BPT)
+    uint32_t gpr_magic;      // ceil(2^32 / gpr): exact floor(r / gpr) = mul_hi(r, magic) for r < gpr + 2^16
     int groups_per_frame;    // gpr * by
     int tiles_per_frame;     // ceil(groups_per_frame / encode_threads_per_tile())
     int ntiles;
@@ -85,12 +89,13 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
     uint32_t tag;
     uint64_t* chain_end;
     unsigned* err;
-    // batch mode (count > 0): string k owns tiles [tile_start[k], tile_start[k+1]), one chain
-    // each; its bytes at in + k*in_pitch (n[k] of them), its code table at code/len + 256*k, its
-    // output at out + k*out_pitch_words from bit start[k], the words before that from
-    // prefix + k*prefix_pitch_words (e.g. the Huffman dictionary), its end bit in chain_end[k]
+    // batch mode (count > 0): string k owns the tiles t with t % count == k (position t / count,
+    // tiles[k] of them), one chain each; its bytes at in + k*in_pitch (n[k] of them), its code
+    // table at code/len + 256*k, its output at out + k*out_pitch_words from bit start[k], the words
+    // before that from prefix + k*prefix_pitch_words (e.g. the Huffman dictionary), its end bit in
+    // chain_end[k].  ntiles = count * max_k tiles[k].
     int count;
-    const uint64_t* tile_start;  // [count + 1]
+    const uint64_t* tiles;       // [count]
     const uint64_t* bn;          // [count]
     const uint64_t* bstart;      // [count]
     uint64_t in_pitch, out_pitch_words, prefix_pitch_words;

@@ -498,11 +498,17 @@ __device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
         g.step = 1;
     }
     g.chain_pos = a.segmented ? g.tif : t;  // tiles before this one in its chain
-    const int gi = g.tif * kEncTPB + tid;
+    // group gi = base + tid: the division by gpr is split into a wave-uniform (scalar) part and a
+    // per-lane remainder r < gpr + kEncTPB, divided by a multiply-high with ceil(2^32 / gpr)
+    const int base = g.tif * kEncTPB;
+    const int q0 = base / a.gpr, r0 = base - q0 * a.gpr;
+    const uint32_t r = uint32_t(r0 + tid);
+    const uint32_t dq = (a.gpr == 1) ? r : __umulhi(r, a.gpr_magic);  // (2^32 does not fit the magic)
+    const int gi = base + tid;
     g.nblk = g.byi = g.bx0 = 0;
     if (gi < a.groups_per_frame) {
-        g.byi = gi / a.gpr;
-        g.bx0 = (gi - g.byi * a.gpr) * Geo<N>::BPT;
+        g.byi = q0 + int(dq);
+        g.bx0 = int(r - dq * uint32_t(a.gpr)) * Geo<N>::BPT;
         g.nblk = min(Geo<N>::BPT, a.bx - g.bx0);
     }
     return g;
@@ -620,14 +626,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     STAMP(0);
     if constexpr (!EXACT) {
         // issued before the pixel loads, so waiting for it does not wait for them
-        for (int i = tid; i < 3 * NN + 9; i += TPB) {
-            double v;
-            if (i < 3 * NN) v = tab->P[Structural<N>::k[i / NN] * NN + i % NN];
-            else if (i < 3 * NN + 3) v = tab->S[Structural<N>::k[i - 3 * NN]];
-            else if (i < 3 * NN + 6) v = tab->rq[Structural<N>::k[i - 3 * NN - 3]];
-            else v = tab->qd[Structural<N>::k[i - 3 * NN - 6]];
-            srow[i] = v;
-        }
+        for (int i = tid; i < 3 * NN + 9; i += TPB) srow[i] = tab->srow[i];
     }
     const TileGeo g = tile_geo<N>(a, t, tid);
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;

@@ -98,23 +98,23 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     if (a.ticket) __syncthreads();
     const int t = a.ticket ? int(misc[4]) : int(blockIdx.x);
     if (t >= a.ntiles) return;
-    // the tile's string: its chain, bytes, code table and output
-    int k = 0, chain_pos = t;
+    // the tile's string: its chain, bytes, code table and output.  A batch interleaves its strings'
+    // tiles (tile t -> string t % count, position t / count; past a string's last tile a slot is
+    // idle), so every chain advances together and each has only ~1/count of the resident tiles in
+    // flight: the look-back finds an inclusive prefix within its first window.
+    int k = 0, chain_pos = t, step = 1;
     const uint8_t* in = a.in;
     uint64_t n = a.n, start = a.start_bit;
     uint32_t* out = a.out;
     const uint32_t* hdr = a.out;  // words holding the bits before `start`
     bool last = (t == a.ntiles - 1);
     if (a.count) {
-        int lo = 0, hi = a.count - 1;  // largest k with tile_start[k] <= t
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (a.tile_start[mid] <= uint64_t(t)) lo = mid;
-            else hi = mid - 1;
-        }
-        k = lo;
-        chain_pos = t - int(a.tile_start[k]);
-        last = uint64_t(t) + 1 == a.tile_start[k + 1];
+        k = t % a.count;
+        chain_pos = t / a.count;
+        step = a.count;
+        const uint64_t tiles_k = a.tiles[k];
+        if (uint64_t(chain_pos) >= tiles_k) return;  // idle slot: no chain state, no output
+        last = uint64_t(chain_pos) + 1 == tiles_k;
         in = a.in + uint64_t(k) * a.in_pitch;
         n = a.bn[k];
         start = a.bstart[k];
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     const uint32_t off = block_excl_scan(mybits, misc, &A);
     if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);
     Probe pr{0, 0, 0};
-    if (tid < 64 && chain_pos != 0) pr = probe_issue(a.st, t, chain_pos, 1, 0, kProbe0);
+    if (tid < 64 && chain_pos != 0) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
     const uint32_t nw = (A + 31) >> 5;
     for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
     __syncthreads();
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     __syncthreads();
 
     // one chain per string in tile order -- the same protocol as encode_kernel
-    const uint64_t excl = chain_resolve(a.st, t, chain_pos, 1, a.tag, img, A, hdr, start, a.err, misc, pr);
+    const uint64_t excl = chain_resolve(a.st, t, chain_pos, step, a.tag, img, A, hdr, start, a.err, misc, pr);
     if (tid == 0 && last) a.chain_end[k] = start + excl + A;
     store_image(out, img, A, start + excl, misc[7], last);
 }
