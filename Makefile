@@ -33,7 +33,7 @@ $(LIBDIR)/libie_hip.so: $(OBJS)
 # ---- host library mirroring the reference interface (libie_host.so) + encoder/decoder CLIs
 HOSTSRC   := $(wildcard $(CSRC)/host/*.cpp)
 HOSTHDR   := $(wildcard $(CSRC)/host/*.hpp) include/ie_host.hpp include/ie_hip.h
-HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC)/host -Wall -Wextra -Wno-unused-parameter
+HOSTFLAGS := -O2 -std=c++17 -fPIC -fopenmp -Iinclude -I$(CSRC)/host -Wall -Wextra -Wno-unused-parameter
 HOSTOBJS  := $(patsubst $(CSRC)/host/%.cpp,$(OBJDIR)/host/%.o,$(HOSTSRC))
 RPATH     := -Wl,-rpath,'$$ORIGIN'
 host: $(LIBDIR)/libie_host.so $(LIBDIR)/encoder $(LIBDIR)/encoder_nohuff $(LIBDIR)/decoder
@@ -43,7 +43,7 @@ $(OBJDIR)/host/%.o: $(CSRC)/host/%.cpp $(HOSTHDR)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
 $(LIBDIR)/libie_host.so: $(HOSTOBJS) $(LIBDIR)/libie_hip.so
-	$(CXX) -shared $(HOSTOBJS) -L$(LIBDIR) -lie_hip $(RPATH) -o $@
+	$(CXX) -shared -fopenmp $(HOSTOBJS) -L$(LIBDIR) -lie_hip $(RPATH) -o $@
 
 $(LIBDIR)/encoder: $(CSRC)/cli/main.cpp $(LIBDIR)/libie_host.so
 	$(CXX) $(HOSTFLAGS) -DENCODER -DENABLE_HUFFMAN $< -L$(LIBDIR) -lie_host -lie_hip $(RPATH) -o $@

@@ -10,6 +10,10 @@
 // both (a) and the first position of every value, so inserting the values in first-position
 // order into the same libstdc++ containers reproduces every step.
 #include <algorithm>
+#include <omp.h>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <queue>
@@ -168,12 +172,17 @@ int64_t huffman_device(ie_ctx* c, const uint8_t* din, size_t n, dc::DeviceBuffer
 int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count, uint8_t* dout,
                          size_t out_pitch, int64_t* bytes, std::string& err) {
     const size_t K = size_t(count);
+    // IE_HTIME=1: per-stage host timing to stderr (profiling aid)
+    static const bool htime = getenv("IE_HTIME") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = now();
     std::vector<uint32_t> hist(256 * K), code(256 * K);
     std::vector<uint64_t> first(256 * K), start(K);
     std::vector<uint8_t> len(256 * K);
     int r;
     if ((r = ie_huffman_hist_batch(c, din, in_pitch, n, count, hist.data(), first.data())))
         return (err = ie_last_error(c), r);
+    const auto t1 = now();
     std::vector<std::vector<uint8_t>> dict(K);
     std::vector<std::string> errs(K);
     std::vector<char> ok(K, 1);
@@ -209,17 +218,11 @@ int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const u
         start[k] = dict_bits;
         bytes[k] = int64_t(total);
     };
-    const size_t T = std::min<size_t>(K, std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
-    if (T <= 1) {
-        for (size_t k = 0; k < K; k++) build(k);
-    } else {
-        std::vector<std::thread> pool;
-        for (size_t i = 0; i < T; i++)
-            pool.emplace_back([&, i] {
-                for (size_t k = i; k < K; k += T) build(k);
-            });
-        for (auto& th : pool) th.join();
-    }
+    // one tree per string on OpenMP's persistent thread team (no thread start-up per call)
+    const int T = int(std::min<size_t>(K, size_t(std::max(1, std::min(16, omp_get_max_threads())))));
+#pragma omp parallel for schedule(dynamic, 1) num_threads(T) if (T > 1)
+    for (int k = 0; k < int(K); k++) build(size_t(k));
+    const auto t2 = now();
     for (size_t k = 0; k < K; k++)
         if (!ok[k]) return (err = errs[k], IE_EINVAL);
     size_t pp = 4;
@@ -229,6 +232,12 @@ int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const u
     if ((r = ie_huffman_pack_batch(c, din, in_pitch, n, count, code.data(), len.data(), prefix.data(), pp, dout,
                                    out_pitch, start.data(), nullptr)))
         return (err = ie_last_error(c), r);
+    if (htime) {
+        const auto t3 = now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[htime] hist+readback %.1f us, trees %.1f us, pack submit %.1f us\n", us(t0, t1), us(t1, t2),
+                us(t2, t3));
+    }
     return IE_OK;
 }
 
