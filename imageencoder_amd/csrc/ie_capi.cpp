@@ -579,7 +579,8 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
     }
     uint64_t end = start_bit;
     if (n) {
-        const int ntiles = int((n + ie::kTPB * ie::kPackBytesPerThread - 1) / (ie::kTPB * ie::kPackBytesPerThread));
+        const uint64_t tb = uint64_t(ie::pack_tile_bytes(int(maxlen)));
+        const int ntiles = int((n + tb - 1) / tb);
         if ((r = prepare_state(c, ntiles, 1))) return r;
         ie::PackArgs a{};
         a.in = din;
@@ -595,6 +596,7 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
         a.tag = c->tag;
         a.chain_end = c->d_chain_end;
         a.err = c->d_err;
+        a.maxlen = int(maxlen);
         ie::launch_pack(a, c->stream);
         HIPCHK(c, hipGetLastError());
         if (c->use_ticket) c->ticket_base += uint64_t(ntiles);
@@ -902,6 +904,9 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
     // prefix[count][pw] (words) len[count*256]
     uint64_t pw = 1, ntiles = 0;
     std::vector<uint64_t> ts(size_t(count) + 1);
+    unsigned maxlen_all = 0;  // one tile shape for the whole batch
+    for (int k = 0; k < count * 256; k++) maxlen_all = std::max<unsigned>(maxlen_all, len[k]);
+    const uint64_t tb = uint64_t(ie::pack_tile_bytes(int(maxlen_all)));
     for (int k = 0; k < count; k++) {
         if (k + 1 < count && n[k] > in_pitch) return fail(c, IE_EINVAL, "string longer than the input pitch");
         unsigned maxlen = 0;
@@ -915,7 +920,7 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         if (start_bit[k] && !prefix) return fail(c, IE_EINVAL, "start_bit > 0 needs a prefix");
         if ((start_bit[k] + 7) / 8 > prefix_pitch && start_bit[k]) return fail(c, IE_EINVAL, "prefix pitch too small");
         pw = std::max<uint64_t>(pw, start_bit[k] / 32 + 1);
-        ts[size_t(k)] = (n[k] + ie::kPackTileBytes - 1) / ie::kPackTileBytes;  // tiles of string k
+        ts[size_t(k)] = (n[k] + tb - 1) / tb;  // tiles of string k
         ntiles = std::max<uint64_t>(ntiles, ts[size_t(k)]);
     }
     ntiles *= uint64_t(count);  // interleaved: tile t -> string t % count (pack_kernel)
@@ -972,6 +977,7 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         a.out_pitch_words = out_pitch / 4;
         a.prefix_pitch_words = pw;
         a.prefix = reinterpret_cast<const uint32_t*>(d + o_pre);
+        a.maxlen = int(maxlen_all);
         ie::launch_pack(a, c->stream);
         HIPCHK(c, hipGetLastError());
         if (c->use_ticket) c->ticket_base += ntiles;

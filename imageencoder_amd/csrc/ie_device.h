@@ -100,9 +100,10 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
     const uint64_t* bstart;      // [count]
     uint64_t in_pitch, out_pitch_words, prefix_pitch_words;
     const uint32_t* prefix;
+    int maxlen;                  // longest code in the table(s): picks the tile shape
 };
-constexpr int kPackBytesPerThread = 16;
-constexpr int kPackTileBytes = 256 * kPackBytesPerThread;
+// input bytes per pack tile for codes of at most maxlen bits (ie_huffman.hip)
+int pack_tile_bytes(int maxlen);
 void launch_pack(const PackArgs& a, hipStream_t s);
 void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, hipStream_t s);
 // count strings at in + k*pitch, n[k] (device array) bytes each, maxn >= every n[k]:

@@ -83,10 +83,12 @@ void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uin
     hipLaunchKernelGGL(hist_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist, first);
 }
 
-// One tile = kTPB threads x kPackBytesPerThread input bytes, codes of up to 32 bits.
-constexpr int kPackWords = kTPB * kPackBytesPerThread + 4;  // 32 bits per byte worst case
-
+// One tile = kTPB threads x BPT input bytes, codes of up to MAXLEN bits: <16, 32> for any code,
+// <64, 16> for Huffman codes (<= 15 bits) and the identity copy -- 4x the bytes per tile, so a
+// quarter of the tiles (and look-backs) for the same LDS image size.
+template <int BPT, int MAXLEN>
 __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
+    constexpr int kPackWords = kTPB * BPT * MAXLEN / 32 + 4;
     __shared__ uint32_t smem[kPackWords + 32];
     __shared__ uint32_t s_code[256];
     __shared__ uint8_t s_len[256];
@@ -127,22 +129,29 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     s_len[tid] = a.len[256 * k + tid];
     __syncthreads();
 
-    const uint64_t p = uint64_t(chain_pos) * (kTPB * kPackBytesPerThread) + uint64_t(tid) * kPackBytesPerThread;
-    uint8_t b[kPackBytesPerThread];
+    const uint64_t p = uint64_t(chain_pos) * (kTPB * BPT) + uint64_t(tid) * BPT;
+    uint32_t w[BPT / 4];  // the thread's bytes, four per word
     int nb = 0;
-    if (p < n) nb = int(min<uint64_t>(kPackBytesPerThread, n - p));
-    if (nb == kPackBytesPerThread && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
-        const uint4 v = *reinterpret_cast<const uint4*>(in + p);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (p < n) nb = int(min<uint64_t>(BPT, n - p));
+    if (nb == BPT && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
 #pragma unroll
-        for (int e = 0; e < 16; e++) b[e] = uint8_t(w[e >> 2] >> (8 * (e & 3)));
+        for (int q = 0; q < BPT / 16; q++) {
+            const uint4 v = *reinterpret_cast<const uint4*>(in + p + 16 * q);
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        }
     } else {
 #pragma unroll
-        for (int e = 0; e < kPackBytesPerThread; e++) b[e] = (e < nb) ? in[p + e] : 0;
+        for (int q = 0; q < BPT / 4; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) v |= (4 * q + e < nb) ? uint32_t(in[p + 4 * q + e]) << (8 * e) : 0u;
+            w[q] = v;
+        }
     }
+    auto byte = [&](int e) -> uint32_t { return (w[e >> 2] >> (8 * (e & 3))) & 0xFFu; };
     uint32_t mybits = 0;
 #pragma unroll
-    for (int e = 0; e < kPackBytesPerThread; e++) mybits += (e < nb) ? s_len[b[e]] : 0u;
+    for (int e = 0; e < BPT; e++) mybits += (e < nb) ? s_len[byte(e)] : 0u;
 
     uint32_t A;
     const uint32_t off = block_excl_scan(mybits, misc, &A);
@@ -155,8 +164,8 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     if (mybits) {
         BitSink sink(img, off);
 #pragma unroll
-        for (int e = 0; e < kPackBytesPerThread; e++)
-            if (e < nb) sink.put(s_len[b[e]], s_code[b[e]]);
+        for (int e = 0; e < BPT; e++)
+            if (e < nb) sink.put(s_len[byte(e)], s_code[byte(e)]);
         sink.finish();
     }
     __syncthreads();
@@ -167,8 +176,11 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     store_image(out, img, A, start + excl, misc[7], last);
 }
 
+int pack_tile_bytes(int maxlen) { return maxlen <= 16 ? kTPB * 64 : kTPB * 16; }
+
 void launch_pack(const PackArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(pack_kernel, dim3(a.ntiles), dim3(kTPB), 0, s, a);
+    if (a.maxlen <= 16) hipLaunchKernelGGL((pack_kernel<64, 16>), dim3(a.ntiles), dim3(kTPB), 0, s, a);
+    else hipLaunchKernelGGL((pack_kernel<16, 32>), dim3(a.ntiles), dim3(kTPB), 0, s, a);
 }
 
 }  // namespace ie
