@@ -829,7 +829,7 @@ int ie_huffman_hist(ie_ctx* c, const uint8_t* bytes, size_t n, uint32_t* hist, u
     }
     HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 256 * sizeof(uint32_t), c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_first, 0xFF, 256 * sizeof(unsigned long long), c->stream));
-    if (n) ie::launch_hist(din, n, c->d_hist, c->d_first, c->stream);
+    if (n) ie::launch_hist(din, n, c->d_hist, c->d_first, reinterpret_cast<unsigned*>(c->d_misc + 3), c->stream);
     HIPCHK(c, hipGetLastError());
     const hipMemcpyKind k1 = is_device_ptr(hist) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     const hipMemcpyKind k2 = is_device_ptr(first_pos) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -868,9 +868,9 @@ int ie_huffman_hist_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         maxn = std::max(maxn, n[k]);
     }
     const size_t hb = size_t(count) * 256 * sizeof(uint32_t), fb = size_t(count) * 256 * sizeof(uint64_t);
-    const size_t nb = size_t(count) * sizeof(uint64_t);
+    const size_t nb = size_t(count) * sizeof(uint64_t), ub = size_t(count) * sizeof(unsigned);
     int r;
-    if ((r = ensure(c, c->d_batch, c->cap_batch, hb + fb + nb))) return r;
+    if ((r = ensure(c, c->d_batch, c->cap_batch, hb + fb + nb + ub))) return r;
     if ((r = ensure_pinned(c, c->h_batch, c->cap_hbatch, nb))) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));  // the pinned staging may still feed a copy
     std::memcpy(c->h_batch, n, nb);
@@ -880,7 +880,8 @@ int ie_huffman_hist_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
     HIPCHK(c, hipMemcpyAsync(dn, c->h_batch, nb, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(dh, 0, hb, c->stream));
     HIPCHK(c, hipMemsetAsync(df, 0xFF, fb, c->stream));
-    ie::launch_hist_batch(in, in_pitch, dn, maxn, count, dh, df, c->stream);
+    auto* du = reinterpret_cast<unsigned*>(c->d_batch + hb + fb + nb);
+    ie::launch_hist_batch(in, in_pitch, dn, maxn, count, dh, df, du, c->stream);
     HIPCHK(c, hipGetLastError());
     const hipMemcpyKind k1 = is_device_ptr(hist) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     const hipMemcpyKind k2 = is_device_ptr(first_pos) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;

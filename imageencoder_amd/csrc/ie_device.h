@@ -105,11 +105,13 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
 // input bytes per pack tile for codes of at most maxlen bits (ie_huffman.hip)
 int pack_tile_bytes(int maxlen);
 void launch_pack(const PackArgs& a, hipStream_t s);
-void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, hipStream_t s);
+// unresolved: device scratch, one word per string
+void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, unsigned* unresolved,
+                 hipStream_t s);
 // count strings at in + k*pitch, n[k] (device array) bytes each, maxn >= every n[k]:
 // hist/first + 256*k
 void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count, uint32_t* hist,
-                       unsigned long long* first, hipStream_t s);
+                       unsigned long long* first, unsigned* unresolved, hipStream_t s);
 
 struct DecArgs {
     const uint64_t* block_bit;  // [nblocks] start bit of every block record (from the walk index)

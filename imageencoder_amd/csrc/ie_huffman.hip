@@ -19,68 +19,137 @@ namespace ie {
 
 constexpr int kHistTile = kTPB * 16;  // bytes per workgroup pass
 
-// Histogram + first occurrence of bytes [0, n) of `in`, grid-strided over workgroups
-// blockIdx.x of gridDim.x; merged into hist / first with global atomics.
-__device__ __forceinline__ void hist_body(const uint8_t* __restrict__ in, uint64_t n, uint32_t* hist,
-                                          unsigned long long* first) {
-    __shared__ uint32_t h[256];
-    __shared__ unsigned long long f[256];
-    const int tid = threadIdx.x;
-    h[tid] = 0;
-    f[tid] = ~0ull;
+// Byte histogram of [0, n) of `in`, grid-strided over workgroups blockIdx.x of gridDim.x: one
+// non-returning LDS add per byte into the wave's own sub-histogram, merged with global atomics.
+// The first occurrences (the reference's unordered_map insertion order) come from first_scan /
+// first_full below, which only touch the bytes up to each value's first appearance.
+__device__ __forceinline__ void hist_body(const uint8_t* __restrict__ in, uint64_t n, uint32_t* hist) {
+    __shared__ uint32_t h[4][256];
+    const int tid = threadIdx.x, wv = tid >> 6;
+#pragma unroll
+    for (int q = 0; q < 4; q++) h[q][tid] = 0;
     __syncthreads();
+    const bool al = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
     for (uint64_t base = uint64_t(blockIdx.x) * kHistTile; base < n; base += uint64_t(gridDim.x) * kHistTile) {
         const uint64_t p = base + uint64_t(tid) * 16;
-        uint8_t b[16];
-        if (p + 16 <= n && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
+        if (p + 16 <= n && al) {
             const uint4 v = *reinterpret_cast<const uint4*>(in + p);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int e = 0; e < 16; e++) b[e] = uint8_t(w[e >> 2] >> (8 * (e & 3)));
+            for (int e = 0; e < 16; e++) atomicAdd(&h[wv][(w[e >> 2] >> (8 * (e & 3))) & 0xFFu], 1u);
         } else {
-#pragma unroll
-            for (int e = 0; e < 16; e++) b[e] = (p + e < n) ? in[p + e] : 0;
-        }
-#pragma unroll
-        for (int e = 0; e < 16; e++) {
-            if (p + e < n) {
-                atomicAdd(&h[b[e]], 1u);
-                if (f[b[e]] > p + e) atomicMin(&f[b[e]], (unsigned long long)(p + e));
-            }
+            for (int e = 0; e < 16; e++)
+                if (p + e < n) atomicAdd(&h[wv][in[p + e]], 1u);
         }
     }
     __syncthreads();
-    if (h[tid]) {
-        atomicAdd(&hist[tid], h[tid]);
-        atomicMin(&first[tid], f[tid]);
-    }
+    const uint32_t c = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    if (c) atomicAdd(&hist[tid], c);
 }
 
-__global__ __launch_bounds__(kTPB) void hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t* hist,
-                                                     unsigned long long* first) {
-    hist_body(in, n, hist, first);
+// First occurrence of every byte value that occurs (hist > 0), scanning from the start of the
+// string in kHistTile chunks and stopping as soon as all of them are found: for encoder output
+// (every value appears within a few KiB) one or two chunks.  At most kFirstScanChunks chunks;
+// values still missing after that are left to first_full (unresolved[k] = 1).
+constexpr int kFirstScanChunks = 64;
+__device__ __forceinline__ void first_scan_body(const uint8_t* __restrict__ in, uint64_t n, const uint32_t* hist,
+                                                unsigned long long* first, unsigned* unresolved) {
+    __shared__ unsigned long long f[256];
+    const int tid = threadIdx.x;
+    f[tid] = ~0ull;
+    const int need = __syncthreads_count(hist[tid] != 0u);
+    int have = 0;
+    for (int ch = 0; ch < kFirstScanChunks && have < need; ch++) {
+        const uint64_t p = uint64_t(ch) * kHistTile + uint64_t(tid) * 16;
+        for (int e = 0; e < 16; e++)
+            if (p + e < n) {
+                const uint32_t b = in[p + e];
+                // (> and not "unset": another thread of this chunk may have set a later position)
+                if (f[b] > p + e) atomicMin(&f[b], (unsigned long long)(p + e));
+            }
+        have = __syncthreads_count(f[tid] != ~0ull);
+        if (uint64_t(ch + 1) * kHistTile >= n) break;
+    }
+    first[tid] = f[tid];
+    if (tid == 0) *unresolved = (have < need) ? 1u : 0u;
+}
+
+// The values first_scan did not find: every byte of the string (past the scanned prefix) checks a
+// per-value "missing" flag; atomicMin where set.  Workgroups of resolved strings exit at once.
+__device__ __forceinline__ void first_full_body(const uint8_t* __restrict__ in, uint64_t n, const uint32_t* hist,
+                                                unsigned long long* first, const unsigned* unresolved) {
+    if (*unresolved == 0u) return;
+    __shared__ unsigned long long f[256];
+    __shared__ uint8_t miss[256];
+    const int tid = threadIdx.x;
+    f[tid] = ~0ull;
+    miss[tid] = (hist[tid] != 0u && first[tid] == ~0ull) ? 1 : 0;
+    __syncthreads();
+    const uint64_t from = uint64_t(kFirstScanChunks) * kHistTile;
+    for (uint64_t base = from + uint64_t(blockIdx.x) * kHistTile; base < n; base += uint64_t(gridDim.x) * kHistTile) {
+        const uint64_t p = base + uint64_t(tid) * 16;
+        for (int e = 0; e < 16; e++)
+            if (p + e < n) {
+                const uint32_t b = in[p + e];
+                if (miss[b] && f[b] > p + e) atomicMin(&f[b], (unsigned long long)(p + e));
+            }
+    }
+    __syncthreads();
+    if (miss[tid] && f[tid] != ~0ull) atomicMin(&first[tid], f[tid]);
+}
+
+__global__ __launch_bounds__(kTPB) void hist_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t* hist) {
+    hist_body(in, n, hist);
+}
+__global__ __launch_bounds__(kTPB) void first_scan_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                          const uint32_t* hist, unsigned long long* first,
+                                                          unsigned* unresolved) {
+    first_scan_body(in, n, hist, first, unresolved);
+}
+__global__ __launch_bounds__(kTPB) void first_full_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                          const uint32_t* hist, unsigned long long* first,
+                                                          const unsigned* unresolved) {
+    first_full_body(in, n, hist, first, unresolved);
 }
 
 // string blockIdx.y of a batch
 __global__ __launch_bounds__(kTPB) void hist_batch_kernel(const uint8_t* __restrict__ in, uint64_t pitch,
-                                                           const uint64_t* __restrict__ n, uint32_t* hist,
-                                                           unsigned long long* first) {
+                                                           const uint64_t* __restrict__ n, uint32_t* hist) {
     const int k = blockIdx.y;
-    hist_body(in + uint64_t(k) * pitch, n[k], hist + 256 * k, first + 256 * k);
+    hist_body(in + uint64_t(k) * pitch, n[k], hist + 256 * k);
+}
+__global__ __launch_bounds__(kTPB) void first_scan_batch_kernel(const uint8_t* __restrict__ in, uint64_t pitch,
+                                                                const uint64_t* __restrict__ n, const uint32_t* hist,
+                                                                unsigned long long* first, unsigned* unresolved) {
+    const int k = blockIdx.x;
+    first_scan_body(in + uint64_t(k) * pitch, n[k], hist + 256 * k, first + 256 * k, unresolved + k);
+}
+__global__ __launch_bounds__(kTPB) void first_full_batch_kernel(const uint8_t* __restrict__ in, uint64_t pitch,
+                                                                const uint64_t* __restrict__ n, const uint32_t* hist,
+                                                                unsigned long long* first, const unsigned* unresolved) {
+    const int k = blockIdx.y;
+    first_full_body(in + uint64_t(k) * pitch, n[k], hist + 256 * k, first + 256 * k, unresolved + k);
 }
 
-void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, hipStream_t s) {
+// unresolved: one word per string (device scratch)
+void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, unsigned* unresolved,
+                 hipStream_t s) {
     const uint64_t tiles = (n + kHistTile - 1) / kHistTile;
     const int grid = int(tiles < 2048 ? (tiles ? tiles : 1) : 2048);
-    hipLaunchKernelGGL(hist_kernel, dim3(grid), dim3(kTPB), 0, s, in, n, hist, first);
+    hipLaunchKernelGGL(hist_kernel, dim3(grid), dim3(kTPB), 0, s, in, n, hist);
+    hipLaunchKernelGGL(first_scan_kernel, dim3(1), dim3(kTPB), 0, s, in, n, hist, first, unresolved);
+    hipLaunchKernelGGL(first_full_kernel, dim3(grid), dim3(kTPB), 0, s, in, n, hist, first, unresolved);
 }
 
 void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count, uint32_t* hist,
-                       unsigned long long* first, hipStream_t s) {
+                       unsigned long long* first, unsigned* unresolved, hipStream_t s) {
     const uint64_t tiles = (maxn + kHistTile - 1) / kHistTile;
     const uint64_t per = (4096 + count - 1) / count;  // ~4096 workgroups over the batch
     const int gx = int(tiles < per ? (tiles ? tiles : 1) : per);
-    hipLaunchKernelGGL(hist_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist, first);
+    hipLaunchKernelGGL(hist_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist);
+    hipLaunchKernelGGL(first_scan_batch_kernel, dim3(count), dim3(kTPB), 0, s, in, pitch, n, hist, first, unresolved);
+    hipLaunchKernelGGL(first_full_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist, first,
+                       unresolved);
 }
 
 // One tile = kTPB threads x BPT input bytes, codes of up to MAXLEN bits: <16, 32> for any code,

@@ -89,6 +89,12 @@ def _byte_sets():
     yield "fib", b"".join(bytes([i]) * f for i, f in enumerate([1, 1, 2, 3, 5, 8, 13, 21, 34, 55, 89, 144]))
     enc = O.load().encode_blocks(synth.frame("U", 512, 256), 4, O.read_matrix("matrix.txt", 4))[0]
     yield "encoded", enc[:60_000].tobytes()
+    # values that first appear past the first-occurrence scan's prefix (64 x 4 KiB): the full pass
+    late = rng.integers(0, 200, 1_200_003, dtype=np.uint8)
+    for v, at in ((230, 300_000), (201, 700_001), (255, 1_200_002), (210, 262_144), (220, 262_143)):
+        late[at] = v
+    late[900_000:900_016] = 240
+    yield "late_values", late.tobytes()
 
 
 BYTE_SETS = list(_byte_sets())
