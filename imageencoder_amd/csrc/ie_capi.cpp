@@ -26,7 +26,7 @@ struct ie_ctx {
     ie::EncTables* d_tab = nullptr;
 
     // decoupled look-back state
-    uint64_t* d_state = nullptr;  // [3 * cap_tiles] tile chain granules (ie_common.cuh)
+    uint64_t* d_state = nullptr;  // [kStateWordsPerTile * cap_tiles] tile chain granules (ie_common.cuh)
     size_t cap_tiles = 0;
     uint32_t tag = 0;
     unsigned long long* d_ticket = nullptr;
@@ -319,16 +319,16 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
             HIPCHK(c, hipFree(c->d_state));
         }
         const size_t cap = std::max<size_t>(ntiles, c->cap_tiles * 2);
-        HIPCHK(c, hipMalloc(&c->d_state, 3 * cap * sizeof(uint64_t)));
+        HIPCHK(c, hipMalloc(&c->d_state, size_t(ie::kStateWordsPerTile) * cap * sizeof(uint64_t)));
         if (c->d_wave_fix) HIPCHK(c, hipFree(c->d_wave_fix));
         HIPCHK(c, hipMalloc(&c->d_wave_fix, cap * 16 * sizeof(uint32_t)));
-        HIPCHK(c, hipMemsetAsync(c->d_state, 0, 3 * cap * sizeof(uint64_t), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->d_state, 0, size_t(ie::kStateWordsPerTile) * cap * sizeof(uint64_t), c->stream));
         c->cap_tiles = cap;
         c->tag = 0;
     }
     c->tag++;
     if (c->tag > 255) {
-        HIPCHK(c, hipMemsetAsync(c->d_state, 0, 3 * c->cap_tiles * sizeof(uint64_t), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->d_state, 0, size_t(ie::kStateWordsPerTile) * c->cap_tiles * sizeof(uint64_t), c->stream));
         c->tag = 1;
     }
     if (size_t(nframes) > c->cap_frames) {

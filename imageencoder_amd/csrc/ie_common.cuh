@@ -135,7 +135,13 @@ __device__ __forceinline__ void st_state(uint64_t* p, uint64_t v) {
 //   st[3t+1] = {tag:8 | inclusive:56}   once the look-back has resolved the exclusive prefix
 //   st[3t+2] = {tag:8 | tail:32}        the last 32 bits of the chain up to and including t
 // The early aggregate lets successors resolve their offsets while this tile is still emitting.
-constexpr int kGran = 3;
+// granules per tile in the state array: 3 packed (24 B per tile) or IE_GRAN_STRIDE words apart
+// (16: each tile's state in a 128-B line of its own, no false sharing between tiles)
+#ifndef IE_GRAN_STRIDE
+#define IE_GRAN_STRIDE 16
+#endif
+constexpr int kGran = IE_GRAN_STRIDE;
+static_assert(kGran >= 3 && kGran <= kStateWordsPerTile, "three granules per tile within the allocation");
 
 __device__ __forceinline__ void publish(uint64_t* st, int t, int g, uint32_t tag, uint64_t v) {
     st_state(&st[kGran * t + g], (uint64_t(tag) << 56) | (v & kMask56));

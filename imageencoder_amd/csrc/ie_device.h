@@ -71,6 +71,8 @@ struct EncArgs {
 };
 
 constexpr int kStamps = 16;
+// chain-state words per tile (the host allocates; ie_common.cuh kGran must not exceed it)
+constexpr int kStateWordsPerTile = 16;
 void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s);
 int encode_blocks_per_thread(int n);  // horizontally adjacent blocks per lane (Geo<N>::BPT)
 int encode_threads_per_tile();       // threads per encoder workgroup (= tile)
