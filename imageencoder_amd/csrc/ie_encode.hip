@@ -60,7 +60,7 @@ template <> struct ZigZagInv<8> {
 #define IE_WAVES4 4
 #endif
 #ifndef IE_WAVES8
-#define IE_WAVES8 2
+#define IE_WAVES8 4
 #endif
 // Threads per tile (= per workgroup).  256 (four waves, 1024 4x4 blocks); 64 makes every wave an
 // independent tile (no workgroup barriers, 16 tiles per CU) but quadruples the look-backs, which
@@ -104,7 +104,9 @@ constexpr int kFixWords = kFixTasks + (kEncTPB / 64) * 128;   // the image is ne
 #endif
 constexpr int kFix8Stride = 20;
 constexpr int kFix8Tasks = kFix8Stride * kEncTPB;
-constexpr int kFix8Words = kFix8Tasks + (kEncTPB / 64) * 128;
+constexpr int kNsStage = 4;  // non-structural rows staged per pass, per wave
+constexpr int kFix8Stage = kFix8Tasks + (kEncTPB / 64) * 128;
+constexpr int kFix8Words = kFix8Stage + (kEncTPB / 64) * kNsStage * 64 * 2;
 
 template <int WPR>
 __device__ __forceinline__ uint32_t pix(const uint32_t (&row)[WPR], int byte) {
@@ -732,27 +734,43 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                     i++;
                 }
                 wave_sync();
-                if (uint32_t(lane) < total - r0) {
-                    const uint32_t tk = task[lane];
-                    const int k = int(tk & 63u), owner = int(tk >> 6);
-                    const int s = (k == Structural<N>::k[0]) ? 0 : (k == Structural<N>::k[1]) ? 1
-                                : (k == Structural<N>::k[2]) ? 2 : -1;
-                    // one code path for both kinds of task: a structural row from its LDS copy,
-                    // any other from the table in global memory (rare), through a generic pointer
-                    BlockPx<N> px;
-#pragma unroll
-                    for (int q4 = 0; q4 < 4; q4++) {
-                        const u32x4 w4 = *reinterpret_cast<const u32x4*>(pxl + kFix8Stride * owner + 4 * q4);
-                        px.w[4 * q4] = w4.x; px.w[4 * q4 + 1] = w4.y; px.w[4 * q4 + 2] = w4.z; px.w[4 * q4 + 3] = w4.w;
+                const bool busy = uint32_t(lane) < total - r0;
+                const uint32_t tk = busy ? task[lane] : 0u;
+                const int k = int(tk & 63u), owner = int(tk >> 6);
+                const int s = (k == Structural<N>::k[0]) ? 0 : (k == Structural<N>::k[1]) ? 1
+                            : (k == Structural<N>::k[2]) ? 2 : -1;
+                // Structural rows come from the LDS copy; any other task's row (rare) is staged
+                // through LDS by the whole wave first, kNsStage rows per pass (one coalesced row
+                // per load), so no dependent add of the FP64 chain waits on global memory.
+                uint64_t ns = __ballot(busy && s < 0);
+                bool done = !busy;
+                double* stage = reinterpret_cast<double*>(img + kFix8Stage) + (tid >> 6) * (kNsStage * NN);
+                do {
+                    int slot = -1;
+                    for (int r = 0; r < kNsStage && ns; r++) {
+                        const int L = __ffsll((unsigned long long)ns) - 1;
+                        ns &= ns - 1;
+                        const int kr = __builtin_amdgcn_readlane(k, L);
+                        stage[r * NN + lane] = tab->P[kr * NN + lane];  // NN = 64 = one double per lane
+                        if (lane == L) slot = r;
                     }
-                    uint32_t v;
-                    if (s >= 0)
-                        v = uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
-                                                       srow[3 * NN + 6 + s], px));
-                    else
-                        v = uint32_t(exact_coef_inl<N>(tab, k, px));
-                    res[lane] = v & 0xFFFFu;
-                }
+                    wave_sync();
+                    if (!done && (s >= 0 || slot >= 0)) {
+                        BlockPx<N> px;
+#pragma unroll
+                        for (int q4 = 0; q4 < 4; q4++) {
+                            const u32x4 w4 = *reinterpret_cast<const u32x4*>(pxl + kFix8Stride * owner + 4 * q4);
+                            px.w[4 * q4] = w4.x; px.w[4 * q4 + 1] = w4.y; px.w[4 * q4 + 2] = w4.z; px.w[4 * q4 + 3] = w4.w;
+                        }
+                        const double* P = (s >= 0) ? srow + s * NN : stage + slot * NN;
+                        const double S = (s >= 0) ? srow[3 * NN + s] : tab->S[k];
+                        const double rq = (s >= 0) ? srow[3 * NN + 3 + s] : tab->rq[k];
+                        const double qd = (s >= 0) ? srow[3 * NN + 6 + s] : tab->qd[k];
+                        res[lane] = uint32_t(exact_coef_row<N>(P, S, rq, qd, px)) & 0xFFFFu;
+                        done = true;
+                    }
+                    wave_sync();  // the next pass rewrites the staged rows
+                } while (ns);
                 wave_sync();
                 m = near8;
                 i = pre - r0;
