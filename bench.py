@@ -200,10 +200,11 @@ def main():
             def step(i):
                 slot = i % nslots
                 out = outs[i % len(outs)]
-                ends = codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, out, out_pitch=pitch,
-                                           nframes=B, start_bit=hdr_bits, mode=mode)
-                # the batch's Huffman pass: one histogram launch, host tree builds, one pack launch
-                hsizes[:] = codec.huffman_encode_batch(out, pitch, [(int(e) + 7) // 8 for e in ends], houts, hpitch)
+                codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, out, out_pitch=pitch,
+                                    nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False)
+                # the batch's Huffman pass: one histogram launch (lengths from the encoder's end
+                # bits on the device), host tree builds, one pack launch
+                hsizes[:] = codec.huffman_encode_after_encode(out, pitch, B, houts, hpitch)
         wall, gpu_s = timer.run(step, args.warmup, args.steps)
         px_total = world * args.steps * B * w * h
         in_bytes_per_launch = B * w * h

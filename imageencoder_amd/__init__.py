@@ -110,6 +110,8 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
     H.ieh_decode_video.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip, ip]
     H.ieh_huffman_encode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t]
     H.ieh_huffman_decode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, ip]
+    H.ieh_huffman_encode_after_encode.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, vp]
+    H.ieh_huffman_encode_after_encode.restype = C.c_int
     H.ieh_write_header.argtypes = [vp, C.c_size_t, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, C.c_int, C.c_int]
     H.ieh_write_header.restype = C.c_int64
@@ -352,6 +354,16 @@ class Codec:
         nb = np.zeros(k, dtype=np.int64)
         self._host_chk(H.ieh_huffman_encode_device_batch(self.h, _ptr(data), in_pitch, n.ctypes.data, k, _ptr(out),
                                                          out_pitch, nb.ctypes.data))
+        return [int(v) for v in nb]
+
+    def huffman_encode_after_encode(self, out, out_pitch: int, count: int, hout, hpitch: int) -> list[int]:
+        """The batched Huffman pass over the ``count`` images the last :meth:`encode_images` call
+        wrote to device ``out`` (lengths from the encoder's end bits, on the device: no size
+        read-back).  Returns the Huffman output bytes per image."""
+        H = load_host_library()
+        nb = np.zeros(count, dtype=np.int64)
+        self._host_chk(H.ieh_huffman_encode_after_encode(self.h, _ptr(out), out_pitch, count, _ptr(hout), hpitch,
+                                                         nb.ctypes.data))
         return [int(v) for v in nb]
 
     def huffman_decode(self, data: bytes):

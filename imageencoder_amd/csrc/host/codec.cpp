@@ -406,6 +406,17 @@ int ieh_huffman_encode_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pit
     return algo::huffman_device_batch(c, din, in_pitch, n, count, dout, out_pitch, bytes, err);
 }
 
+// The batched Huffman pass straight after ie_encode_images on the same context: the string
+// lengths come from the encoder's end bits on the device (no size read-back in between).
+int ieh_huffman_encode_after_encode(ie_ctx* c, const uint8_t* din, size_t in_pitch, int count, uint8_t* dout,
+                                    size_t out_pitch, int64_t* bytes) {
+    if (!c || !din || count <= 0 || !dout || !bytes) return IE_EINVAL;
+    if (!dc::is_device(c, din) || !dc::is_device(c, dout)) return IE_EINVAL;
+    std::string err;
+    return algo::huffman_device_batch(c, din, in_pitch, nullptr, count, dout, out_pitch, bytes, err,
+                                      ie_last_end_bits(c));
+}
+
 void ieh_release(ie_ctx* c) {
     std::lock_guard<std::mutex> lk(dc::g_mu);
     dc::g_scratch.erase(c);

@@ -50,7 +50,7 @@ bool build_code(const uint32_t* hist, const uint64_t* first, util::BitStreamWrit
                 uint8_t* len, uint64_t& data_bits, std::string& err);
 int64_t huffman_device(ie_ctx* c, const uint8_t* din, size_t n, dc::DeviceBuffer& out, std::string& err);
 int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count, uint8_t* dout,
-                         size_t out_pitch, int64_t* bytes, std::string& err);
+                         size_t out_pitch, int64_t* bytes, std::string& err, const uint64_t* d_end_bits = nullptr);
 }  // namespace algo
 
 namespace dc {

@@ -169,8 +169,10 @@ int64_t huffman_device(ie_ctx* c, const uint8_t* din, size_t n, dc::DeviceBuffer
 // A batch of device-resident strings (string k: n[k] bytes at din + k*in_pitch) into
 // dout + k*out_pitch: one histogram launch, the tree builds on host threads, one pack launch.
 // bytes[k] = output length of string k.  Asynchronous after the histogram read-back.
-int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count, uint8_t* dout,
-                         size_t out_pitch, int64_t* bytes, std::string& err) {
+// d_end_bits (device, optional): the strings' end bits instead of host lengths n -- the encoder's
+// own output (ie_last_end_bits): the lengths are then recovered from the histograms.
+int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n_in, int count, uint8_t* dout,
+                         size_t out_pitch, int64_t* bytes, std::string& err, const uint64_t* d_end_bits) {
     const size_t K = size_t(count);
     // IE_HTIME=1: per-stage host timing to stderr (profiling aid)
     static const bool htime = getenv("IE_HTIME") != nullptr;
@@ -180,8 +182,18 @@ int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const u
     std::vector<uint64_t> first(256 * K), start(K);
     std::vector<uint8_t> len(256 * K);
     int r;
-    if ((r = ie_huffman_hist_batch(c, din, in_pitch, n, count, hist.data(), first.data())))
+    std::vector<uint64_t> nv;
+    const uint64_t* n = n_in;
+    if (d_end_bits) {
+        if ((r = ie_huffman_hist_batch_ends(c, din, in_pitch, d_end_bits, count, hist.data(), first.data())))
+            return (err = ie_last_error(c), r);
+        nv.assign(K, 0);
+        for (size_t k = 0; k < K; k++)
+            for (int b = 0; b < 256; b++) nv[k] += hist[256 * k + b];
+        n = nv.data();
+    } else if ((r = ie_huffman_hist_batch(c, din, in_pitch, n, count, hist.data(), first.data()))) {
         return (err = ie_last_error(c), r);
+    }
     const auto t1 = now();
     std::vector<std::vector<uint8_t>> dict(K);
     std::vector<std::string> errs(K);

@@ -891,6 +891,35 @@ int ie_huffman_hist_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
     return IE_OK;
 }
 
+const uint64_t* ie_last_end_bits(ie_ctx* c) { return c ? c->d_chain_end : nullptr; }
+
+int ie_huffman_hist_batch_ends(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* end_bits, int count,
+                               uint32_t* hist, uint64_t* first_pos) {
+    if (!c || !in || !end_bits || count <= 0 || !hist || !first_pos) return IE_EINVAL;
+    if (!is_device_ptr(in) || !is_device_ptr(end_bits))
+        return fail(c, IE_EINVAL, "batched Huffman input and end bits must be device memory");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t hb = size_t(count) * 256 * sizeof(uint32_t), fb = size_t(count) * 256 * sizeof(uint64_t);
+    const size_t nb = size_t(count) * sizeof(uint64_t), ub = size_t(count) * sizeof(unsigned);
+    int r;
+    if ((r = ensure(c, c->d_batch, c->cap_batch, hb + fb + nb + ub))) return r;
+    uint32_t* dh = reinterpret_cast<uint32_t*>(c->d_batch);
+    auto* df = reinterpret_cast<unsigned long long*>(c->d_batch + hb);
+    auto* dn = reinterpret_cast<uint64_t*>(c->d_batch + hb + fb);
+    auto* du = reinterpret_cast<unsigned*>(c->d_batch + hb + fb + nb);
+    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream);
+    HIPCHK(c, hipMemsetAsync(dh, 0, hb, c->stream));
+    HIPCHK(c, hipMemsetAsync(df, 0xFF, fb, c->stream));
+    ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream);
+    HIPCHK(c, hipGetLastError());
+    const hipMemcpyKind k1 = is_device_ptr(hist) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    const hipMemcpyKind k2 = is_device_ptr(first_pos) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    HIPCHK(c, hipMemcpyAsync(hist, dh, hb, k1, c->stream));
+    HIPCHK(c, hipMemcpyAsync(first_pos, df, fb, k2, c->stream));
+    if (k1 == hipMemcpyDeviceToHost || k2 == hipMemcpyDeviceToHost) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return IE_OK;
+}
+
 int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
                           const uint32_t* code, const uint8_t* len, const uint8_t* prefix, size_t prefix_pitch,
                           uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit) {

@@ -158,7 +158,7 @@ struct Probe {
 // First probe window: most tiles find an inclusive prefix among their nearest predecessors, and
 // every probed state is an uncached agent-scope load, so the first round reads only a few.
 #ifndef IE_PROBE0
-#define IE_PROBE0 8
+#define IE_PROBE0 16
 #endif
 constexpr int kProbe0 = IE_PROBE0;
 

@@ -107,6 +107,7 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
 // input bytes per pack tile for codes of at most maxlen bits (ie_huffman.hip)
 int pack_tile_bytes(int maxlen);
 void launch_pack(const PackArgs& a, hipStream_t s);
+void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s);
 // unresolved: device scratch, one word per string
 void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, unsigned* unresolved,
                  hipStream_t s);

@@ -131,6 +131,16 @@ __global__ __launch_bounds__(kTPB) void first_full_batch_kernel(const uint8_t* _
     first_full_body(in + uint64_t(k) * pitch, n[k], hist + 256 * k, first + 256 * k, unresolved + k);
 }
 
+// n[k] = the byte length of a stream ending at bit ends[k] (capped at cap): the batched Huffman
+// pass reads the encoder's own end bits, with no host round trip in between.
+__global__ void ends_to_bytes_kernel(const uint64_t* ends, uint64_t cap, int count, uint64_t* n) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < count) n[k] = min<uint64_t>((ends[k] + 7) / 8, cap);
+}
+void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s) {
+    hipLaunchKernelGGL(ends_to_bytes_kernel, dim3((count + kTPB - 1) / kTPB), dim3(kTPB), 0, s, ends, cap, count, n);
+}
+
 // unresolved: one word per string (device scratch)
 void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, unsigned* unresolved,
                  hipStream_t s) {

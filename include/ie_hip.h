@@ -130,6 +130,16 @@ int ie_huffman_pack(ie_ctx* ctx, const uint8_t* bytes, size_t n, const uint32_t*
 int ie_huffman_hist_batch(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
                           uint32_t* hist, uint64_t* first_pos);
 
+/* The device array of per-image end bits of the last ie_encode_images launch (valid until the
+ * next encode or Huffman call on the context; stream-ordered). */
+const uint64_t* ie_last_end_bits(ie_ctx* ctx);
+
+/* ie_huffman_hist_batch with the string lengths taken on the device from stream end bits
+ * (n[k] = ceil(end_bits[k] / 8), e.g. ie_last_end_bits): the encoder -> Huffman pipeline needs no
+ * host round trip for the sizes.  The host can recover n[k] as the sum of string k's histogram. */
+int ie_huffman_hist_batch_ends(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const uint64_t* end_bits,
+                               int count, uint32_t* hist, uint64_t* first_pos);
+
 /* Batched re-encode (Huffman.cpp:314-319 for every string of the batch in one launch): string k
  * with the code table code/len[256*k ...] into out + k*out_pitch from bit start_bit[k].  The
  * bits before start_bit[k] (the dictionary, Huffman.cpp:283-311, or the '0' bit of the "no gain"

@@ -250,6 +250,10 @@ int ieh_huffman_encode_device_batch(ie_ctx* ctx, const uint8_t* din, size_t in_p
 void ieh_release(ie_ctx* ctx);
 // Huffman post-pass of n bytes (host or device) into out (host).  Returns output bytes.
 int64_t ieh_huffman_encode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap);
+// Batched Huffman pass over the images of the last ie_encode_images launch on ctx (device output
+// at din + k*in_pitch), lengths from the encoder's end bits on the device; bytes[k] = output size.
+int ieh_huffman_encode_after_encode(ie_ctx* ctx, const uint8_t* din, size_t in_pitch, int count, uint8_t* dout,
+                                    size_t out_pitch, int64_t* bytes);
 // Huffman<uint8_t>::decode alone (Huffman.cpp:354-402; the bit walk on the device): decoded byte
 // count, or 0 with *passthrough = 1 when the stream has no dictionary.
 int64_t ieh_huffman_decode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap, int* passthrough);

@@ -308,3 +308,30 @@ def test_huffman_decode_rejects_invalid(codec):
     assert O.load().huffman_decode(crafted) is None
     with pytest.raises(IEError):
         codec.huffman_decode(crafted)
+
+
+def test_huffman_after_encode_pipeline(codec):
+    """encode_images -> Huffman pass with the lengths taken from the encoder's end bits on the
+    device (the C5 pipeline): every image's Huffman-coded file equals the reference's."""
+    import torch
+    from imageencoder_amd import stream_bound, write_header
+    n, q, w, h, f = 4, O.read_matrix("matrix.txt", 4), 320, 192, 5
+    codec.set_quant(q, n)
+    hdr, hb = write_header(n, q, True, w, h, huffman=True)
+    pitch = (stream_bound(w, h, n, 1, hb) + 255) // 256 * 256
+    y = synth.frames("M", w, h, f, seed=31)
+    out = torch.zeros(pitch * f, dtype=torch.uint8)
+    for k in range(f):  # each image's settings header, then the records from bit hb
+        out[k * pitch: k * pitch + len(hdr)] = torch.from_numpy(np.frombuffer(hdr, np.uint8).copy())
+    out = out.cuda()
+    hpitch = 2 * pitch
+    hout = torch.zeros(hpitch * f, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    codec.encode_images(torch.from_numpy(y).cuda(), w, h, out, out_pitch=pitch, nframes=f, start_bit=hb,
+                        want_sizes=False)
+    sizes = codec.huffman_encode_after_encode(out, pitch, f, hout, hpitch)
+    torch.cuda.synchronize()
+    host = hout.cpu().numpy()
+    for k in range(f):
+        want = O.load().encode_image(y[k], n, q, rle=True, huffman=True)
+        assert host[k * hpitch: k * hpitch + sizes[k]].tobytes() == want, k
