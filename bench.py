@@ -128,7 +128,9 @@ class Timer:
         wall = time.perf_counter() - t0
         if self.world > 1:
             dist.barrier()
-        t = torch.tensor([wall], dtype=torch.float64, device=self.dev)
+        # gloo (rehearsal backend) reduces host tensors; RCCL device tensors
+        t = torch.tensor([wall], dtype=torch.float64,
+                         device="cpu" if self.world > 1 and dist.get_backend() == "gloo" else self.dev)
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item()), ev0.elapsed_time(ev1) / 1e3
@@ -149,9 +151,17 @@ def main():
     from imageencoder_amd import dist as D
     from tests import oracle_lib as O
 
+    # IE_BENCH_BACKEND=gloo with ranks sharing the visible GPUs (local % device_count) rehearses the
+    # multi-rank control flow on a box with fewer GPUs than ranks; the real run is RCCL, one GPU each
+    backend = os.environ.get("IE_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
