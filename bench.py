@@ -110,10 +110,14 @@ class Timer:
     def __init__(self, torch, dist, dev, stream, world):
         self.torch, self.dist, self.dev, self.stream, self.world = torch, dist, dev, stream, world
 
-    def run(self, step, warmup, steps):
+    def run(self, step, warmup, steps, drain=None):
+        """drain (pipelined steps): completes the work the last step left in flight -- once after
+        the warmup (outside the timed region) and once after the K timed steps (inside it)."""
         torch, dist = self.torch, self.dist
         for i in range(warmup):
             step(i)
+        if drain:
+            drain()
         torch.cuda.synchronize(self.dev)
         if self.world > 1:
             dist.barrier()
@@ -123,6 +127,8 @@ class Timer:
         ev0.record(self.stream)
         for i in range(steps):
             step(warmup + i)
+        if drain:
+            drain()
         ev1.record(self.stream)
         torch.cuda.synchronize(self.dev)
         wall = time.perf_counter() - t0
@@ -187,7 +193,8 @@ def main():
     if args.workload in ("c2", "c3", "c5"):
         hdr_bits = write_header(n, q, True, w, h, huffman=cfg["huffman"])[1]
         pitch = (stream_bound(w, h, n, 1, hdr_bits) + 255) // 256 * 256
-        outs = [torch.zeros(pitch * B, dtype=torch.uint8, device=dev) for _ in range(min(nslots, 2))]
+        # two output buffers in turn (the pipelined Huffman step needs both; see step below)
+        outs = [torch.zeros(pitch * B, dtype=torch.uint8, device=dev) for _ in range(2)]
         # sizes for the algorithmic byte count (deterministic per frame)
         ends_per_slot = []
         for slot in range(nslots):
@@ -206,16 +213,27 @@ def main():
             hpitch = 2 * pitch  # >= 32-bit codes x payload bytes
             houts = torch.zeros(hpitch * B, dtype=torch.uint8, device=dev)
             hsizes = []
+            pending = []  # the batch whose trees + pack are still to do: (output buffer, slot)
+
+            def finish():
+                if pending:
+                    out, hslot = pending.pop()
+                    hsizes[:] = codec.huffman_finish_after_encode(out, pitch, B, hslot, houts, hpitch)
 
             def step(i):
+                # a batch's Huffman pass: one histogram launch (lengths from the encoder's end bits
+                # on the device), host tree builds, one pack launch.  Pipelined: batch i's encode
+                # and histogram are issued before batch i-1's trees, so the host builds those
+                # while the device encodes (two output buffers alternate, so batch i never
+                # overwrites the bytes batch i-1's pack still reads)
                 slot = i % nslots
                 out = outs[i % len(outs)]
                 codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, out, out_pitch=pitch,
                                     nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False)
-                # the batch's Huffman pass: one histogram launch (lengths from the encoder's end
-                # bits on the device), host tree builds, one pack launch
-                hsizes[:] = codec.huffman_encode_after_encode(out, pitch, B, houts, hpitch)
-        wall, gpu_s = timer.run(step, args.warmup, args.steps)
+                codec.huffman_begin_after_encode(out, pitch, B, i % 2)
+                finish()
+                pending.append((out, i % 2))
+        wall, gpu_s = timer.run(step, args.warmup, args.steps, drain=finish if cfg["huffman"] else None)
         px_total = world * args.steps * B * w * h
         in_bytes_per_launch = B * w * h
         # dominant kernel alone: the block encoder's launch time on its stream

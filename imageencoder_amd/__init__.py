@@ -112,6 +112,10 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
     H.ieh_huffman_decode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, ip]
     H.ieh_huffman_encode_after_encode.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, vp]
     H.ieh_huffman_encode_after_encode.restype = C.c_int
+    H.ieh_huffman_begin_after_encode.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_int]
+    H.ieh_huffman_begin_after_encode.restype = C.c_int
+    H.ieh_huffman_finish_after_encode.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_int, vp, C.c_size_t, vp]
+    H.ieh_huffman_finish_after_encode.restype = C.c_int
     H.ieh_write_header.argtypes = [vp, C.c_size_t, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, C.c_int, C.c_int]
     H.ieh_write_header.restype = C.c_int64
@@ -363,6 +367,23 @@ class Codec:
         H = load_host_library()
         nb = np.zeros(count, dtype=np.int64)
         self._host_chk(H.ieh_huffman_encode_after_encode(self.h, _ptr(out), out_pitch, count, _ptr(hout), hpitch,
+                                                         nb.ctypes.data))
+        return [int(v) for v in nb]
+
+    def huffman_begin_after_encode(self, out, out_pitch: int, count: int, slot: int) -> None:
+        """First half of :meth:`huffman_encode_after_encode` for pipelining batches: launches the
+        histogram of the last :meth:`encode_images` output and returns (read-back into ``slot``,
+        0 or 1).  Finish it with :meth:`huffman_finish_after_encode` on the same arguments after
+        issuing the next batch's encode and begin."""
+        H = load_host_library()
+        self._host_chk(H.ieh_huffman_begin_after_encode(self.h, _ptr(out), out_pitch, count, slot))
+
+    def huffman_finish_after_encode(self, out, out_pitch: int, count: int, slot: int, hout, hpitch: int) -> list[int]:
+        """Second half: trees for the batch begun in ``slot``, then the pack launch into ``hout``.
+        Returns the Huffman output bytes per image (``out`` must still hold that batch)."""
+        H = load_host_library()
+        nb = np.zeros(count, dtype=np.int64)
+        self._host_chk(H.ieh_huffman_finish_after_encode(self.h, _ptr(out), out_pitch, count, slot, _ptr(hout), hpitch,
                                                          nb.ctypes.data))
         return [int(v) for v in nb]
 

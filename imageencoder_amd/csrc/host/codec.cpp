@@ -417,6 +417,23 @@ int ieh_huffman_encode_after_encode(ie_ctx* c, const uint8_t* din, size_t in_pit
                                       ie_last_end_bits(c));
 }
 
+// Pipelined form: _begin launches the histogram of the images the last ie_encode_images call
+// wrote (read back into slot 0 or 1) and returns at once; _finish (same din / pitch / count / slot)
+// builds the trees and launches the pack.  Issue batch i+1's encode and _begin before batch i's
+// _finish and the host's tree builds overlap the device's encode.
+int ieh_huffman_begin_after_encode(ie_ctx* c, const uint8_t* din, size_t in_pitch, int count, int slot) {
+    if (!c || !din || count <= 0 || !dc::is_device(c, din)) return IE_EINVAL;
+    return ie_huffman_hist_batch_ends_async(c, din, in_pitch, ie_last_end_bits(c), count, slot);
+}
+
+int ieh_huffman_finish_after_encode(ie_ctx* c, const uint8_t* din, size_t in_pitch, int count, int slot, uint8_t* dout,
+                                    size_t out_pitch, int64_t* bytes) {
+    if (!c || !din || count <= 0 || !dout || !bytes) return IE_EINVAL;
+    if (!dc::is_device(c, din) || !dc::is_device(c, dout)) return IE_EINVAL;
+    std::string err;
+    return algo::huffman_device_batch_finish(c, din, in_pitch, count, slot, dout, out_pitch, bytes, err);
+}
+
 void ieh_release(ie_ctx* c) {
     std::lock_guard<std::mutex> lk(dc::g_mu);
     dc::g_scratch.erase(c);

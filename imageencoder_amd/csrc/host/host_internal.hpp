@@ -51,6 +51,8 @@ bool build_code(const uint32_t* hist, const uint64_t* first, util::BitStreamWrit
 int64_t huffman_device(ie_ctx* c, const uint8_t* din, size_t n, dc::DeviceBuffer& out, std::string& err);
 int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count, uint8_t* dout,
                          size_t out_pitch, int64_t* bytes, std::string& err, const uint64_t* d_end_bits = nullptr);
+int huffman_device_batch_finish(ie_ctx* c, const uint8_t* din, size_t in_pitch, int count, int slot, uint8_t* dout,
+                                size_t out_pitch, int64_t* bytes, std::string& err);
 }  // namespace algo
 
 namespace dc {

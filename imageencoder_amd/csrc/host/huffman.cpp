@@ -166,35 +166,15 @@ int64_t huffman_device(ie_ctx* c, const uint8_t* din, size_t n, dc::DeviceBuffer
     return int64_t(total);
 }
 
-// A batch of device-resident strings (string k: n[k] bytes at din + k*in_pitch) into
-// dout + k*out_pitch: one histogram launch, the tree builds on host threads, one pack launch.
-// bytes[k] = output length of string k.  Asynchronous after the histogram read-back.
-// d_end_bits (device, optional): the strings' end bits instead of host lengths n -- the encoder's
-// own output (ie_last_end_bits): the lengths are then recovered from the histograms.
-int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n_in, int count, uint8_t* dout,
-                         size_t out_pitch, int64_t* bytes, std::string& err, const uint64_t* d_end_bits) {
+// The host half of a batched pass, once the histograms are on the host: the tree builds on host
+// threads, then one pack launch (asynchronous).  n[k] = string k's length.
+static int trees_and_pack(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n, int count,
+                          const uint32_t* hist, const uint64_t* first, uint8_t* dout, size_t out_pitch, int64_t* bytes,
+                          std::string& err) {
     const size_t K = size_t(count);
-    // IE_HTIME=1: per-stage host timing to stderr (profiling aid)
-    static const bool htime = getenv("IE_HTIME") != nullptr;
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    const auto t0 = now();
-    std::vector<uint32_t> hist(256 * K), code(256 * K);
-    std::vector<uint64_t> first(256 * K), start(K);
+    std::vector<uint32_t> code(256 * K);
+    std::vector<uint64_t> start(K);
     std::vector<uint8_t> len(256 * K);
-    int r;
-    std::vector<uint64_t> nv;
-    const uint64_t* n = n_in;
-    if (d_end_bits) {
-        if ((r = ie_huffman_hist_batch_ends(c, din, in_pitch, d_end_bits, count, hist.data(), first.data())))
-            return (err = ie_last_error(c), r);
-        nv.assign(K, 0);
-        for (size_t k = 0; k < K; k++)
-            for (int b = 0; b < 256; b++) nv[k] += hist[256 * k + b];
-        n = nv.data();
-    } else if ((r = ie_huffman_hist_batch(c, din, in_pitch, n, count, hist.data(), first.data()))) {
-        return (err = ie_last_error(c), r);
-    }
-    const auto t1 = now();
     std::vector<std::vector<uint8_t>> dict(K);
     std::vector<std::string> errs(K);
     std::vector<char> ok(K, 1);
@@ -234,23 +214,69 @@ int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const u
     const int T = int(std::min<size_t>(K, size_t(std::max(1, std::min(16, omp_get_max_threads())))));
 #pragma omp parallel for schedule(dynamic, 1) num_threads(T) if (T > 1)
     for (int k = 0; k < int(K); k++) build(size_t(k));
-    const auto t2 = now();
     for (size_t k = 0; k < K; k++)
         if (!ok[k]) return (err = errs[k], IE_EINVAL);
     size_t pp = 4;
     for (const auto& d : dict) pp = std::max(pp, d.size());
     std::vector<uint8_t> prefix(pp * K, 0);
     for (size_t k = 0; k < K; k++) std::memcpy(&prefix[pp * k], dict[k].data(), dict[k].size());
+    int r;
     if ((r = ie_huffman_pack_batch(c, din, in_pitch, n, count, code.data(), len.data(), prefix.data(), pp, dout,
                                    out_pitch, start.data(), nullptr)))
         return (err = ie_last_error(c), r);
-    if (htime) {
-        const auto t3 = now();
-        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-        fprintf(stderr, "[htime] hist+readback %.1f us, trees %.1f us, pack submit %.1f us\n", us(t0, t1), us(t1, t2),
-                us(t2, t3));
-    }
     return IE_OK;
+}
+
+// A batch of device-resident strings (string k: n[k] bytes at din + k*in_pitch) into
+// dout + k*out_pitch: one histogram launch, the tree builds on host threads, one pack launch.
+// bytes[k] = output length of string k.  Asynchronous after the histogram read-back.
+// d_end_bits (device, optional): the strings' end bits instead of host lengths n -- the encoder's
+// own output (ie_last_end_bits): the lengths are then recovered from the histograms.
+int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const uint64_t* n_in, int count, uint8_t* dout,
+                         size_t out_pitch, int64_t* bytes, std::string& err, const uint64_t* d_end_bits) {
+    const size_t K = size_t(count);
+    // IE_HTIME=1: per-stage host timing to stderr (profiling aid)
+    static const bool htime = getenv("IE_HTIME") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = now();
+    std::vector<uint32_t> hist(256 * K);
+    std::vector<uint64_t> first(256 * K);
+    int r;
+    std::vector<uint64_t> nv;
+    const uint64_t* n = n_in;
+    if (d_end_bits) {
+        if ((r = ie_huffman_hist_batch_ends(c, din, in_pitch, d_end_bits, count, hist.data(), first.data())))
+            return (err = ie_last_error(c), r);
+        nv.assign(K, 0);
+        for (size_t k = 0; k < K; k++)
+            for (int b = 0; b < 256; b++) nv[k] += hist[256 * k + b];
+        n = nv.data();
+    } else if ((r = ie_huffman_hist_batch(c, din, in_pitch, n, count, hist.data(), first.data()))) {
+        return (err = ie_last_error(c), r);
+    }
+    const auto t1 = now();
+    r = trees_and_pack(c, din, in_pitch, n, count, hist.data(), first.data(), dout, out_pitch, bytes, err);
+    if (htime) {
+        const auto t2 = now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[htime] hist+readback %.1f us, trees + pack submit %.1f us\n", us(t0, t1), us(t1, t2));
+    }
+    return r;
+}
+
+// Pipelined form of huffman_device_batch(d_end_bits): the second half, after
+// ie_huffman_hist_batch_ends_async(slot) -- waits for that slot's histograms, then trees + pack.
+int huffman_device_batch_finish(ie_ctx* c, const uint8_t* din, size_t in_pitch, int count, int slot, uint8_t* dout,
+                                size_t out_pitch, int64_t* bytes, std::string& err) {
+    const size_t K = size_t(count);
+    std::vector<uint32_t> hist(256 * K);
+    std::vector<uint64_t> first(256 * K);
+    int r;
+    if ((r = ie_huffman_hist_batch_wait(c, slot, hist.data(), first.data()))) return (err = ie_last_error(c), r);
+    std::vector<uint64_t> n(K, 0);
+    for (size_t k = 0; k < K; k++)
+        for (int b = 0; b < 256; b++) n[k] += hist[256 * k + b];
+    return trees_and_pack(c, din, in_pitch, n.data(), count, hist.data(), first.data(), dout, out_pitch, bytes, err);
 }
 
 int Huffman::encode(ie_ctx* c, const uint8_t* in, size_t n, std::vector<uint8_t>& out) {

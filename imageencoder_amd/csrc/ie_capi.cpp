@@ -62,6 +62,17 @@ struct ie_ctx {
     size_t cap_batch = 0;
     uint8_t* h_batch = nullptr;
     size_t cap_hbatch = 0;
+    // pipelined batches: two pinned slots for the histogram read-back and two for the pack tables,
+    // each guarded by an event (no stream-wide synchronisation between batches)
+    uint8_t* h_hist[2] = {};
+    size_t cap_hhist[2] = {};
+    hipEvent_t ev_hist[2] = {};
+    int hist_count[2] = {};
+    uint8_t* h_pack[2] = {};
+    size_t cap_hpack[2] = {};
+    hipEvent_t ev_pack[2] = {};
+    bool pack_recorded[2] = {};
+    int pack_slot = 0;
     // decoder scratch
     uint8_t* d_dec = nullptr;          // staged stream + padding
     size_t cap_dec = 0;
@@ -675,6 +686,12 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_hist);
     (void)hipFree(c->d_batch);
     (void)hipHostFree(c->h_batch);
+    for (int i = 0; i < 2; i++) {
+        if (c->h_hist[i]) (void)hipHostFree(c->h_hist[i]);
+        if (c->h_pack[i]) (void)hipHostFree(c->h_pack[i]);
+        if (c->ev_hist[i]) (void)hipEventDestroy(c->ev_hist[i]);
+        if (c->ev_pack[i]) (void)hipEventDestroy(c->ev_pack[i]);
+    }
     (void)hipFree(c->d_first);
     (void)hipFree(c->d_dec);
     (void)hipFree(c->d_walk);
@@ -920,6 +937,45 @@ int ie_huffman_hist_batch_ends(ie_ctx* c, const uint8_t* in, size_t in_pitch, co
     return IE_OK;
 }
 
+int ie_huffman_hist_batch_ends_async(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* end_bits,
+                                     int count, int slot) {
+    if (!c || !in || !end_bits || count <= 0 || slot < 0 || slot > 1) return IE_EINVAL;
+    if (!is_device_ptr(in) || !is_device_ptr(end_bits))
+        return fail(c, IE_EINVAL, "batched Huffman input and end bits must be device memory");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t hb = size_t(count) * 256 * sizeof(uint32_t), fb = size_t(count) * 256 * sizeof(uint64_t);
+    const size_t nb = size_t(count) * sizeof(uint64_t), ub = size_t(count) * sizeof(unsigned);
+    int r;
+    if ((r = ensure(c, c->d_batch, c->cap_batch, hb + fb + nb + ub))) return r;
+    if ((r = ensure_pinned(c, c->h_hist[slot], c->cap_hhist[slot], hb + fb))) return r;
+    if (!c->ev_hist[slot]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_hist[slot], hipEventDisableTiming));
+    uint32_t* dh = reinterpret_cast<uint32_t*>(c->d_batch);
+    auto* df = reinterpret_cast<unsigned long long*>(c->d_batch + hb);
+    auto* dn = reinterpret_cast<uint64_t*>(c->d_batch + hb + fb);
+    auto* du = reinterpret_cast<unsigned*>(c->d_batch + hb + fb + nb);
+    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream);
+    HIPCHK(c, hipMemsetAsync(dh, 0, hb, c->stream));
+    HIPCHK(c, hipMemsetAsync(df, 0xFF, fb, c->stream));
+    ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream);
+    HIPCHK(c, hipGetLastError());
+    // histograms and first positions are contiguous on the device: one read-back
+    HIPCHK(c, hipMemcpyAsync(c->h_hist[slot], c->d_batch, hb + fb, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_hist[slot], c->stream));
+    c->hist_count[slot] = count;
+    return IE_OK;
+}
+
+int ie_huffman_hist_batch_wait(ie_ctx* c, int slot, uint32_t* hist, uint64_t* first_pos) {
+    if (!c || slot < 0 || slot > 1 || !hist || !first_pos) return IE_EINVAL;
+    if (!c->ev_hist[slot] || !c->hist_count[slot]) return fail(c, IE_EINVAL, "no histogram pending in this slot");
+    HIPCHK(c, hipEventSynchronize(c->ev_hist[slot]));
+    const size_t hb = size_t(c->hist_count[slot]) * 256 * sizeof(uint32_t);
+    std::memcpy(hist, c->h_hist[slot], hb);
+    std::memcpy(first_pos, c->h_hist[slot] + hb, size_t(c->hist_count[slot]) * 256 * sizeof(uint64_t));
+    c->hist_count[slot] = 0;
+    return IE_OK;
+}
+
 int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
                           const uint32_t* code, const uint8_t* len, const uint8_t* prefix, size_t prefix_pitch,
                           uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit) {
@@ -961,9 +1017,13 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
     const size_t o_pre = o_code + 4 * 256 * K, o_len = o_pre + 4 * size_t(pw) * K, total = o_len + 256 * K;
     int r;
     if ((r = ensure(c, c->d_batch, c->cap_batch, total))) return r;
-    if ((r = ensure_pinned(c, c->h_batch, c->cap_hbatch, total))) return r;
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // the pinned staging may still feed a copy
-    uint8_t* h = c->h_batch;
+    // two pinned staging slots in turn: wait only for this slot's previous copy, not the stream
+    const int ps = c->pack_slot;
+    c->pack_slot ^= 1;
+    if (c->pack_recorded[ps]) HIPCHK(c, hipEventSynchronize(c->ev_pack[ps]));
+    if ((r = ensure_pinned(c, c->h_pack[ps], c->cap_hpack[ps], total))) return r;
+    if (!c->ev_pack[ps]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_pack[ps], hipEventDisableTiming));
+    uint8_t* h = c->h_pack[ps];
     std::memcpy(h + o_ts, ts.data(), 8 * (K + 1));
     std::memcpy(h + o_n, n, 8 * K);
     std::memcpy(h + o_st, start_bit, 8 * K);
@@ -979,6 +1039,8 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         if (sb % 8) d[nbytes - 1] &= uint8_t(0xFF00u >> (sb % 8));  // bits from start_bit on are the packer's
     }
     HIPCHK(c, hipMemcpyAsync(c->d_batch, h, total, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_pack[ps], c->stream));
+    c->pack_recorded[ps] = true;
     const uint8_t* d = c->d_batch;
     // strings without bytes: the prefix alone
     for (size_t k = 0; k < K; k++)

@@ -140,6 +140,15 @@ const uint64_t* ie_last_end_bits(ie_ctx* ctx);
 int ie_huffman_hist_batch_ends(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const uint64_t* end_bits,
                                int count, uint32_t* hist, uint64_t* first_pos);
 
+/* The same, split for pipelining batches: _async launches the histogram and its read-back into
+ * pinned slot `slot` (0 or 1) and returns at once; _wait blocks until that slot's read-back is
+ * complete and copies out count*256 counts and first positions.  While the host builds the trees
+ * of batch i (between _wait and ie_huffman_pack_batch), the device runs batch i+1's encode and
+ * histogram.  Same reference interface as ie_huffman_hist_batch (Huffman.cpp:237-243). */
+int ie_huffman_hist_batch_ends_async(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const uint64_t* end_bits,
+                                     int count, int slot);
+int ie_huffman_hist_batch_wait(ie_ctx* ctx, int slot, uint32_t* hist, uint64_t* first_pos);
+
 /* Batched re-encode (Huffman.cpp:314-319 for every string of the batch in one launch): string k
  * with the code table code/len[256*k ...] into out + k*out_pitch from bit start_bit[k].  The
  * bits before start_bit[k] (the dictionary, Huffman.cpp:283-311, or the '0' bit of the "no gain"

@@ -254,6 +254,11 @@ int64_t ieh_huffman_encode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* ou
 // at din + k*in_pitch), lengths from the encoder's end bits on the device; bytes[k] = output size.
 int ieh_huffman_encode_after_encode(ie_ctx* ctx, const uint8_t* din, size_t in_pitch, int count, uint8_t* dout,
                                     size_t out_pitch, int64_t* bytes);
+// The same in two halves for pipelining batches (slot 0 / 1 alternating): _begin launches the
+// histogram and returns; _finish waits for it, builds the trees and launches the pack.
+int ieh_huffman_begin_after_encode(ie_ctx* ctx, const uint8_t* din, size_t in_pitch, int count, int slot);
+int ieh_huffman_finish_after_encode(ie_ctx* ctx, const uint8_t* din, size_t in_pitch, int count, int slot,
+                                    uint8_t* dout, size_t out_pitch, int64_t* bytes);
 // Huffman<uint8_t>::decode alone (Huffman.cpp:354-402; the bit walk on the device): decoded byte
 // count, or 0 with *passthrough = 1 when the stream has no dictionary.
 int64_t ieh_huffman_decode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap, int* passthrough);

@@ -335,3 +335,44 @@ def test_huffman_after_encode_pipeline(codec):
     for k in range(f):
         want = O.load().encode_image(y[k], n, q, rle=True, huffman=True)
         assert host[k * hpitch: k * hpitch + sizes[k]].tobytes() == want, k
+
+
+@pytest.mark.gpu
+def test_huffman_after_encode_pipelined(codec):
+    """Batches pipelined as in bench.py's C5 step: batch i+1's encode and histogram are issued
+    before batch i's trees + pack (two output buffers, histogram slots alternating); every
+    image's Huffman-coded file still equals the reference's."""
+    import torch
+    from imageencoder_amd import stream_bound, write_header
+    n, q, w, h, f, nb = 4, O.read_matrix("matrix.txt", 4), 256, 128, 3, 4
+    codec.set_quant(q, n)
+    hdr, hb = write_header(n, q, True, w, h, huffman=True)
+    pitch = (stream_bound(w, h, n, 1, hb) + 255) // 256 * 256
+    ys = [synth.frames("M" if b % 2 else "U", w, h, f, seed=50 + b) for b in range(nb)]
+    outs = []
+    for _ in range(2):
+        o = torch.zeros(pitch * f, dtype=torch.uint8)
+        for k in range(f):
+            o[k * pitch: k * pitch + len(hdr)] = torch.from_numpy(np.frombuffer(hdr, np.uint8).copy())
+        outs.append(o.cuda())
+    hpitch = 2 * pitch
+    houts = [torch.zeros(hpitch * f, dtype=torch.uint8, device="cuda") for _ in range(nb)]
+    sizes = [None] * nb
+    torch.cuda.synchronize()
+    pending = None
+    for b in range(nb):
+        codec.encode_images(torch.from_numpy(ys[b]).cuda(), w, h, outs[b % 2], out_pitch=pitch, nframes=f,
+                            start_bit=hb, want_sizes=False)
+        codec.huffman_begin_after_encode(outs[b % 2], pitch, f, b % 2)
+        if pending is not None:
+            p = pending
+            sizes[p] = codec.huffman_finish_after_encode(outs[p % 2], pitch, f, p % 2, houts[p], hpitch)
+        pending = b
+    sizes[pending] = codec.huffman_finish_after_encode(outs[pending % 2], pitch, f, pending % 2, houts[pending],
+                                                       hpitch)
+    torch.cuda.synchronize()
+    for b in range(nb):
+        host = houts[b].cpu().numpy()
+        for k in range(f):
+            want = O.load().encode_image(ys[b][k], n, q, rle=True, huffman=True)
+            assert host[k * hpitch: k * hpitch + sizes[b][k]].tobytes() == want, (b, k)
