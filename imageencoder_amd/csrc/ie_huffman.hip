@@ -204,8 +204,12 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
         if (chain_pos == 0)  // the prefix words (the chain's bits before `start` live in hdr)
             for (uint32_t w = tid; w < uint32_t(start >> 5); w += kTPB) out[w] = hdr[w];
     }
-    s_code[tid] = a.code[256 * k + tid];
-    s_len[tid] = a.len[256 * k + tid];
+    if constexpr (MAXLEN <= 16) {  // {code, len << 16}
+        s_code[tid] = (a.code[256 * k + tid] & 0xFFFFu) | (uint32_t(a.len[256 * k + tid]) << 16);
+    } else {
+        s_code[tid] = a.code[256 * k + tid];
+        s_len[tid] = a.len[256 * k + tid];
+    }
     __syncthreads();
 
     const uint64_t p = uint64_t(chain_pos) * (kTPB * BPT) + uint64_t(tid) * BPT;
@@ -229,8 +233,25 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     }
     auto byte = [&](int e) -> uint32_t { return (w[e >> 2] >> (8 * (e & 3))) & 0xFFu; };
     uint32_t mybits = 0;
+    // codes of <= 16 bits: one LDS read per byte ({code, len << 16}); the emission's units, pairs
+    // of codes (<= 32 bits), stay in registers: cp[i] the pair's bits, lp the lengths, 4 per word
+    constexpr int NPAIR = MAXLEN <= 16 ? BPT / 2 : 1;
+    uint32_t cp[NPAIR], lp[(NPAIR + 3) / 4];
+    if constexpr (MAXLEN <= 16) {
 #pragma unroll
-    for (int e = 0; e < BPT; e++) mybits += (e < nb) ? s_len[byte(e)] : 0u;
+        for (int i = 0; i < NPAIR; i++) {
+            const uint32_t e1 = (2 * i < nb) ? s_code[byte(2 * i)] : 0u;
+            const uint32_t e2 = (2 * i + 1 < nb) ? s_code[byte(2 * i + 1)] : 0u;
+            const uint32_t l2 = e2 >> 16, l = (e1 >> 16) + l2;
+            cp[i] = ((e1 & 0xFFFFu) << l2) | (e2 & 0xFFFFu);
+            if (i % 4 == 0) lp[i / 4] = l;
+            else lp[i / 4] |= l << (8 * (i % 4));
+            mybits += l;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < BPT; e++) mybits += (e < nb) ? s_len[byte(e)] : 0u;
+    }
 
     uint32_t A;
     const uint32_t off = block_excl_scan(mybits, misc, &A);
@@ -241,11 +262,30 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
     __syncthreads();
     if (mybits) {
-        BitSink sink(img, off);
+        if constexpr (MAXLEN <= 16) {
+            // two codes at a time (<= 32 bits), so at most one completed word per step; bits of
+            // acc above the pending ones are stale and never reach a word (32-bit truncation)
+            uint64_t acc = 0;
+            uint32_t n = off & 31u, wi = off >> 5;
 #pragma unroll
-        for (int e = 0; e < BPT; e++)
-            if (e < nb) sink.put(s_len[byte(e)], s_code[byte(e)]);
-        sink.finish();
+            for (int i = 0; i < NPAIR; i++) {
+                const uint32_t l = (lp[i / 4] >> (8 * (i % 4))) & 0xFFu;
+                acc = (acc << l) | cp[i];
+                n += l;
+                if (n >= 32u) {
+                    n -= 32u;
+                    atomicOr(&img[wi], uint32_t(acc >> n));
+                    wi++;
+                }
+            }
+            if (n) atomicOr(&img[wi], uint32_t(acc << (32u - n)));
+        } else {
+            BitSink sink(img, off);
+#pragma unroll
+            for (int e = 0; e < BPT; e++)
+                if (e < nb) sink.put(s_len[byte(e)], s_code[byte(e)]);
+            sink.finish();
+        }
     }
     __syncthreads();
 
