@@ -924,9 +924,7 @@ int ie_huffman_hist_batch_ends(ie_ctx* c, const uint8_t* in, size_t in_pitch, co
     auto* df = reinterpret_cast<unsigned long long*>(c->d_batch + hb);
     auto* dn = reinterpret_cast<uint64_t*>(c->d_batch + hb + fb);
     auto* du = reinterpret_cast<unsigned*>(c->d_batch + hb + fb + nb);
-    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream);
-    HIPCHK(c, hipMemsetAsync(dh, 0, hb, c->stream));
-    HIPCHK(c, hipMemsetAsync(df, 0xFF, fb, c->stream));
+    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream, dh, df);
     ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream);
     HIPCHK(c, hipGetLastError());
     const hipMemcpyKind k1 = is_device_ptr(hist) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -953,9 +951,7 @@ int ie_huffman_hist_batch_ends_async(ie_ctx* c, const uint8_t* in, size_t in_pit
     auto* df = reinterpret_cast<unsigned long long*>(c->d_batch + hb);
     auto* dn = reinterpret_cast<uint64_t*>(c->d_batch + hb + fb);
     auto* du = reinterpret_cast<unsigned*>(c->d_batch + hb + fb + nb);
-    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream);
-    HIPCHK(c, hipMemsetAsync(dh, 0, hb, c->stream));
-    HIPCHK(c, hipMemsetAsync(df, 0xFF, fb, c->stream));
+    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream, dh, df);
     ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream);
     HIPCHK(c, hipGetLastError());
     // histograms and first positions are contiguous on the device: one read-back

@@ -107,7 +107,9 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
 // input bytes per pack tile for codes of at most maxlen bits (ie_huffman.hip)
 int pack_tile_bytes(int maxlen);
 void launch_pack(const PackArgs& a, hipStream_t s);
-void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s);
+// hist / first (optional, count*256 each): cleared to 0 / ~0 by the same launch
+void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s,
+                          uint32_t* hist = nullptr, unsigned long long* first = nullptr);
 // unresolved: device scratch, one word per string
 void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long long* first, unsigned* unresolved,
                  hipStream_t s);

@@ -18,6 +18,7 @@
 namespace ie {
 
 constexpr int kHistTile = kTPB * 16;  // bytes per workgroup pass
+constexpr int kHistLoads = 4;          // hist_body: 16-byte loads per thread in flight
 
 // Byte histogram of [0, n) of `in`, grid-strided over workgroups blockIdx.x of gridDim.x: one
 // non-returning LDS add per byte into the wave's own sub-histogram, merged with global atomics.
@@ -30,16 +31,35 @@ __device__ __forceinline__ void hist_body(const uint8_t* __restrict__ in, uint64
     for (int q = 0; q < 4; q++) h[q][tid] = 0;
     __syncthreads();
     const bool al = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
-    for (uint64_t base = uint64_t(blockIdx.x) * kHistTile; base < n; base += uint64_t(gridDim.x) * kHistTile) {
-        const uint64_t p = base + uint64_t(tid) * 16;
-        if (p + 16 <= n && al) {
-            const uint4 v = *reinterpret_cast<const uint4*>(in + p);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    // kHistLoads 16-byte loads per thread in flight per step (a workgroup step covers
+    // kHistLoads * kHistTile bytes; load q of thread tid at q * kHistTile + 16 * tid: coalesced)
+    constexpr uint64_t kStep = uint64_t(kHistLoads) * kHistTile;
+    for (uint64_t base = uint64_t(blockIdx.x) * kStep; base < n; base += uint64_t(gridDim.x) * kStep) {
+        if (base + kStep <= n && al) {
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            v4u v[kHistLoads];
 #pragma unroll
-            for (int e = 0; e < 16; e++) atomicAdd(&h[wv][(w[e >> 2] >> (8 * (e & 3))) & 0xFFu], 1u);
+            for (int q = 0; q < kHistLoads; q++)
+                v[q] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + base + q * kHistTile) + tid);
+#pragma unroll
+            for (int q = 0; q < kHistLoads; q++) {
+                const uint32_t w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                for (int e = 0; e < 16; e++) atomicAdd(&h[wv][(w[e >> 2] >> (8 * (e & 3))) & 0xFFu], 1u);
+            }
         } else {
-            for (int e = 0; e < 16; e++)
-                if (p + e < n) atomicAdd(&h[wv][in[p + e]], 1u);
+            for (int q = 0; q < kHistLoads; q++) {
+                const uint64_t p = base + uint64_t(q) * kHistTile + uint64_t(tid) * 16;
+                if (p + 16 <= n && al) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(in + p);
+                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int e = 0; e < 16; e++) atomicAdd(&h[wv][(w[e >> 2] >> (8 * (e & 3))) & 0xFFu], 1u);
+                } else {
+                    for (int e = 0; e < 16; e++)
+                        if (p + e < n) atomicAdd(&h[wv][in[p + e]], 1u);
+                }
+            }
         }
     }
     __syncthreads();
@@ -133,12 +153,22 @@ __global__ __launch_bounds__(kTPB) void first_full_batch_kernel(const uint8_t* _
 
 // n[k] = the byte length of a stream ending at bit ends[k] (capped at cap): the batched Huffman
 // pass reads the encoder's own end bits, with no host round trip in between.
-__global__ void ends_to_bytes_kernel(const uint64_t* ends, uint64_t cap, int count, uint64_t* n) {
+// Also clears the histograms (hist = 0) and first positions (~0) of the count strings when given:
+// no separate memset launches in the pipeline.
+__global__ void ends_to_bytes_kernel(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, uint32_t* hist,
+                                     unsigned long long* first) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < count) n[k] = min<uint64_t>((ends[k] + 7) / 8, cap);
+    if (hist && k < 256 * count) {
+        hist[k] = 0u;
+        first[k] = ~0ull;
+    }
 }
-void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s) {
-    hipLaunchKernelGGL(ends_to_bytes_kernel, dim3((count + kTPB - 1) / kTPB), dim3(kTPB), 0, s, ends, cap, count, n);
+void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s, uint32_t* hist,
+                          unsigned long long* first) {
+    const int threads = hist ? 256 * count : count;
+    hipLaunchKernelGGL(ends_to_bytes_kernel, dim3((threads + kTPB - 1) / kTPB), dim3(kTPB), 0, s, ends, cap, count, n,
+                       hist, first);
 }
 
 // unresolved: one word per string (device scratch)
