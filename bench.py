@@ -221,15 +221,17 @@ def main():
                     hsizes[:] = codec.huffman_finish_after_encode(out, pitch, B, hslot, houts, hpitch)
 
             def step(i):
-                # a batch's Huffman pass: one histogram launch (lengths from the encoder's end bits
-                # on the device), host tree builds, one pack launch.  Pipelined: batch i's encode
+                # a batch's Huffman pass: the byte counts (from the encoder), the first positions
+                # (lengths from the encoder's end bits on the device), host tree builds, one pack
+                # launch.  Pipelined: batch i's encode
                 # and histogram are issued before batch i-1's trees, so the host builds those
                 # while the device encodes (two output buffers alternate, so batch i never
                 # overwrites the bytes batch i-1's pack still reads)
                 slot = i % nslots
                 out = outs[i % len(outs)]
+                # the encoder also counts the bytes it stores (the histogram of the Huffman pass)
                 codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, out, out_pitch=pitch,
-                                    nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False)
+                                    nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False, count_bytes=True)
                 codec.huffman_begin_after_encode(out, pitch, B, i % 2)
                 finish()
                 pending.append((out, i % 2))

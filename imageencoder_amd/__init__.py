@@ -65,6 +65,12 @@ def load_library(path: str | None = None) -> C.CDLL:
                                    u8p, C.c_size_t, C.c_uint64, u64p, u64p]
     L.ie_encode_images.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                    u8p, C.c_size_t, C.c_uint64, u64p]
+    L.ie_encode_images_counted.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
+                                           C.c_int, u8p, C.c_size_t, C.c_uint64]
+    L.ie_huffman_hist_batch_ends_async.argtypes = [vp, u8p, C.c_size_t, u64p, C.c_int, C.c_int]
+    L.ie_huffman_hist_batch_wait.argtypes = [vp, C.c_int, vp, vp]
+    L.ie_last_end_bits.argtypes = [vp]
+    L.ie_last_end_bits.restype = C.c_void_p
     L.ie_last_fallbacks.argtypes = [vp, u64p]
     L.ie_quantize_frames.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, vp]
     for name in ("ie_huffman_hist", "ie_huffman_pack", "ie_bitcopy", "ie_decode_frames"):
@@ -229,9 +235,16 @@ class Codec:
 
     def encode_images(self, y, w: int, h: int, out, out_pitch: int, nframes: int, start_bit: int = 0,
                       stride: int | None = None, frame_pitch: int | None = None, rle: bool = True,
-                      mode: int = MODE_FAST, want_sizes: bool = True):
+                      mode: int = MODE_FAST, want_sizes: bool = True, count_bytes: bool = False):
+        """count_bytes (device ``out``): also count every image's stream bytes for the following
+        Huffman pass (:meth:`huffman_begin_after_encode` then skips its histogram kernel);
+        implies want_sizes=False."""
         stride = w if stride is None else stride
         frame_pitch = stride * h if frame_pitch is None else frame_pitch
+        if count_bytes:
+            self._chk(self.L.ie_encode_images_counted(self.h, _ptr(y), w, h, stride, frame_pitch, nframes, int(rle),
+                                                      mode, _ptr(out), out_pitch, start_bit))
+            return None
         eb = np.zeros(nframes, dtype=np.uint64)
         ebp = eb.ctypes.data_as(C.POINTER(C.c_uint64)) if want_sizes else None
         self._chk(self.L.ie_encode_images(self.h, _ptr(y), w, h, stride, frame_pitch, nframes, int(rle), mode,
@@ -386,6 +399,17 @@ class Codec:
         self._host_chk(H.ieh_huffman_finish_after_encode(self.h, _ptr(out), out_pitch, count, slot, _ptr(hout), hpitch,
                                                          nb.ctypes.data))
         return [int(v) for v in nb]
+
+    def huffman_hist_after_encode(self, out, out_pitch: int, count: int):
+        """(hist [count, 256] uint32, first [count, 256] uint64) of the images the last encode
+        wrote (counts fused into the encoder when it ran with count_bytes=True)."""
+        u64p = C.POINTER(C.c_uint64)
+        ends = C.cast(C.c_void_p(self.L.ie_last_end_bits(self.h)), u64p)
+        self._chk(self.L.ie_huffman_hist_batch_ends_async(self.h, _ptr(out), out_pitch, ends, count, 0))
+        hist = np.zeros((count, 256), dtype=np.uint32)
+        first = np.zeros((count, 256), dtype=np.uint64)
+        self._chk(self.L.ie_huffman_hist_batch_wait(self.h, 0, hist.ctypes.data, first.ctypes.data))
+        return hist, first
 
     def huffman_decode(self, data: bytes):
         """The Huffman decode alone (device bit walk): (decoded bytes, passthrough)."""

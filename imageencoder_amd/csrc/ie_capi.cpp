@@ -73,6 +73,7 @@ struct ie_ctx {
     hipEvent_t ev_pack[2] = {};
     bool pack_recorded[2] = {};
     int pack_slot = 0;
+    int fused_count = 0;  // > 0: the last encode (ie_encode_images_counted) left this many histograms in d_batch
     // decoder scratch
     uint8_t* d_dec = nullptr;          // staged stream + padding
     size_t cap_dec = 0;
@@ -406,7 +407,9 @@ size_t bound_bits_per_block(int n) { return 4 + 16 * size_t(n * n + 1); }
 // Common driver of ie_encode_frames (segmented = 0) and ie_encode_images (segmented = 1).
 int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
            int use_rle, int mode, uint8_t* out, size_t out_cap, size_t out_pitch, uint64_t start_bit,
-           int segmented, uint64_t* frame_bits, uint64_t* end_bits, int16_t* coef = nullptr) {
+           int segmented, uint64_t* frame_bits, uint64_t* end_bits, int16_t* coef = nullptr,
+           uint32_t* hist = nullptr) {
+    c->fused_count = 0;  // any encode replaces the batch scratch's meaning
     int r = check_dims(c, w, h, nframes);
     if (r) return r;
     if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
@@ -490,6 +493,8 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.tab = c->d_tab;
     a.rec_bits = c->h_tab->rec_bits;
     a.coef = coef;
+    a.hist = hist;
+    if (hist) HIPCHK(c, hipMemsetAsync(hist, 0, size_t(nframes) * 256 * sizeof(uint32_t), c->stream));
     static const int ablate = getenv("IE_ABLATE") ? atoi(getenv("IE_ABLATE")) : 0;  // profiling only
 #ifndef IE_ABLATE_FORCE
 #define IE_ABLATE_FORCE 0
@@ -527,7 +532,7 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
         if (c->use_ticket) return fail(c, IE_EDEVICE, "tile look-back timed out");
         c->use_ticket = true;  // dispatch order did not hold: order the tiles explicitly and redo
         return encode(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_cap, out_pitch, start_bit,
-                      segmented, frame_bits, end_bits, coef);
+                      segmented, frame_bits, end_bits, coef, hist);
     }
     if (!out_dev) {
         for (int ch = 0; ch < nchains; ch++) {
@@ -757,6 +762,24 @@ int ie_encode_images(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, s
                   out_pitch, start_bit, 1, nullptr, end_bits);
 }
 
+int ie_encode_images_counted(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
+                             int use_rle, int mode, uint8_t* out, size_t out_pitch, uint64_t start_bit) {
+    if (!c || !y || !out || nframes <= 0) return IE_EINVAL;
+    // no fused variant (EXACT mode, 8x8 -- its registers are full --, host output): the histogram
+    // pass counts later
+    if (mode == IE_MODE_EXACT || c->n != 4 || !is_device_ptr(out))
+        return ie_encode_images(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_pitch, start_bit,
+                                nullptr);
+    // the counts go where ie_huffman_hist_batch_ends_async expects them (d_batch, same layout)
+    const size_t K = size_t(nframes);
+    int r;
+    if ((r = ensure(c, c->d_batch, c->cap_batch, K * 256 * 12 + K * 8 + K * 4))) return r;
+    r = encode(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_pitch * K, out_pitch, start_bit, 1,
+               nullptr, nullptr, nullptr, reinterpret_cast<uint32_t*>(c->d_batch));
+    if (r == IE_OK) c->fused_count = nframes;
+    return r;
+}
+
 int ie_quantize_frames(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
                        int mode, int16_t* coef) {
     if (!c || !y || !coef) return IE_EINVAL;
@@ -876,6 +899,7 @@ int ie_bitcopy(ie_ctx* c, const uint8_t* bytes, size_t n, uint8_t* out, size_t o
 
 int ie_huffman_hist_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
                           uint32_t* hist, uint64_t* first_pos) {
+    if (c) c->fused_count = 0;
     if (!c || !in || !n || count <= 0 || !hist || !first_pos) return IE_EINVAL;
     if (!is_device_ptr(in)) return fail(c, IE_EINVAL, "batched Huffman input must be device memory");
     HIPCHK(c, hipSetDevice(c->device));
@@ -912,6 +936,7 @@ const uint64_t* ie_last_end_bits(ie_ctx* c) { return c ? c->d_chain_end : nullpt
 
 int ie_huffman_hist_batch_ends(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* end_bits, int count,
                                uint32_t* hist, uint64_t* first_pos) {
+    if (c) c->fused_count = 0;
     if (!c || !in || !end_bits || count <= 0 || !hist || !first_pos) return IE_EINVAL;
     if (!is_device_ptr(in) || !is_device_ptr(end_bits))
         return fail(c, IE_EINVAL, "batched Huffman input and end bits must be device memory");
@@ -941,9 +966,13 @@ int ie_huffman_hist_batch_ends_async(ie_ctx* c, const uint8_t* in, size_t in_pit
     if (!is_device_ptr(in) || !is_device_ptr(end_bits))
         return fail(c, IE_EINVAL, "batched Huffman input and end bits must be device memory");
     HIPCHK(c, hipSetDevice(c->device));
+    // counts left by ie_encode_images_counted for exactly this batch: only the first positions remain
+    const bool fused = c->fused_count == count;
+    c->fused_count = 0;
     const size_t hb = size_t(count) * 256 * sizeof(uint32_t), fb = size_t(count) * 256 * sizeof(uint64_t);
     const size_t nb = size_t(count) * sizeof(uint64_t), ub = size_t(count) * sizeof(unsigned);
     int r;
+    if (fused && c->cap_batch < hb + fb + nb + ub) return fail(c, IE_EINVAL, "fused histogram scratch lost");
     if ((r = ensure(c, c->d_batch, c->cap_batch, hb + fb + nb + ub))) return r;
     if ((r = ensure_pinned(c, c->h_hist[slot], c->cap_hhist[slot], hb + fb))) return r;
     if (!c->ev_hist[slot]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_hist[slot], hipEventDisableTiming));
@@ -951,8 +980,8 @@ int ie_huffman_hist_batch_ends_async(ie_ctx* c, const uint8_t* in, size_t in_pit
     auto* df = reinterpret_cast<unsigned long long*>(c->d_batch + hb);
     auto* dn = reinterpret_cast<uint64_t*>(c->d_batch + hb + fb);
     auto* du = reinterpret_cast<unsigned*>(c->d_batch + hb + fb + nb);
-    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream, dh, df);
-    ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream);
+    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream, fused ? nullptr : dh, df);
+    ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream, !fused);
     HIPCHK(c, hipGetLastError());
     // histograms and first positions are contiguous on the device: one read-back
     HIPCHK(c, hipMemcpyAsync(c->h_hist[slot], c->d_batch, hb + fb, hipMemcpyDeviceToHost, c->stream));
@@ -977,6 +1006,7 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
                           uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit) {
     if (!c || !in || !n || count <= 0 || !code || !len || !out || !start_bit || (!prefix && prefix_pitch))
         return IE_EINVAL;
+    c->fused_count = 0;  // the staged tables overwrite the batch scratch
     if (!is_device_ptr(in) || !is_device_ptr(out))
         return fail(c, IE_EINVAL, "batched Huffman input and output must be device memory");
     if (reinterpret_cast<uintptr_t>(out) % 4 || out_pitch % 4)

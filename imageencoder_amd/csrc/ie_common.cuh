@@ -305,9 +305,13 @@ __device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain
 #ifndef IE_NT_STORE
 #define IE_NT_STORE 1
 #endif
-template <int TPB = kTPB>
+// An optional observer of every stored word: cnt(word index, value as stored).
+struct NoCount {
+    __device__ __forceinline__ void operator()(uint64_t, uint32_t) const {}
+};
+template <int TPB = kTPB, class Cnt = NoCount>
 __device__ __forceinline__ void store_image(uint32_t* out, const uint32_t* L, uint32_t bits, uint64_t P,
-                                            uint32_t prev, bool last, bool skip0 = false) {
+                                            uint32_t prev, bool last, bool skip0 = false, const Cnt& cnt = Cnt()) {
     // Output word r (r = 0 at word floor(P/32)) is the funnel shift of image words r-1 and r:
     // alignbit(L[r-1], L[r], s), with L[-1] = prev and s = 0 giving L[r] itself.  The caller's
     // image is zero through word ceil(bits/32), so L[r] needs no bound check.
@@ -324,7 +328,11 @@ __device__ __forceinline__ void store_image(uint32_t* out, const uint32_t* L, ui
     // skip0: word 0 is written later by the caller (its predecessor bits are not known yet)
     const uint32_t head0 = min(nw, uint32_t((4u - uint32_t(w0 & 3u)) & 3u));
     const uint32_t head = (skip0 && head0 == 0) ? min(nw, 4u) : head0;
-    if (tid < head && !(skip0 && tid == 0)) out[w0 + tid] = word(tid);
+    if (tid < head && !(skip0 && tid == 0)) {
+        const uint32_t v = word(tid);
+        out[w0 + tid] = v;
+        cnt(w0 + tid, v);
+    }
     const uint32_t nq = (nw - head) >> 2;
 #pragma unroll 2
     for (uint32_t q = tid; q < nq; q += TPB) {
@@ -345,23 +353,33 @@ __device__ __forceinline__ void store_image(uint32_t* out, const uint32_t* L, ui
 #else
         *reinterpret_cast<uint4*>(out + w0 + r) = v;
 #endif
+        cnt(w0 + r, v.x);
+        cnt(w0 + r + 1, v.y);
+        cnt(w0 + r + 2, v.z);
+        cnt(w0 + r + 3, v.w);
     }
     const uint32_t t0 = head + 4u * nq;
-    if (tid < nw - t0) out[w0 + t0 + tid] = word(t0 + tid);
+    if (tid < nw - t0) {
+        const uint32_t v = word(t0 + tid);
+        out[w0 + t0 + tid] = v;
+        cnt(w0 + t0 + tid, v);
+    }
 }
 
 // The tile store after chain_resolve(..., defer_tail = true): the bulk of the words first, then
 // (misc[8] set) thread 0 fetches the predecessor's tail and completes the first word.
-template <int TPB = kTPB>
+template <int TPB = kTPB, class Cnt = NoCount>
 __device__ __forceinline__ void store_tile(uint32_t* out, const uint32_t* L, uint32_t bits, uint64_t P,
                                            const uint32_t* misc, bool last, const uint64_t* st, int pred,
-                                           uint32_t tag, unsigned* err) {
+                                           uint32_t tag, unsigned* err, const Cnt& cnt = Cnt()) {
     const bool pend = misc[8] != 0u;
-    store_image<TPB>(out, L, bits, P, misc[7], last, pend);
+    store_image<TPB>(out, L, bits, P, misc[7], last, pend, cnt);
     if (pend && threadIdx.x == 0) {
         const uint32_t pt = wait_tail(st, pred, tag, err);
         const uint32_t s = uint32_t(P & 31);
-        out[P >> 5] = bswap32((pt << (32 - s)) | (L[0] >> s));
+        const uint32_t v = bswap32((pt << (32 - s)) | (L[0] >> s));
+        out[P >> 5] = v;
+        cnt(P >> 5, v);
     }
 }
 

@@ -68,6 +68,9 @@ struct EncArgs {
     uint64_t* stamps;        // profiling only (IE_STAMPS): [tile][kStamps] s_memtime per phase, thread 0
     int rec_bits;            // = tab->rec_bits (host copy): launch_encode sizes the LDS tile image from it
     int img_words;           // set by launch_encode
+    // optional (segmented launches): per-frame byte histograms [nframes][256] of the stream bytes
+    // [0, ceil(end/8)) -- header included -- ADDED to by the launch (the Huffman pass's counts)
+    uint32_t* hist;
 };
 
 constexpr int kStamps = 16;
@@ -107,7 +110,7 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
 // input bytes per pack tile for codes of at most maxlen bits (ie_huffman.hip)
 int pack_tile_bytes(int maxlen);
 void launch_pack(const PackArgs& a, hipStream_t s);
-// hist / first (optional, count*256 each): cleared to 0 / ~0 by the same launch
+// hist / first (each optional, count*256): cleared to 0 / ~0 by the same launch
 void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s,
                           uint32_t* hist = nullptr, unsigned long long* first = nullptr);
 // unresolved: device scratch, one word per string
@@ -115,8 +118,10 @@ void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long lo
                  hipStream_t s);
 // count strings at in + k*pitch, n[k] (device array) bytes each, maxn >= every n[k]:
 // hist/first + 256*k
+// counts = false: hist already holds the counts (an encoder launch with EncArgs::hist); only the
+// first occurrences are computed
 void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count, uint32_t* hist,
-                       unsigned long long* first, unsigned* unresolved, hipStream_t s);
+                       unsigned long long* first, unsigned* unresolved, hipStream_t s, bool counts = true);
 
 struct DecArgs {
     const uint64_t* block_bit;  // [nblocks] start bit of every block record (from the walk index)

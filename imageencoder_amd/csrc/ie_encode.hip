@@ -587,7 +587,24 @@ __device__ __forceinline__ void emit_block_sink(WordSink& k, const uint32_t (&zp
 #else
 #define IE_ENC_BOUNDS(N) __launch_bounds__(kEncTPB, Geo<N>::WAVES)
 #endif
-template <int N, bool EXACT>
+// HIST: count the stored bytes into a per-tile LDS histogram (256 words after the misc area),
+// merged into a.hist[frame] at the end: the Huffman pass's histogram without re-reading the stream.
+struct HistCount {
+    uint32_t* hl;
+    uint64_t limit;  // bytes at stream positions >= limit are padding (the chain's last word)
+    __device__ __forceinline__ void operator()(uint64_t gw, uint32_t v) const {
+        if (limit == ~0ull) {  // (wave-uniform) not the chain's last tile: every byte counts
+#pragma unroll
+            for (int k = 0; k < 4; k++) atomicAdd(&hl[(v >> (8 * k)) & 0xFFu], 1u);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (4 * gw + k < limit) atomicAdd(&hl[(v >> (8 * k)) & 0xFFu], 1u);
+        }
+    }
+};
+
+template <int N, bool EXACT, bool HIST = false>
 __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     constexpr int NN = N * N;
     constexpr int NP = NN / 2;
@@ -626,6 +643,8 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
         t = int(blockIdx.x);
     }
     STAMP(0);
+    uint32_t* const hl = misc + 32;  // HIST: the tile's byte histogram
+    if constexpr (HIST) hl[tid] = 0u;  // (visible after the scan's barriers)
     if constexpr (!EXACT) {
         // issued before the pixel loads, so waiting for it does not wait for them
         for (int i = tid; i < 3 * NN + 9; i += TPB) srow[i] = tab->srow[i];
@@ -1085,8 +1104,22 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     STAMP(8);
 
     // ---------------------------------------------------------------- 4. store
-    if (!(ablate & 8))
+    if constexpr (HIST) {
+        static_assert(TPB == 256, "one histogram bin per thread");
+        if (tif == 0)  // the words before the first record word hold only the caller's header
+            for (uint32_t i = tid; i < uint32_t(a.start_bit >> 5); i += TPB) {
+                const uint32_t v = out[i];
+#pragma unroll
+                for (int k = 0; k < 4; k++) atomicAdd(&hl[(v >> (8 * k)) & 0xFFu], 1u);
+            }
+        const uint64_t end = a.start_bit + excl + A;
+        const HistCount cnt{hl, chain_last ? (end + 7) / 8 : ~0ull};
+        store_tile<TPB>(out, img, A, a.start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err, cnt);
+        lds_barrier();
+        if (hl[tid]) atomicAdd(&a.hist[size_t(frame) * 256 + tid], hl[tid]);
+    } else if (!(ablate & 8)) {
         store_tile<TPB>(out, img, A, a.start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err);
+    }
     STAMP(9);
 }
 
@@ -1104,9 +1137,13 @@ void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s) {
     a.img_words = image_words_for(4, 4, IE_STATIC_IMG4);
     const size_t lds = 0;
 #else
-    const size_t lds = (size_t(a.img_words) + 32) * sizeof(uint32_t);
+    const size_t lds = (size_t(a.img_words) + 32 + (a.hist ? 256 : 0)) * sizeof(uint32_t);
 #endif
     const dim3 grid(a.ntiles), block(kEncTPB);
+    if (a.hist) {  // segmented 4x4 FAST launches only (ie_encode_images_counted; 8x8 would spill)
+        hipLaunchKernelGGL((encode_kernel<4, false, true>), grid, block, lds, s, a, a.tab);
+        return;
+    }
     if (n == 4) {
         if (exact) hipLaunchKernelGGL((encode_kernel<4, true>), grid, block, lds, s, a, a.tab);
         else hipLaunchKernelGGL((encode_kernel<4, false>), grid, block, lds, s, a, a.tab);

@@ -159,14 +159,14 @@ __global__ void ends_to_bytes_kernel(const uint64_t* ends, uint64_t cap, int cou
                                      unsigned long long* first) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < count) n[k] = min<uint64_t>((ends[k] + 7) / 8, cap);
-    if (hist && k < 256 * count) {
-        hist[k] = 0u;
-        first[k] = ~0ull;
+    if (k < 256 * count) {
+        if (hist) hist[k] = 0u;
+        if (first) first[k] = ~0ull;
     }
 }
 void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s, uint32_t* hist,
                           unsigned long long* first) {
-    const int threads = hist ? 256 * count : count;
+    const int threads = (hist || first) ? 256 * count : count;
     hipLaunchKernelGGL(ends_to_bytes_kernel, dim3((threads + kTPB - 1) / kTPB), dim3(kTPB), 0, s, ends, cap, count, n,
                        hist, first);
 }
@@ -182,11 +182,11 @@ void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long lo
 }
 
 void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count, uint32_t* hist,
-                       unsigned long long* first, unsigned* unresolved, hipStream_t s) {
+                       unsigned long long* first, unsigned* unresolved, hipStream_t s, bool counts) {
     const uint64_t tiles = (maxn + kHistTile - 1) / kHistTile;
     const uint64_t per = (4096 + count - 1) / count;  // ~4096 workgroups over the batch
     const int gx = int(tiles < per ? (tiles ? tiles : 1) : per);
-    hipLaunchKernelGGL(hist_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist);
+    if (counts) hipLaunchKernelGGL(hist_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist);
     hipLaunchKernelGGL(first_scan_batch_kernel, dim3(count), dim3(kTPB), 0, s, in, pitch, n, hist, first, unresolved);
     hipLaunchKernelGGL(first_full_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist, first,
                        unresolved);

@@ -92,6 +92,15 @@ int ie_encode_images(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride,
                      int nframes, int use_rle, int mode, uint8_t* out, size_t out_pitch,
                      uint64_t start_bit, uint64_t* end_bits);
 
+/* ie_encode_images (device output) that also counts the bytes of every image's stream -- the
+ * caller's header words included, bytes [0, ceil(end_bit / 8)) -- while storing them: the counts
+ * stay on the device for the next ie_huffman_hist_batch_ends_async over the same batch, which
+ * then skips its own histogram pass (Huffman.cpp:237-243 without re-reading the stream).  MODE_EXACT,
+ * 8x8 blocks or host output: a plain ie_encode_images (the histogram pass counts later).  No end bits are
+ * returned (ie_last_end_bits holds them on the device). */
+int ie_encode_images_counted(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch,
+                             int nframes, int use_rle, int mode, uint8_t* out, size_t out_pitch, uint64_t start_bit);
+
 /* Quantised DCT coefficients only (Block::processDCTDivQ, Block.cpp:139-153): coef receives
  * nframes * (w/n) * (h/n) blocks of n*n int16 in natural (row-major) order, block raster order.
  * coef may be host or device memory.  Diagnostic / analysis entry point. */

@@ -338,10 +338,12 @@ def test_huffman_after_encode_pipeline(codec):
 
 
 @pytest.mark.gpu
-def test_huffman_after_encode_pipelined(codec):
+@pytest.mark.parametrize("counted", [False, True], ids=["hist_pass", "counted_encode"])
+def test_huffman_after_encode_pipelined(codec, counted):
     """Batches pipelined as in bench.py's C5 step: batch i+1's encode and histogram are issued
     before batch i's trees + pack (two output buffers, histogram slots alternating); every
-    image's Huffman-coded file still equals the reference's."""
+    image's Huffman-coded file still equals the reference's.  counted: the byte counts come from
+    the encoder itself (ie_encode_images_counted)."""
     import torch
     from imageencoder_amd import stream_bound, write_header
     n, q, w, h, f, nb = 4, O.read_matrix("matrix.txt", 4), 256, 128, 3, 4
@@ -362,7 +364,7 @@ def test_huffman_after_encode_pipelined(codec):
     pending = None
     for b in range(nb):
         codec.encode_images(torch.from_numpy(ys[b]).cuda(), w, h, outs[b % 2], out_pitch=pitch, nframes=f,
-                            start_bit=hb, want_sizes=False)
+                            start_bit=hb, want_sizes=False, count_bytes=counted)
         codec.huffman_begin_after_encode(outs[b % 2], pitch, f, b % 2)
         if pending is not None:
             p = pending
@@ -376,3 +378,42 @@ def test_huffman_after_encode_pipelined(codec):
         for k in range(f):
             want = O.load().encode_image(ys[b][k], n, q, rle=True, huffman=True)
             assert host[k * hpitch: k * hpitch + sizes[b][k]].tobytes() == want, (b, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,f,start_bit,kind", [
+    (320, 192, 3, 165, "M"),     # a settings header ending inside a word
+    (200, 56, 4, 0, "U"),        # no header; ragged tile coverage
+    (1000, 600, 3, 64, "U"),     # multi-tile chains, header of whole words
+    (3840, 2160, 2, 171, "M"),   # 4K: hundreds of tiles per chain
+])
+def test_counted_encode_histogram(codec, w, h, f, start_bit, kind):
+    """ie_encode_images_counted's fused byte counts equal the separate histogram pass's and a
+    host bincount of each stream's bytes [0, ceil(end / 8)) -- header words included, the last
+    word's padding bytes excluded; the first positions match too."""
+    import torch
+    from imageencoder_amd import stream_bound
+    n, q = 4, O.read_matrix("matrix.txt", 4)
+    codec.set_quant(q, n)
+    pitch = (stream_bound(w, h, n, 1, start_bit) + 255) // 256 * 256
+    y = torch.from_numpy(synth.frames(kind, w, h, f, seed=77)).cuda()
+    rng = np.random.default_rng(5)
+    out = torch.zeros(pitch * f, dtype=torch.uint8)
+    nh = (start_bit + 7) // 8
+    for k in range(f):  # header bytes (random), bits from start_bit on left zero
+        hdr = rng.integers(0, 256, nh, dtype=np.uint8)
+        if start_bit % 8:
+            hdr[-1] &= np.uint8((0xFF00 >> (start_bit % 8)) & 0xFF)
+        out[k * pitch: k * pitch + nh] = torch.from_numpy(hdr)
+    out = out.cuda()
+    codec.encode_images(y, w, h, out, out_pitch=pitch, nframes=f, start_bit=start_bit, count_bytes=True)
+    h_fused, f_fused = codec.huffman_hist_after_encode(out, pitch, f)
+    ends = codec.encode_images(y, w, h, out, out_pitch=pitch, nframes=f, start_bit=start_bit)
+    h_pass, f_pass = codec.huffman_hist_after_encode(out, pitch, f)
+    host = out.cpu().numpy()
+    for k in range(f):
+        nb = (int(ends[k]) + 7) // 8
+        want = np.bincount(host[k * pitch: k * pitch + nb], minlength=256).astype(np.uint32)
+        np.testing.assert_array_equal(h_pass[k], want)
+        np.testing.assert_array_equal(h_fused[k], want)
+    np.testing.assert_array_equal(f_fused, f_pass)

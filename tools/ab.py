@@ -23,6 +23,8 @@ ap.add_argument("--frames", type=int, default=16)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--kind", default="U")
+ap.add_argument("--op", default="encode", choices=["encode", "counted"],
+                help="counted: time ie_encode_images_counted (the encoder with the fused byte histogram)")
 ap.add_argument("libs", nargs="+")
 args = ap.parse_args()
 
@@ -57,7 +59,17 @@ for path in args.libs:
     out.zero_()
     eb = np.zeros(nf, dtype=np.uint64)
 
+    if args.op == "counted":
+        L.ie_encode_images_counted.argtypes = [vp, vp, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
+                                               C.c_int, vp, C.c_size_t, C.c_uint64]
+
     def run(L=L, hnd=hnd, out=out, pitch=pitch, eb=eb, sizes=False):
+        if args.op == "counted" and not sizes:
+            r = L.ie_encode_images_counted(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, nf, 1, 0,
+                                           C.c_void_p(out.data_ptr()), pitch, 165)
+            if r != 0:
+                raise RuntimeError(L.ie_last_error(hnd))
+            return
         r = L.ie_encode_images(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, nf, 1, 0, C.c_void_p(out.data_ptr()),
                                pitch, 165, eb.ctypes.data_as(C.POINTER(C.c_uint64)) if sizes else None)
         if r != 0:
