@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--mode", default="fast", choices=["fast", "exact"])
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-iters", type=int, default=4)
+    p.add_argument("--no-decode", action="store_true", help="skip the one-image decode timing (inverse path)")
     p.add_argument("--single-frame", action="store_true",
                    help="also time one-image launches (the latency of a single 4K encode)")
     return p.parse_args()
@@ -258,6 +259,23 @@ def main():
             _, g1 = timer.run(single, 2, 4 * B)
             extra["single_frame"] = {"us_per_frame": round(g1 / (4 * B) * 1e6, 2),
                                      "Mpx_s": round(w * h / (g1 / (4 * B)) / 1e6, 1)}
+        if not cfg["huffman"] and not args.no_decode:
+            # the inverse path: one image's stream decoded back to pixels on the
+            # device (chunked record walk + index scan + FP64 IDCT), wall time per call incl. syncs
+            ends0 = codec.encode_images(frames[:B], w, h, outs[0], out_pitch=pitch, nframes=B, start_bit=hdr_bits,
+                                        mode=mode)
+            nb0 = (int(ends0[0]) + 7) // 8
+            pix = torch.empty((h, w), dtype=torch.uint8, device=dev)
+            one = outs[0][:nb0]
+            codec.decode_frames(one, w, h, pix, start_bit=hdr_bits, length=nb0)
+            torch.cuda.synchronize(dev)
+            kd = 10
+            t0 = time.perf_counter()
+            for _ in range(kd):
+                codec.decode_frames(one, w, h, pix, start_bit=hdr_bits, length=nb0)
+            torch.cuda.synchronize(dev)
+            td = (time.perf_counter() - t0) / kd
+            extra["decode_one_image"] = {"us": round(td * 1e6, 1), "Mpx_s": round(w * h / td / 1e6, 1)}
         workload = (f"{args.workload}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
                     f"{' +Huffman' if cfg['huffman'] else ''}, batch of {B} independent images per step, "
                     f"{R} distinct resident frames per GPU ({R * w * h / 2**20:.0f} MiB)")

@@ -378,22 +378,31 @@ int decode_frames_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, 
     hipLaunchKernelGGL(walk_kernel, g, blk, 0, s, wa);
     uint64_t* cur = exA;
     uint64_t* nxt = exB;
-    int rounds = 0;
-    for (; rounds < max_rounds; rounds++) {
+    // fix-up rounds in growing groups (1, 2, 4, 8, 8, ...) between host checks: most 4x4 streams
+    // settle after one round, 8x8 ones take ~20; a round after convergence is a near-empty launch
+    // (~15 us), a host round trip per round costs more
+    int rounds = 0, group = 1;
+    bool done = false;
+    // (convergence takes at most max_rounds rounds; a group after it confirms it)
+    while (!done && rounds < max_rounds + 8) {
         unsigned h = 0;
         if (hipMemsetAsync(changed, 0, sizeof(unsigned), s) != hipSuccess) return -1;
-        wa.first = 0;
-        wa.exit_in = cur;
-        wa.exit_out = nxt;
-        hipLaunchKernelGGL(walk_kernel, g, blk, 0, s, wa);
+        for (int r = 0; r < group; r++) {
+            wa.first = 0;
+            wa.exit_in = cur;
+            wa.exit_out = nxt;
+            hipLaunchKernelGGL(walk_kernel, g, blk, 0, s, wa);
+            uint64_t* t = cur;
+            cur = nxt;
+            nxt = t;
+        }
+        rounds += group;
+        group = group < 8 ? 2 * group : 8;
         if (hipMemcpyAsync(&h, changed, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
         if (hipStreamSynchronize(s) != hipSuccess) return -1;
-        uint64_t* t = cur;
-        cur = nxt;
-        nxt = t;
-        if (!h) break;
+        done = (h == 0);
     }
-    if (rounds == max_rounds) return -2;
+    if (!done) return -2;
     hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
     hipLaunchKernelGGL(index_kernel, g, blk, 0, s, wa, base, block_bit, uint64_t(da.nframes) * da.bx * da.by);
     DecArgs d = da;
