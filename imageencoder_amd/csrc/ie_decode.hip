@@ -124,21 +124,31 @@ __global__ void index_kernel(WalkArgs a, const uint64_t* base, uint64_t* block_b
     walk(a, a.entry[k], cstart + a.chunk_bits, &x, &c, &b, block_bit, nblocks);
 }
 
-// exclusive scan of per-chunk counts (single workgroup, sequential over strips)
-__global__ void scan_counts_kernel(const uint32_t* count, uint64_t* base, int n) {
+// exclusive scan of per-chunk counts: one workgroup, each thread owns kScanRun consecutive counts
+// (one block scan per kTPB * kScanRun counts instead of one per kTPB)
+constexpr int kScanRun = 32;
+__global__ __launch_bounds__(kTPB) void scan_counts_kernel(const uint32_t* count, uint64_t* base, int n) {
     __shared__ uint32_t scratch[8];
-    __shared__ uint64_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int s = 0; s < n; s += kTPB) {
-        const int i = s + threadIdx.x;
-        const uint32_t v = (i < n) ? count[i] : 0u;
+    uint64_t carry = 0;  // the same in every thread
+    for (int s = 0; s < n; s += kTPB * kScanRun) {
+        const int i0 = s + int(threadIdx.x) * kScanRun;
+        uint32_t v[kScanRun];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < kScanRun; j++) {
+            v[j] = (i0 + j < n) ? count[i0 + j] : 0u;
+            sum += v[j];
+        }
         uint32_t tot;
-        const uint32_t ex = block_excl_scan(v, scratch, &tot);
-        if (i < n) base[i] = carry + ex;
-        __syncthreads();
-        if (threadIdx.x == 0) carry += tot;
-        __syncthreads();
+        const uint32_t ex = block_excl_scan(sum, scratch, &tot);
+        uint64_t run = carry + ex;
+#pragma unroll
+        for (int j = 0; j < kScanRun; j++) {
+            if (i0 + j < n) base[i0 + j] = run;
+            run += v[j];
+        }
+        carry += tot;
+        __syncthreads();  // scratch is reused by the next strip's scan
     }
 }
 
