@@ -1187,7 +1187,11 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     HIPCHK(c, hipMemcpyAsync(c->d_dec, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                              c->stream));
     const uint64_t nbits = uint64_t(len) * 8;
-    const uint64_t chunk_bits = 4096;
+    // walk chunk (measured on 4K: 4x4 4096 bits, 8x8 16384 -- its wrong-phase walks couple late,
+    // so longer chunks mean fewer fix-up rounds); IE_DEC_CHUNK4 / IE_DEC_CHUNK8 override (tuning aid)
+    static const uint64_t chunk4 = getenv("IE_DEC_CHUNK4") ? strtoull(getenv("IE_DEC_CHUNK4"), nullptr, 10) : 4096;
+    static const uint64_t chunk8 = getenv("IE_DEC_CHUNK8") ? strtoull(getenv("IE_DEC_CHUNK8"), nullptr, 10) : 16384;
+    const uint64_t chunk_bits = std::max<uint64_t>(256, n == 4 ? chunk4 : chunk8);
     const size_t nchunks = size_t((nbits - start_bit) / chunk_bits + 1);
     if ((r = ensure(c, c->d_walk, c->cap_walk, 4 * nchunks))) return r;
     if ((r = ensure(c, c->d_count, c->cap_count, nchunks))) return r;
