@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-iters", type=int, default=4)
     p.add_argument("--no-decode", action="store_true", help="skip the one-image decode timing (inverse path)")
+    p.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) timing")
     p.add_argument("--single-frame", action="store_true",
                    help="also time one-image launches (the latency of a single 4K encode)")
     return p.parse_args()
@@ -259,6 +260,19 @@ def main():
             _, g1 = timer.run(single, 2, 4 * B)
             extra["single_frame"] = {"us_per_frame": round(g1 / (4 * B) * 1e6, 2),
                                      "Mpx_s": round(w * h / (g1 / (4 * B)) / 1e6, 1)}
+        if not cfg["huffman"] and not args.no_e2e:
+            # end to end from HOST buffers (reported separately, never `value`): pageable
+            # numpy frames in, the library stages them over PCIe, encodes, copies the streams back
+            yh = frames[:B].cpu().numpy()
+            oh = np.zeros(pitch * B, dtype=np.uint8)
+            codec.encode_images(yh, w, h, oh, out_pitch=pitch, nframes=B, start_bit=hdr_bits, mode=mode)
+            ke = 3
+            t0 = time.perf_counter()
+            for _ in range(ke):
+                codec.encode_images(yh, w, h, oh, out_pitch=pitch, nframes=B, start_bit=hdr_bits, mode=mode)
+            te = (time.perf_counter() - t0) / ke
+            extra["e2e_host_buffers"] = {"ms_per_batch": round(te * 1e3, 2), "Mpx_s": round(B * w * h / te / 1e6, 1),
+                                         "note": "pageable host frames in, host streams out (PCIe both ways)"}
         if not cfg["huffman"] and not args.no_decode:
             # the inverse path: one image's stream decoded back to pixels on the
             # device (chunked record walk + index scan + FP64 IDCT), wall time per call incl. syncs
