@@ -55,8 +55,10 @@ def parse():
     p.add_argument("--cpu-iters", type=int, default=4)
     p.add_argument("--no-decode", action="store_true", help="skip the one-image decode timing (inverse path)")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) timing")
-    p.add_argument("--single-frame", action="store_true",
-                   help="also time one-image launches (the latency of a single 4K encode)")
+    p.add_argument("--batch", type=int, default=None, help="frames per launch (default: the workload's)")
+    p.add_argument("--resident", type=int, default=None, help="distinct resident frames (default: the workload's)")
+    p.add_argument("--no-single-frame", dest="single_frame", action="store_false",
+                   help="skip timing one-image launches (configs[1] taken literally: one 4K frame per launch)")
     return p.parse_args()
 
 
@@ -174,6 +176,8 @@ def main():
     dev = torch.device("cuda", local)
 
     w, h, n, B, R = cfg["w"], cfg["h"], cfg["n"], cfg["batch"], cfg["resident"]
+    B = args.batch or B
+    R = max(args.resident or R, B)
     q = O.read_matrix(cfg["matrix"], n)
     codec = Codec(local, q, n)
     # a dedicated stream: the encoder's launches and the timing events share it (the default
