@@ -1132,7 +1132,9 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
     HIPCHK(c, hipMemcpyAsync(c->d_hlut, lut, 32768 * sizeof(uint16_t),
                              is_device_ptr(lut) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
     const uint64_t nbits = uint64_t(len) * 8;
-    const uint64_t chunk_bits = 2048;
+    // walk chunk of the Huffman decode; IE_HUF_CHUNK overrides (tuning aid)
+    static const uint64_t huf_chunk = getenv("IE_HUF_CHUNK") ? strtoull(getenv("IE_HUF_CHUNK"), nullptr, 10) : 2048;
+    const uint64_t chunk_bits = std::max<uint64_t>(256, huf_chunk);
     const size_t nchunks = size_t((nbits - start_bit + chunk_bits - 1) / chunk_bits);
     if (!nchunks) return IE_OK;
     if ((r = ensure(c, c->d_walk, c->cap_walk, 4 * nchunks))) return r;
