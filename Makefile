@@ -18,7 +18,7 @@ all: lib host oracle
 
 lib: $(LIBDIR)/libie_hip.so
 
-$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.cuh include/ie_hip.h
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp include/ie_hip.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -58,11 +58,14 @@ oracle:
 ref:
 	$(MAKE) -C oracle ref
 
-# Check the exact FP64 path really is unfused: dump the gfx950 ISA of the encode kernels.
-asmcheck:
+# Check the exact FP64 paths really are unfused: dump the gfx950 ISA of the
+# encode and decode kernels and scan it (tools/asmcheck.py; also reports VGPRs / scratch).
+ASMS := $(OBJDIR)/asm/ie_encode.s $(OBJDIR)/asm/ie_decode.s
+$(OBJDIR)/asm/%.s: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp $(CSRC)/ie_dct.h
 	@mkdir -p $(OBJDIR)/asm
-	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $(CSRC)/ie_encode.hip -o $(OBJDIR)/asm/ie_encode.s
-	@python3 tools/asmcheck.py $(OBJDIR)/asm/ie_encode.s
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o $@
+asmcheck: $(ASMS)
+	python3 tools/asmcheck.py $(ASMS)
 
 clean:
 	rm -rf $(OBJDIR) $(LIBDIR)

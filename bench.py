@@ -4,26 +4,37 @@ MI355X, with the reference's own OpenMP CPU encoder timed beside it.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
 
-A "step" is one launch of the encoder over one batch of distinct synthetic frames resident in
-HBM (a rotating set larger than the 256 MiB Infinity Cache, so HBM is what is measured):
+A "step" is one pass of the encoder over one batch of distinct synthetic frames resident in HBM
+(a rotating set larger than the 256 MiB Infinity Cache, so HBM is what is measured):
 
-  c2 (default)  3840x2160, 4x4 blocks, matrix.txt, RLE: a batch of independent images
-  c3            3840x2160, 8x8 blocks, matrix8_1.txt, RLE
-  c4            1920x1080 gop=1 video batch, 4x4: frames sharded over ranks, ONE stream
-                assembled on rank 0 by an RCCL gather (encode + gather are both timed)
-  c5            3840x2160, 4x4, Huffman post-pass on every image (device histogram + host
-                tree build + device re-encode)
+  c2 (default at N=1)  3840x2160, 4x4 blocks, matrix.txt, RLE: a batch of independent images
+  c3                   3840x2160, 8x8 blocks, matrix8_1.txt, RLE
+  c4 (default at N>1)  1920x1080 gop=1 video, 4x4: 64 frames per GPU (512 at N=8), sharded over
+                       the ranks and assembled into ONE stream on rank 0 (all_gather of the bit
+                       counts, per-rank bit re-shift, RCCL point-to-point gather); encode and
+                       gather are both timed, the gather of one sub-batch overlapping the encode
+                       of the next (imageencoder_amd/dist.py PipelinedGather)
+  c5                   3840x2160, 4x4, Huffman post-pass on every image (device histogram +
+                       host tree build + device re-encode)
 
-For N>1 run under torch.distributed.run: one process per GPU, each rank encodes its own batch
-(weak scaling); rank 0 prints one JSON line.  value = all pixels encoded by all ranks / max-over-
+--gpus N > 1 without a torch.distributed environment re-launches itself as
+``python -m torch.distributed.run --nproc-per-node N`` (this parent never touches a GPU) and
+relays rank 0's line.  One process per GPU; value = all pixels encoded by all ranks / max-over-
 ranks wall time of the K timed steps (inputs already resident, outputs left in HBM).
+
+After the timed steps every run checks its own output (``bit_exact``): the reference golden md5
+of the 4K synthetic image (c2/c3/c5: image 0 of the batch is that golden's frame) or, for c4, the
+golden 3-frame 1080p gop=1 stream plus the assembled N-rank stream against a single-GPU encode of
+the same frames; asynchronous launches are checked for look-back timeouts (ie_sync).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -33,15 +44,23 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")  # data files (matrices, manifest of md5s)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 WORKLOADS = {
-    "c2": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=False),
-    "c3": dict(w=3840, h=2160, n=8, matrix="matrix8_1.txt", batch=16, resident=64, gen="U", huffman=False),
-    "c4": dict(w=1920, h=1080, n=4, matrix="matrix.txt", batch=64, resident=128, gen="U", huffman=False),
-    "c5": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=True),
+    "c2": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=False,
+               golden="synU4k_4x4"),
+    "c3": dict(w=3840, h=2160, n=8, matrix="matrix8_1.txt", batch=16, resident=64, gen="U", huffman=False,
+               golden="synU4k_8x8"),
+    # c4: batch = frames per GPU per step, split into `chunks` pipelined sub-batches
+    "c4": dict(w=1920, h=1080, n=4, matrix="matrix.txt", batch=64, resident=128, gen="U", huffman=False,
+               chunks=4, golden="vidU1080x3_4x4"),
+    "c5": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=True,
+               golden="synU4k_4x4_huff"),
 }
+METRIC = "Mpixels/s encode (DCT+quant+RLE), 4K grayscale, 1/2/4/8 GPU + CPU ref"
+ARITH = "FP32 separable DCT + FP64 re-evaluation of near-tie coefficients (bit-exact vs the FP64 reference)"
 
 
 def parse():
@@ -49,12 +68,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    p.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                   help="default: c2 at one GPU, c4 (the multi-GPU configuration) above")
     p.add_argument("--mode", default="fast", choices=["fast", "exact"])
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    p.add_argument("--cpu-iters", type=int, default=4)
+    p.add_argument("--cpu-iters", type=int, default=2)
     p.add_argument("--no-decode", action="store_true", help="skip the one-image decode timing (inverse path)")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) timing")
+    p.add_argument("--no-check", action="store_true", help="skip the output self-check")
     p.add_argument("--batch", type=int, default=None, help="frames per launch (default: the workload's)")
     p.add_argument("--resident", type=int, default=None, help="distinct resident frames (default: the workload's)")
     p.add_argument("--no-single-frame", dest="single_frame", action="store_false",
@@ -62,49 +83,84 @@ def parse():
     return p.parse_args()
 
 
+def launch_ranks(args) -> int:
+    """--gpus N outside torch.distributed: start N ranks (this process never initialises HIP)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def host_info() -> dict:
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "nproc": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(cfg, frame: np.ndarray) -> dict | None:
     """The reference encoder itself (oracle/_ref/ref_harness, compiled from the reference sources
-    with OpenMP) timed on this host on a bounded sample: cfg-sized frames, --cpu-iters passes.
-    Falls back to the oracle restatement (kind "port") if the reference build is absent."""
-    from tests import oracle_lib as O
-
-    threads = min(16, os.cpu_count() or 1)
+    with OpenMP) timed on this host on a bounded sample, OMP_NUM_THREADS = nproc: time4 runs the
+    reference's ImageEncoder::process, time8 the same loop over its Block<8>.  Falls back to the
+    oracle restatement (kind "port") only if the reference build is absent."""
+    info = host_info()
+    threads = info["nproc"]
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    w, h = cfg["w"], cfg["h"]
+    w, h, n = cfg["w"], cfg["h"], cfg["n"]
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness_huff" if cfg["huffman"] else "ref_harness")
     iters = ARGS.cpu_iters
-    if cfg["n"] == 4 and os.path.exists(harness):
+    why = "oracle/_ref not built"
+    if os.path.exists(harness) and not (n == 8 and cfg["huffman"]):
         with tempfile.TemporaryDirectory() as d:
             raw = os.path.join(d, "in.raw")
             frame.tofile(raw)
             # the reference opens the matrix with std::fstream(in|out): it needs a writable copy
             mat = os.path.join(d, cfg["matrix"])
-            shutil.copyfile(os.path.join(ROOT, "tests", "golden", cfg["matrix"]), mat)
+            shutil.copyfile(os.path.join(GOLDEN, cfg["matrix"]), mat)
             os.chmod(mat, 0o644)
-            r = subprocess.run([harness, "time4", raw, str(w), str(h), "1", mat, str(iters)],
-                               env=env, capture_output=True, text=True, timeout=600)
+            mode = "time4" if n == 4 else "time8"
+            r = subprocess.run([harness, mode, raw, str(w), str(h), "1", mat, str(iters)],
+                               env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, timeout=900)
             line = [ln for ln in r.stderr.splitlines() if ln.startswith("{")]
             why = f"ref_harness rc={r.returncode}: {r.stderr.strip()[-200:]}"
             if r.returncode == 0 and line:
                 res = json.loads(line[-1])
+                what = ("ImageEncoder::process" if n == 4 else
+                        "ImageEncoder::process loop over its Block<8> (ImageEncoder.cpp:52-147)")
                 return dict(value=round(w * h / (res["mean_ms"] * 1e3), 3), unit="Mpx/s", cores=threads,
                             kind="reference",
-                            sample=f"{iters} x {w}x{h} {cfg['gen']} frame, reference ImageEncoder::process "
-                                   f"(OpenMP{', Huffman' if cfg['huffman'] else ''}) via oracle/_ref/ref_harness, "
-                                   f"{threads} threads, mean {res['mean_ms']:.1f} ms/frame")
-    if cfg["n"] != 4:
-        why = ("the reference fixes its block size at compile time (Block.hpp:13, BlockSize = 4u): an 8x8 "
-               "reference build would mean editing its sources, so the 8x8 baseline is the oracle port")
-    # port: the oracle restatement (single image encode, OpenMP transform, serial emission)
+                            sample=f"{iters} x {w}x{h} {cfg['gen']} frame, reference {what} "
+                                   f"(OpenMP{', Huffman' if cfg['huffman'] else ''}) via oracle/_ref/ref_harness "
+                                   f"{mode}, OMP_NUM_THREADS={threads}, mean {res['mean_ms']:.1f} ms/frame",
+                            host=info)
+    # port: the oracle restatement (test infrastructure, allowed in this leg only)
+    from tests import oracle_lib as O
     oracle = O.load()
-    q = O.read_matrix(cfg["matrix"], cfg["n"])
+    from imageencoder_amd import read_matrix
+    q = read_matrix(os.path.join(GOLDEN, cfg["matrix"]), n)
     t0 = time.perf_counter()
     for _ in range(iters):
-        oracle.encode_image(frame, cfg["n"], q, rle=True, huffman=cfg["huffman"])
+        oracle.encode_image(frame, n, q, rle=True, huffman=cfg["huffman"])
     dt = (time.perf_counter() - t0) / iters
     return dict(value=round(w * h / (dt * 1e6), 3), unit="Mpx/s", cores=threads, kind="port",
                 sample=f"{iters} x {w}x{h} {cfg['gen']} frame, oracle restatement, {threads} threads",
-                reference_unavailable=locals().get("why", "oracle/_ref not built"))
+                reference_unavailable=why, host=info)
 
 
 class Timer:
@@ -146,20 +202,34 @@ class Timer:
         return float(t.item()), ev0.elapsed_time(ev1) / 1e3
 
 
+def golden(name: str) -> dict:
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return {c["name"]: c for c in json.load(f)}[name]
+
+
+def md5(b: bytes) -> str:
+    return hashlib.md5(b).hexdigest()
+
+
 def main():
     global ARGS
     ARGS = args = parse()
-    cfg = WORKLOADS[args.workload]
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    wl = args.workload or ("c2" if world == 1 else "c4")
+    cfg = WORKLOADS[wl]
 
     import torch
     import torch.distributed as dist
 
-    from imageencoder_amd import MODE_EXACT, MODE_FAST, Codec, stream_bound, synth, write_header
+    from imageencoder_amd import (MODE_EXACT, MODE_FAST, Codec, read_matrix, stream_bound, synth,
+                                  write_header)
     from imageencoder_amd import dist as D
-    from tests import oracle_lib as O
 
     # IE_BENCH_BACKEND=gloo with ranks sharing the visible GPUs (local % device_count) rehearses the
     # multi-rank control flow on a box with fewer GPUs than ranks; the real run is RCCL, one GPU each
@@ -178,7 +248,7 @@ def main():
     w, h, n, B, R = cfg["w"], cfg["h"], cfg["n"], cfg["batch"], cfg["resident"]
     B = args.batch or B
     R = max(args.resident or R, B)
-    q = O.read_matrix(cfg["matrix"], n)
+    q = read_matrix(os.path.join(GOLDEN, cfg["matrix"]), n)
     codec = Codec(local, q, n)
     # a dedicated stream: the encoder's launches and the timing events share it (the default
     # stream's handle is NULL, which ie_set_stream reads as "the context's own stream")
@@ -187,20 +257,23 @@ def main():
     codec.set_stream(stream.cuda_stream)
     mode = MODE_EXACT if args.mode == "exact" else MODE_FAST
     timer = Timer(torch, dist, dev, stream, world)
-
-    # resident synthetic frames, distinct per rank (seed offset), generated on the host once
-    seed = synth.DEFAULT_SEED + 1000 * rank
-    frames = torch.empty((R, h, w), dtype=torch.uint8, device=dev)
-    for i in range(R):
-        frames[i].copy_(torch.from_numpy(synth.frame(cfg["gen"], w, h, seed + i)))
-    nslots = R // B
     extra = {}
+    check = {}
 
-    if args.workload in ("c2", "c3", "c5"):
-        hdr_bits = write_header(n, q, True, w, h, huffman=cfg["huffman"])[1]
+    if wl in ("c2", "c3", "c5"):
+        # resident synthetic frames, distinct per rank (seed offset), generated on the device;
+        # rank 0's frame 0 is the golden synU4k frame (seed DEFAULT_SEED)
+        seed = synth.DEFAULT_SEED + 1000 * rank
+        frames = synth.uniform_device(w, h, R, seed, dev, torch)
+        nslots = R // B
+        hdr, hdr_bits = write_header(n, q, True, w, h, huffman=cfg["huffman"])
         pitch = (stream_bound(w, h, n, 1, hdr_bits) + 255) // 256 * 256
-        # two output buffers in turn (the pipelined Huffman step needs both; see step below)
+        # two output buffers in turn (the pipelined Huffman step needs both); every image's region
+        # starts with its settings header (the encoder keeps the bits before start_bit)
         outs = [torch.zeros(pitch * B, dtype=torch.uint8, device=dev) for _ in range(2)]
+        hdr_t = torch.from_numpy(hdr).to(dev)
+        for o in outs:
+            o.view(B, pitch)[:, : hdr.size].copy_(hdr_t)
         # sizes for the algorithmic byte count (deterministic per frame)
         ends_per_slot = []
         for slot in range(nslots):
@@ -215,13 +288,14 @@ def main():
                 slot = i % nslots
                 codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, outs[i % len(outs)], out_pitch=pitch,
                                     nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False)
+            drain = None
         else:
             hpitch = 2 * pitch  # >= 32-bit codes x payload bytes
             houts = torch.zeros(hpitch * B, dtype=torch.uint8, device=dev)
             hsizes = []
             pending = []  # the batch whose trees + pack are still to do: (output buffer, slot)
 
-            def finish():
+            def drain():
                 if pending:
                     out, hslot = pending.pop()
                     hsizes[:] = codec.huffman_finish_after_encode(out, pitch, B, hslot, houts, hpitch)
@@ -229,19 +303,19 @@ def main():
             def step(i):
                 # a batch's Huffman pass: the byte counts (from the encoder), the first positions
                 # (lengths from the encoder's end bits on the device), host tree builds, one pack
-                # launch.  Pipelined: batch i's encode
-                # and histogram are issued before batch i-1's trees, so the host builds those
-                # while the device encodes (two output buffers alternate, so batch i never
-                # overwrites the bytes batch i-1's pack still reads)
+                # launch.  Pipelined: batch i's encode and histogram are issued before batch i-1's
+                # trees, so the host builds those while the device encodes (two output buffers
+                # alternate, so batch i never overwrites the bytes batch i-1's pack still reads)
                 slot = i % nslots
                 out = outs[i % len(outs)]
                 # the encoder also counts the bytes it stores (the histogram of the Huffman pass)
                 codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, out, out_pitch=pitch,
                                     nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False, count_bytes=True)
                 codec.huffman_begin_after_encode(out, pitch, B, i % 2)
-                finish()
+                drain()
                 pending.append((out, i % 2))
-        wall, gpu_s = timer.run(step, args.warmup, args.steps, drain=finish if cfg["huffman"] else None)
+        wall, gpu_s = timer.run(step, args.warmup, args.steps, drain=drain)
+        codec.sync()  # raises if any asynchronous launch of the timed region timed out
         px_total = world * args.steps * B * w * h
         in_bytes_per_launch = B * w * h
         # dominant kernel alone: the block encoder's launch time on its stream
@@ -264,6 +338,20 @@ def main():
             _, g1 = timer.run(single, 2, 4 * B)
             extra["single_frame"] = {"us_per_frame": round(g1 / (4 * B) * 1e6, 2),
                                      "Mpx_s": round(w * h / (g1 / (4 * B)) / 1e6, 1)}
+        codec.sync()
+        if not args.no_check and rank == 0:
+            # image 0 of slot 0 is the reference's golden 4K frame: its file md5
+            g = golden(cfg["golden"])
+            out = outs[0]
+            ends = codec.encode_images(frames[:B], w, h, out, out_pitch=pitch, nframes=B, start_bit=hdr_bits,
+                                       mode=mode)
+            if cfg["huffman"]:
+                sizes = codec.huffman_encode_after_encode(out, pitch, B, houts, hpitch)
+                got = houts[: sizes[0]].cpu().numpy().tobytes()
+            else:
+                got = out[: (int(ends[0]) + 7) // 8].cpu().numpy().tobytes()
+            check = {"golden": cfg["golden"], "md5": md5(got), "expected_md5": g["md5"],
+                     "bit_exact": md5(got) == g["md5"] and len(got) == g["size"]}
         if not cfg["huffman"] and not args.no_e2e:
             # end to end from HOST buffers (reported separately, never `value`): pageable
             # numpy frames in, the library stages them over PCIe, encodes, copies the streams back
@@ -294,65 +382,95 @@ def main():
             torch.cuda.synchronize(dev)
             td = (time.perf_counter() - t0) / kd
             extra["decode_one_image"] = {"us": round(td * 1e6, 1), "Mpx_s": round(w * h / td / 1e6, 1)}
-        workload = (f"{args.workload}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
+        workload = (f"{wl}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
                     f"{' +Huffman' if cfg['huffman'] else ''}, batch of {B} independent images per step, "
                     f"{R} distinct resident frames per GPU ({R * w * h / 2**20:.0f} MiB)")
         parallelism = f"independent images sharded x{world} (no collective)"
+        cpu_frame = frames[0].cpu().numpy() if rank == 0 else None
     else:  # c4: one gop=1 video stream, frames sharded over ranks, RCCL gather to rank 0
-        F = B * world
-        f0, f1 = D.frame_range(F, rank, world)
-        nloc = f1 - f0
+        K = cfg["chunks"]
+        m = max(B // K, 1)  # frames per rank per chunk
+        nloc = m * K
+        F = nloc * world
+        nsets = max(R // nloc, 1)  # distinct resident batches per rank
+        # resident frames: set p, global frame g of the batch -> seed DEFAULT_SEED + p*F + g
+        frames = torch.empty((nsets, nloc, h, w), dtype=torch.uint8, device=dev)
+        for p in range(nsets):
+            for k in range(K):
+                fr = D.chunk_frames(k, rank, world, F, K)
+                frames[p, k * m:(k + 1) * m].copy_(
+                    synth.uniform_device(w, h, m, synth.DEFAULT_SEED + p * F + fr.start, dev, torch))
         hdr, hb = write_header(n, q, True, w, h, video=True, frames=F, gop=1, merange=16)
         root_cap = stream_bound(w, h, n, F, hb) + 64
-        out_root = torch.zeros(root_cap if rank == 0 else 8, dtype=torch.uint8, device=dev)
-        if rank == 0:
-            out_root[:hdr.size].copy_(torch.from_numpy(hdr))
-        seg_cap = stream_bound(w, h, n, max(nloc, 1), 0) + 64
-        seg = torch.zeros(seg_cap, dtype=torch.uint8, device=dev)
-        shifted = torch.zeros(seg_cap + 8, dtype=torch.uint8, device=dev)
+        seg_cap = stream_bound(w, h, n, m, 0) + 64
+        comm = torch.cuda.Stream(dev)
+        shifter = Codec(local, q, n)  # its own context: the bit copies run beside the encodes
+        shifter.set_stream(comm.cuda_stream)
+        gloo = world > 1 and dist.get_backend() == "gloo"
 
-        def shift(src, nbytes, start):
-            shifted[:8].zero_()
-            codec.bitcopy(src[:nbytes], shifted, start)
-            return shifted
+        def encode(k, i, seg, bits):
+            codec.encode_frames(frames[i % nsets, k * m:(k + 1) * m], w, h, seg, start_bit=0, nframes=m,
+                                mode=mode, want_sizes=False)
+            codec.end_bits_into(bits)
 
-        def new_bytes(k):
-            return torch.zeros(k, dtype=torch.uint8, device=dev)
+        def shift(src, nbytes, start, dst):
+            shifter.bitcopy(src[:nbytes], dst, start)
 
-        stats = {}
-
-        def encode_local(i, sizes=True):
-            slot = (i * nloc) % max(R - nloc + 1, 1)
-            y = frames[slot:slot + nloc]
-            dst, sb = (out_root, hb) if rank == 0 else (seg, 0)
-            r = codec.encode_frames(y, w, h, dst, start_bit=sb, nframes=nloc, mode=mode, want_sizes=sizes)
-            if not sizes:
-                return None, None
-            return (None if rank == 0 else seg), r[1] - sb
-
-        def step(i):
-            if world == 1:  # the stream is complete after the launch: no host round trip per step
-                encode_local(i, sizes=False)
-                return
-            sg, bits = encode_local(i)
-            stats["total_bits"] = D.gather_stream(dist, rank, world, sg, bits, hb, out_root, shift, new_bytes)
-
-        wall, gpu_s = timer.run(step, args.warmup, args.steps)
-        if world == 1:
-            stats["total_bits"] = hb + encode_local(0)[1]
-        # the encoder launch alone (asynchronous: no size read-back between launches)
-        wall_enc, gpu_enc = timer.run(lambda i: encode_local(i, sizes=False), 1, args.steps)
+        G = D.PipelinedGather(dist, rank, world, F, K, hdr, hb, seg_cap, root_cap, encode, shift, dev,
+                              comm_dev="cpu" if gloo else None, enc_stream=stream, comm_stream=comm)
+        wall, _ = timer.run(G.step, args.warmup, args.steps)
+        codec.sync()
+        shifter.sync()
+        total_bits = G.total
+        # the encoder launches alone (no gather): the dominant kernel's time
+        def enc_only(i):
+            for k in range(K):
+                codec.encode_frames(frames[i % nsets, k * m:(k + 1) * m], w, h, G.segs[k], start_bit=0, nframes=m,
+                                    mode=mode, want_sizes=False)
+        wall_enc, gpu_enc = timer.run(enc_only, 1, args.steps)
+        codec.sync()
         px_total = world * args.steps * nloc * w * h
         extra["encode_only_Mpx_s"] = round(px_total / wall_enc / 1e6, 2)
-        extra["stream_bytes"] = (stats["total_bits"] + 7) // 8
-        in_bytes_per_launch = nloc * w * h
-        out_bytes_per_launch = extra["stream_bytes"] / world
-        enc_s = gpu_enc / args.steps
+        extra["stream_bytes"] = (total_bits + 7) // 8
+        extra["world_size_backend"] = {"world": dist.get_world_size() if world > 1 else 1,
+                                       "backend": dist.get_backend() if world > 1 else None}
+        in_bytes_per_launch = m * w * h
+        out_bytes_per_launch = extra["stream_bytes"] / (world * K)
+        enc_s = gpu_enc / (args.steps * K)
         fallbacks = codec.last_fallbacks()
+        if not args.no_check:
+            ok = True
+            if world > 1:
+                # the assembled stream of the last step vs ONE device encoding the same F frames
+                last = (args.warmup + args.steps - 1) % nsets
+                G.step(last)
+                torch.cuda.synchronize(dev)
+                if rank == 0:
+                    allf = synth.uniform_device(w, h, F, synth.DEFAULT_SEED + last * F, dev, torch)
+                    ref = torch.zeros(root_cap, dtype=torch.uint8, device=dev)
+                    ref[: hdr.size].copy_(torch.from_numpy(hdr).to(dev))
+                    _, end = codec.encode_frames(allf, w, h, ref, start_bit=hb, nframes=F, mode=mode)
+                    nbytes = (end + 7) // 8
+                    ok = end == G.total and torch.equal(ref[:nbytes], G.out[:nbytes])
+                    check["gathered_equals_single_gpu"] = bool(ok)
+                    del allf, ref
+            if rank == 0:
+                # the golden gop=1 stream (3 x 1080p YUV420 frames) through the same encoder
+                g = golden(cfg["golden"])
+                gy = torch.from_numpy(synth.frames("U", w, h, 3, seed=g["input"]["seed"])).to(dev)
+                ghdr, ghb = write_header(n, q, True, w, h, video=True, frames=3, gop=1, merange=16)
+                gout = torch.zeros(stream_bound(w, h, n, 3, ghb) + 64, dtype=torch.uint8, device=dev)
+                gout[: ghdr.size].copy_(torch.from_numpy(ghdr).to(dev))
+                _, gend = codec.encode_frames(gy, w, h, gout, start_bit=ghb, nframes=3, mode=mode)
+                got = gout[: (gend + 7) // 8].cpu().numpy().tobytes()
+                check.update({"golden": cfg["golden"], "md5": md5(got), "expected_md5": g["md5"]})
+                check["bit_exact"] = bool(ok and md5(got) == g["md5"])
         B = nloc
-        workload = (f"c4: {F} x {w}x{h} gop=1 video ({nloc} frames per GPU), {n}x{n} {cfg['matrix']} RLE, "
-                    f"ONE stream assembled on rank 0 (all_gather of sizes + bit re-shift + P2P gather)")
-        parallelism = f"frame-sharded x{world} + RCCL gather"
+        workload = (f"c4: {F} x {w}x{h} gop=1 video ({nloc} frames per GPU in {K} pipelined sub-batches of {m}), "
+                    f"{n}x{n} {cfg['matrix']} RLE, ONE stream assembled on rank 0 (all_gather of sizes + bit "
+                    f"re-shift + P2P gather, overlapped with the next sub-batch's encode)")
+        parallelism = f"frame-sharded x{world} + RCCL gather" if world > 1 else "one GPU (no collective)"
+        cpu_frame = frames[0, 0].cpu().numpy() if rank == 0 else None
 
     value = px_total / wall / 1e6
     alg_bytes = in_bytes_per_launch + out_bytes_per_launch
@@ -360,15 +478,15 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(cfg, synth.frame(cfg["gen"], w, h, seed))
+        cpu = cpu_baseline(cfg, cpu_frame)
 
     if rank == 0:
         traffic = None
-        tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
+        tf = os.path.join(ROOT, "profiles", f"traffic_{wl}.json")
         if os.path.exists(tf):
             traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
         line = {
-            "metric": "Mpixels/s encode (DCT+quant+RLE), 4K grayscale, 1/2/4/8 GPU + CPU ref",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "Mpx/s",
             "n_gpus": world,
@@ -378,7 +496,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "u8->int16 (FP32 DCT + FP64 near-tie fix-up)" if mode == MODE_FAST else "u8->int16 (FP64 DCT)",
             "data": "synthetic (splitmix64 uniform 8-bit frames, seeded per rank)",
             "config": {"workload": workload, "block": n, "frames_per_step_per_gpu": B, "mode": args.mode,
                        "parallelism": parallelism},
@@ -395,8 +513,10 @@ def main():
                 "read_only_frac": round(in_bytes_per_launch / enc_s / 1e9 / HBM_PEAK_GBS, 4),
             },
             "cpu_baseline": cpu,
+            "bit_exact": check.get("bit_exact"),
+            "check": check,
             "fallback_coefs_per_launch": fallbacks,
-            "arith": "FP32 separable DCT + FP64 re-evaluation of near-tie coefficients (bit-exact)",
+            "arith": ARITH,
         }
         line.update(extra)
         print(json.dumps(line), flush=True)

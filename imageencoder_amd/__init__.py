@@ -166,6 +166,16 @@ def write_header(n: int, q, rle: bool, w: int, h: int, huffman: bool = False, vi
     return out[: (bits + 7) // 8].copy(), int(bits)
 
 
+def read_matrix(path: str, n: int) -> np.ndarray:
+    """A quantisation matrix file: n*n whitespace-separated unsigned values, row-major
+    (dc::MatrixReader<N>::read, MatrixReader.cpp:65-134).  Raises ValueError on a malformed file."""
+    with open(path) as f:
+        vals = [int(t) for t in f.read().split()]
+    if len(vals) != n * n or any(v <= 0 or v > 0xFFFF for v in vals):
+        raise ValueError(f"{path}: expected {n * n} values in 1..65535, got {len(vals)}")
+    return np.array(vals, dtype=np.uint16)
+
+
 def stream_bound(w: int, h: int, n: int, nframes: int = 1, start_bit: int = 0) -> int:
     return int(load_library().ie_stream_bound(w, h, n, nframes, start_bit))
 
@@ -261,6 +271,12 @@ class Codec:
         self._chk(self.L.ie_quantize_frames(self.h, _ptr(y), w, h, stride, frame_pitch, nframes, mode,
                                             coef.ctypes.data))
         return coef
+
+    def end_bits_into(self, dst, count: int = 1):
+        """Stream-ordered device copy of the last encode's end bit(s) (one per chain) into the
+        device tensor ``dst`` (uint64/int64): no host read-back."""
+        src = self.L.ie_last_end_bits(self.h)
+        self._chk(self.L.ie_memcpy(self.h, C.c_void_p(_ptr(dst)), C.c_void_p(src), 8 * count))
 
     def last_fallbacks(self) -> int:
         v = C.c_uint64(0)

@@ -26,7 +26,7 @@ struct ie_ctx {
     ie::EncTables* d_tab = nullptr;
 
     // decoupled look-back state
-    uint64_t* d_state = nullptr;  // [kStateWordsPerTile * cap_tiles] tile chain granules (ie_common.cuh)
+    uint64_t* d_state = nullptr;  // [kStateWordsPerTile * cap_tiles] tile chain granules (ie_common.hpp)
     size_t cap_tiles = 0;
     uint32_t tag = 0;
     unsigned long long* d_ticket = nullptr;
@@ -40,6 +40,10 @@ struct ie_ctx {
     int last_fix_words = 0;
     unsigned err_seen[66] = {};         // counter values at the previous read
     bool use_ticket = false;            // order tiles with an atomic ticket (after a timeout)
+    // Asynchronous launches (no read-back) since the last error read: a look-back timeout found
+    // at the next read is charged to them (their output is invalid), never silently retried away.
+    unsigned async_pending = 0;
+    const char* async_what = nullptr;
 
     // staging for host-resident inputs / outputs
     uint8_t* d_in = nullptr;
@@ -57,6 +61,7 @@ struct ie_ctx {
     uint32_t* d_code = nullptr;        // [256] codes, then [256/4] packed lengths (one block)
     uint32_t* h_code = nullptr;        // pinned mirror
     uint32_t* d_hist = nullptr;        // [256]
+    uint32_t* d_ident = nullptr;       // identity code table of ie_bitcopy (built once)
     // batched Huffman: device + pinned staging (hist/first of every string, then the pack tables)
     uint8_t* d_batch = nullptr;
     size_t cap_batch = 0;
@@ -370,10 +375,30 @@ int read_errors(ie_ctx* c, unsigned* timeouts, uint64_t* fallbacks) {
         HIPCHK(c, hipMemcpy(w.data(), c->d_wave_fix, w.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
         for (uint32_t v : w) f += v;
     }
-    if (timeouts) *timeouts = e[0] - c->err_seen[0];
+    const unsigned t = e[0] - c->err_seen[0];
+    if (timeouts) *timeouts = t;
     if (fallbacks) *fallbacks = f;
     std::memcpy(c->err_seen, e, sizeof(e));
+    const unsigned pending = c->async_pending;
+    const char* what = c->async_what;
+    c->async_pending = 0;
+    c->async_what = nullptr;
+    if (t && pending) {
+        // a launch that returned without a read-back timed out: its output is invalid and there is
+        // nothing to re-run here -- fail loudly (later launches order their tiles by ticket)
+        c->use_ticket = true;
+        return fail(c, IE_EDEVICE, std::string("tile look-back timed out in an earlier asynchronous ") +
+                                       (what ? what : "launch") + " (" + std::to_string(pending) +
+                                       " unchecked launch(es)); its output is invalid");
+    }
     return IE_OK;
+}
+
+// An asynchronous launch returned without reading the error counters: the next read (ie_sync or
+// any synchronous call) checks it.
+void note_async(ie_ctx* c, const char* what) {
+    c->async_pending++;
+    c->async_what = what;
 }
 
 struct Geometry {
@@ -495,12 +520,22 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.coef = coef;
     a.hist = hist;
     if (hist) HIPCHK(c, hipMemsetAsync(hist, 0, size_t(nframes) * 256 * sizeof(uint32_t), c->stream));
-    static const int ablate = getenv("IE_ABLATE") ? atoi(getenv("IE_ABLATE")) : 0;  // profiling only
+#ifndef IE_PROFILE
+#define IE_PROFILE 0
+#endif
 #ifndef IE_ABLATE_FORCE
 #define IE_ABLATE_FORCE 0
 #endif
+    // Profiling knobs exist only in IE_PROFILE builds (tools/variants.sh): the product library
+    // never reads IE_ABLATE / IE_STAMPS, so no environment variable can change its output.
+#if IE_PROFILE
+    static const int ablate = getenv("IE_ABLATE") ? atoi(getenv("IE_ABLATE")) : 0;
+    static const char* stamp_file = getenv("IE_STAMPS");  // per-tile phase stamps
+#else
+    constexpr int ablate = 0;
+    const char* stamp_file = nullptr;
+#endif
     a.ablate = ablate | IE_ABLATE_FORCE;  // IE_ABLATE_FORCE: A/B builds of an ablation
-    static const char* stamp_file = getenv("IE_STAMPS");  // profiling only: per-tile phase stamps
     uint64_t* d_stamps = nullptr;
     if (stamp_file) {
         HIPCHK(c, hipMalloc(&d_stamps, size_t(g.ntiles) * ie::kStamps * sizeof(uint64_t)));
@@ -522,7 +557,10 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     if (c->use_ticket) c->ticket_base += uint64_t(g.ntiles);
 
     const bool want = frame_bits || end_bits || !out_dev;
-    if (!want) return IE_OK;
+    if (!want) {
+        note_async(c, hist ? "counting encode" : "encode");
+        return IE_OK;
+    }
     std::vector<uint64_t> fs(nframes), ce(nchains);
     HIPCHK(c, hipMemcpyAsync(fs.data(), c->d_frame_start, nframes * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(ce.data(), c->d_chain_end, nchains * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
@@ -556,8 +594,10 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
 }
 
 // Variable-length re-encode of n bytes (Huffman.cpp:314-319) into one stream from start_bit.
+// identity: the code is the byte itself (8 bits) -- ie_bitcopy; its device table is built once per
+// context, so a device-to-device bit copy never waits for the stream.
 int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const uint8_t* len, uint8_t* out,
-         size_t out_cap, uint64_t start_bit, uint64_t* end_bit) {
+         size_t out_cap, uint64_t start_bit, uint64_t* end_bit, bool identity = false) {
     HIPCHK(c, hipSetDevice(c->device));
     int r;
     unsigned maxlen = 0;
@@ -568,11 +608,23 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
     const uint64_t end_bound = start_bit + uint64_t(maxlen) * n;
     const size_t need_bytes = size_t((end_bound + 31) / 32) * 4;
     if (out_cap < need_bytes) return fail(c, IE_ECAP, "output capacity below start_bit + max_len * n bits");
-    // code table through pinned memory (the caller's arrays may be gone when the copy runs)
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    std::memcpy(c->h_code, code, 256 * sizeof(uint32_t));
-    std::memcpy(reinterpret_cast<uint8_t*>(c->h_code + 256), len, 256);
-    HIPCHK(c, hipMemcpyAsync(c->d_code, c->h_code, 2 * 256 * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    const uint32_t* d_code = c->d_code;
+    if (identity) {
+        if (!c->d_ident) {
+            HIPCHK(c, hipMalloc(&c->d_ident, 2 * 256 * sizeof(uint32_t)));
+            std::vector<uint32_t> t(2 * 256);
+            std::memcpy(t.data(), code, 256 * sizeof(uint32_t));
+            std::memcpy(reinterpret_cast<uint8_t*>(t.data() + 256), len, 256);
+            HIPCHK(c, hipMemcpy(c->d_ident, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
+        d_code = c->d_ident;
+    } else {
+        // code table through pinned memory (the caller's arrays may be gone when the copy runs)
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        std::memcpy(c->h_code, code, 256 * sizeof(uint32_t));
+        std::memcpy(reinterpret_cast<uint8_t*>(c->h_code + 256), len, 256);
+        HIPCHK(c, hipMemcpyAsync(c->d_code, c->h_code, 2 * 256 * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    }
     const uint8_t* din = bytes;
     if (n && !is_device_ptr(bytes)) {
         if ((r = ensure(c, c->d_in, c->cap_in, n))) return r;
@@ -601,8 +653,8 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
         ie::PackArgs a{};
         a.in = din;
         a.n = n;
-        a.code = c->d_code;
-        a.len = reinterpret_cast<const uint8_t*>(c->d_code + 256);
+        a.code = d_code;
+        a.len = reinterpret_cast<const uint8_t*>(d_code + 256);
         a.ntiles = ntiles;
         a.out = dout;
         a.start_bit = start_bit;
@@ -616,14 +668,17 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
         ie::launch_pack(a, c->stream);
         HIPCHK(c, hipGetLastError());
         if (c->use_ticket) c->ticket_base += uint64_t(ntiles);
-        if (!end_bit && out_dev) return IE_OK;
+        if (!end_bit && out_dev) {
+            note_async(c, "Huffman pack");
+            return IE_OK;
+        }
         HIPCHK(c, hipMemcpyAsync(&end, c->d_chain_end, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         unsigned timeouts = 0;
         if ((r = read_errors(c, &timeouts, nullptr))) return r;
         if (timeouts) {
             if (c->use_ticket) return fail(c, IE_EDEVICE, "tile look-back timed out");
             c->use_ticket = true;
-            return pack(c, bytes, n, code, len, out, out_cap, start_bit, end_bit);
+            return pack(c, bytes, n, code, len, out, out_cap, start_bit, end_bit, identity);
         }
     }
     if (!out_dev && end > start_bit) {
@@ -650,6 +705,9 @@ int ie_create(int device, ie_ctx** out) {
     chk(hipSetDevice(device), "hipSetDevice");
     if (r == IE_OK) chk(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking), "hipStreamCreate");
     c->stream = c->own;
+    // Debug switch: order tiles by the atomic ticket from the first launch (exercises the
+    // timeout-recovery path, which dispatch order otherwise never needs)
+    if (const char* ft = getenv("IE_FORCE_TICKET")) c->use_ticket = atoi(ft) != 0;
     if (r == IE_OK) chk(hipMalloc(&c->d_tab, sizeof(ie::EncTables)), "hipMalloc(tables)");
     if (r == IE_OK) chk(hipHostMalloc(&c->h_tab, sizeof(ie::EncTables)), "hipHostMalloc(tables)");
     if (r == IE_OK) chk(hipMalloc(&c->d_ticket, sizeof(unsigned long long)), "hipMalloc(ticket)");
@@ -679,6 +737,7 @@ int ie_destroy(ie_ctx* c) {
     (void)hipHostFree(c->h_tab);
     (void)hipFree(c->d_state);
     (void)hipFree(c->d_ticket);
+    (void)hipFree(c->d_ident);
     (void)hipFree(c->d_frame_start);
     (void)hipFree(c->d_chain_end);
     (void)hipFree(c->d_err);
@@ -723,6 +782,13 @@ int ie_set_stream(ie_ctx* c, void* s) {
 int ie_sync(ie_ctx* c) {
     if (!c) return IE_EINVAL;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    unsigned timeouts = 0;
+    int r = read_errors(c, &timeouts, nullptr);  // fails if an unchecked launch timed out
+    if (r) return r;
+    if (timeouts) {  // (no asynchronous launch pending: a synchronous caller already re-ran it)
+        c->use_ticket = true;
+        return fail(c, IE_EDEVICE, "tile look-back timed out");
+    }
     return IE_OK;
 }
 
@@ -893,8 +959,10 @@ int ie_bitcopy(ie_ctx* c, const uint8_t* bytes, size_t n, uint8_t* out, size_t o
         code[b] = uint32_t(b);
         len[b] = 8;
     }
+    // device to device: asynchronous on the context's stream (checked at the next ie_sync)
     uint64_t end = 0;
-    return pack(c, bytes, n, code, len, out, out_cap, start_bit, &end);
+    const bool async = is_device_ptr(out) && (!n || is_device_ptr(bytes));
+    return pack(c, bytes, n, code, len, out, out_cap, start_bit, async ? nullptr : &end, true);
 }
 
 int ie_huffman_hist_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,
@@ -1100,7 +1168,10 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         HIPCHK(c, hipGetLastError());
         if (c->use_ticket) c->ticket_base += ntiles;
     }
-    if (!end_bit) return IE_OK;
+    if (!end_bit) {
+        if (ntiles) note_async(c, "Huffman batch pack");
+        return IE_OK;
+    }
     std::vector<uint64_t> ends(K);
     if (ntiles) HIPCHK(c, hipMemcpyAsync(ends.data(), c->d_chain_end, 8 * K, hipMemcpyDeviceToHost, c->stream));
     unsigned timeouts = 0;

@@ -1,4 +1,4 @@
-// imageencoder_amd/csrc/ie_common.cuh -- device building blocks shared by the gfx950 kernels:
+// imageencoder_amd/csrc/ie_common.hpp -- device building blocks shared by the gfx950 kernels:
 // wave/workgroup scans, the LDS bit sink, the decoupled look-back over tile states and the
 // funnel-shift store of a tile's bit image.  Wavefront = 64 lanes, workgroup = kTPB = 256.
 #pragma once

@@ -19,7 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "ie_common.cuh"
+#include "ie_common.hpp"
 #include "ie_device.h"
 
 namespace ie {

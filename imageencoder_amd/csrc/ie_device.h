@@ -54,7 +54,7 @@ struct EncArgs {
     uint32_t* out;           // 4-byte aligned, word w = stream bytes [4w, 4w+4)
     uint64_t out_pitch_words;
     uint64_t start_bit;
-    uint64_t* st;            // [3*ntiles] tile chain granules (ie_common.cuh)
+    uint64_t* st;            // [3*ntiles] tile chain granules (ie_common.hpp)
     unsigned long long* ticket;  // nullptr: tiles in blockIdx order; else an atomic ticket
     unsigned long long ticket_base;
     uint32_t tag;            // epoch tag 1..255
@@ -74,7 +74,7 @@ struct EncArgs {
 };
 
 constexpr int kStamps = 16;
-// chain-state words per tile (the host allocates; ie_common.cuh kGran must not exceed it)
+// chain-state words per tile (the host allocates; ie_common.hpp kGran must not exceed it)
 constexpr int kStateWordsPerTile = 16;
 void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s);
 int encode_blocks_per_thread(int n);  // horizontally adjacent blocks per lane (Geo<N>::BPT)

@@ -70,3 +70,32 @@ def yuv420(y: np.ndarray, fill: int = 0x80) -> bytes:
     buf = np.full((count, h * w + h * w // 2), fill, dtype=np.uint8)
     buf[:, : h * w] = y.reshape(count, h * w)
     return buf.tobytes()
+
+
+def _u64(v: int) -> int:
+    """A 64-bit constant as the signed int64 torch stores (two's complement)."""
+    v &= 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >> 63 else v
+
+
+def uniform_device(w: int, h: int, count: int, seed: int, device, torch=None):
+    """``frames("U", w, h, count, seed)`` generated on a torch device: the same splitmix64 bytes
+    (int64 arithmetic wraps like uint64; right shifts are masked to be logical).  Bench and test
+    data only -- the generator, not the product."""
+    if torch is None:
+        import torch
+    out = torch.empty((count, h, w), dtype=torch.uint8, device=device)
+    n = w * h
+    i = torch.arange(1, n + 1, dtype=torch.int64, device=device)
+    g, m1, m2 = _u64(0x9E3779B97F4A7C15), _u64(0xBF58476D1CE4E5B9), _u64(0x94D049BB133111EB)
+
+    def srl(z, k):
+        return (z >> k) & ((1 << (64 - k)) - 1)
+
+    for f in range(count):
+        z = i * g + _u64(seed + f)
+        z = (z ^ srl(z, 30)) * m1
+        z = (z ^ srl(z, 27)) * m2
+        z = z ^ srl(z, 31)
+        out[f].view(-1).copy_((z & 0xFF).to(torch.uint8))
+    return out

@@ -60,6 +60,10 @@ const char* ie_last_error(const ie_ctx* ctx);
 /* Run on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores
  * the context's own stream. */
 int ie_set_stream(ie_ctx* ctx, void* hip_stream);
+/* Wait for the context's stream, then check the device error counters: IE_EDEVICE if a tile
+ * look-back timed out in any launch that returned without a read-back (asynchronous encodes,
+ * packs, bit copies) since the last check -- that launch's output is invalid.  Later launches
+ * then order their tiles by an atomic ticket.  Call it after a pipeline of asynchronous calls. */
 int ie_sync(ie_ctx* ctx);
 
 /* Quantisation matrix, n x n row-major uint16 (MatrixReader<N>::read, MatrixReader.cpp:65-134;
@@ -171,7 +175,8 @@ int ie_huffman_pack_batch(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const
                           uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit);
 
 /* Copy n bytes into out starting at bit start_bit, i.e. shifted by start_bit % 8 (the "no gain"
- * path of Huffman.cpp:329-341 writes '0' + the input: start_bit = 1). */
+ * path of Huffman.cpp:329-341 writes '0' + the input: start_bit = 1).  Device input and output:
+ * asynchronous on the context's stream, like an encode without sizes (checked at ie_sync). */
 int ie_bitcopy(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint8_t* out, size_t out_cap, uint64_t start_bit);
 
 /* Huffman decode on the device (algo::Huffman<uint8_t>::decode, Huffman.cpp:354-402, replacing the

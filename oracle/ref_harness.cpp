@@ -14,11 +14,18 @@
 //      in the Huffman build, the Huffman pass) -- i.e. the hot path, without the file IO that
 //      main.cpp:68,111 folds into its "Elapsed time".  The object is deliberately leaked: the
 //      reference destructor frees an uninitialised pointer (ImageBase.cpp:78-88,161-165).
+//      `time8` times the same work for 8x8 blocks: dc::ImageEncoder is hard-wired to Block<>
+//      (BlockSize = 4), so it runs the body of ImageEncoder::process (ImageEncoder.cpp:52-147)
+//      statement for statement over the unmodified dc::Block<8>: block creation as
+//      ImageProcessor::process (ImageBase.cpp:175-206), the header, the OpenMP
+//      `parallel for schedule(dynamic)` over processDCTDivQ + createRLESequence with its atomic
+//      counter and critical progress call (:121-132), then the serial streamEncoded loop (:135-138).
 //
 // Usage (all files raw bytes):
 //   ref_harness enc8  <raw> <w> <h> <rle> <matrix8.txt> <out> [huff]
 //   ref_harness dec8  <enc> <out>
 //   ref_harness time4 <raw> <w> <h> <rle> <matrix.txt> <iters> [out]
+//   ref_harness time8 <raw> <w> <h> <rle> <matrix8.txt> <iters> [out]
 //   ref_harness cos   <n>                      (prints the reference cos-product inputs as hex)
 #include "Block.cpp"
 #include "MatrixReader.cpp"
@@ -160,6 +167,74 @@ static int time4(int argc, char** argv) {
     return 0;
 }
 
+// ImageEncoder::process (ImageEncoder.cpp:52-147) for Block<8>; see the header comment.
+static double encode8_once(const std::vector<uint8_t>& raw, uint16_t w, uint16_t h, bool rle,
+                           dc::MatrixReader<8>& m, std::vector<uint8_t>* out) {
+    auto t0 = std::chrono::steady_clock::now();
+    // ImageProcessor::process (ImageBase.cpp:175-206): one heap Block per 8x8 block
+    std::vector<dc::Block<8>*>* blocks = new std::vector<dc::Block<8>*>();
+    const size_t bx = w / 8, by = h / 8;
+    uint8_t* rows[8];
+    uint8_t* buf = const_cast<uint8_t*>(raw.data());
+    for (size_t y = 0; y < by; y++)
+        for (size_t x = 0; x < bx; x++) {
+            for (size_t r = 0; r < 8; r++) rows[r] = buf + y * 64 * bx + x * 8 + r * w;
+            blocks->push_back(new dc::Block<8>(rows));
+        }
+    size_t output_length = 1 + 30 + 5 + size_t(m.getMaxBitLength()) * 64;
+    output_length += blocks->size() * blocks->front()->streamSize();
+    output_length++;
+    output_length = util::round_to_byte(output_length);
+    util::BitStreamWriter* wr = new util::BitStreamWriter(output_length);
+    wr->put_bit(0);
+    m.write(*wr);
+    wr->put(1, uint32_t(rle));
+    wr->put(15, w);
+    wr->put(15, h);
+    const size_t block_count = blocks->size();
+    size_t blockid = 0u;
+    util::Logger::WriteProgress(0, block_count);
+    #pragma omp parallel for shared(blockid) schedule(dynamic)
+    for (auto it = blocks->begin(); it < blocks->end(); it++) {
+        dc::Block<8>* b = *it;
+        b->processDCTDivQ(m.getData());
+        b->createRLESequence();
+        #pragma omp atomic
+        ++blockid;
+        #pragma omp critical
+        util::Logger::WriteProgress(blockid, block_count);
+    }
+    for (dc::Block<8>* b : *blocks) b->streamEncoded(*wr, rle);
+    auto t1 = std::chrono::steady_clock::now();
+    if (out) out->assign(wr->get_buffer(), wr->get_buffer() + wr->get_last_byte_position());
+    // (blocks and writer leaked like the reference's own objects in time4)
+    return std::chrono::duration<double, std::milli>(t1 - t0).count();
+}
+
+static int time8(int argc, char** argv) {
+    if (argc < 8) return 1;
+    std::vector<uint8_t> raw = read_file(argv[2]);
+    const uint16_t w = uint16_t(std::atoi(argv[3])), h = uint16_t(std::atoi(argv[4]));
+    const bool rle = std::atoi(argv[5]) != 0;
+    const int iters = std::atoi(argv[7]);
+    dc::MatrixReader<8> m;
+    if (!m.read(argv[6])) return 4;
+    if (raw.size() != size_t(w) * h || w % 8 || h % 8) return 3;
+    util::Logger::Create("");
+    dc::Block<8>::CreateZigZagLUT();
+    double best = 1e30, total = 0;
+    std::vector<uint8_t> out;
+    for (int it = 0; it < iters; it++) {
+        const double ms = encode8_once(raw, w, h, rle, m, (it == iters - 1 && argc > 8) ? &out : nullptr);
+        best = ms < best ? ms : best;
+        total += ms;
+    }
+    if (argc > 8) write_file(argv[8], out.data(), out.size());
+    std::fprintf(stderr, "{\"iters\": %d, \"best_ms\": %.3f, \"mean_ms\": %.3f, \"px\": %zu}\n",
+                 iters, best, total / iters, size_t(w) * h);
+    return 0;
+}
+
 // The cos table the reference evaluates inside transformDCT (algo.cpp:312,318-319), printed
 // as exact hex doubles so the repo can pin its own host table against it.
 static int costab(int argc, char** argv) {
@@ -177,6 +252,7 @@ int main(int argc, char** argv) {
     if (mode == "enc8") return enc8(argc, argv);
     if (mode == "dec8") return dec8(argc, argv);
     if (mode == "time4") return time4(argc, argv);
+    if (mode == "time8") return time8(argc, argv);
     if (mode == "cos") return costab(argc, argv);
     return 1;
 }

@@ -107,3 +107,77 @@ def test_numpy_shift(start):
     bits = np.unpackbits(out)
     assert not bits[:start].any()
     assert np.array_equal(bits[start:start + 37 * 8], np.unpackbits(src))
+
+
+def _pipe_worker(rank, world, port, w, h, F, nchunks, gen, steps, result_q):
+    """PipelinedGather on CPU/gloo: round-robin chunks, the oracle as each rank's encoder."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 4
+        q = O.read_matrix("matrix.txt", n)
+        oracle = O.load()
+        hdr, hb = write_header(n, q, True, w, h, video=True, frames=F, gop=1, merange=16)
+        cap = (hb + 7) // 8 + F * (w * h * 17 // 8 + w * h // (n * n)) + 64
+        seg_cap = F * (w * h * 17 // 8 + w * h // (n * n)) + 64
+
+        def frames_for(k, step):  # each step encodes a different batch (seed offset)
+            fr = D.chunk_frames(k, rank, world, F, nchunks)
+            return synth.frames(gen, w, h, F, seed=77 + step)[fr.start:fr.stop]
+
+        def encode(k, step, seg, bits):
+            y = frames_for(k, step)
+            seg.zero_()
+            if len(y) == 0:
+                bits.fill_(0)
+                return
+            buf, end, _ = oracle.encode_blocks(y, n, q, rle=True, start_bit=0)
+            seg[: buf.size].copy_(torch.from_numpy(buf))
+            bits.fill_(end)
+
+        def shift(src, nbytes, start, dst):
+            v = torch.from_numpy(D.numpy_shift(src.numpy(), nbytes, start))
+            dst[: v.numel()].copy_(v)
+
+        g = D.PipelinedGather(dist, rank, world, F, nchunks, hdr, hb, seg_cap, cap, encode, shift, "cpu")
+        outs = []
+        for step in range(steps):
+            g.step(step)
+            if rank == 0:
+                outs.append((g.total, g.out[: (g.total + 7) // 8].numpy().tobytes()))
+        if rank == 0:
+            result_q.put(outs)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,F,nchunks,gen", [(2, 8, 2, "U"), (3, 9, 3, "M"), (2, 5, 2, "M"), (3, 2, 1, "U")])
+def test_pipelined_gather_matches_reference(world, F, nchunks, gen):
+    """Round-robin chunks assembled by PipelinedGather equal the single-process gop=1 stream of
+    the same frames in global order, for two consecutive steps over different frames (the root
+    buffer is reused: stale bytes must not leak into the next stream)."""
+    w, h, steps = 64, 48, 2
+    ctx = mp.get_context("spawn")
+    qres = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, w, h, F, nchunks, gen, steps, qres))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = qres.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    q = O.read_matrix("matrix.txt", 4)
+    for step, (total, got) in enumerate(outs):
+        ys = synth.frames(gen, w, h, F, seed=77 + step)
+        ref = O.load().encode_video(synth.yuv420(ys), w, h, 4, q, rle=True, huffman=False, merange=16)
+        assert got == ref, f"step {step}"
+        assert (total + 7) // 8 == len(ref)
+
+
+def test_chunk_frames_round_robin():
+    got = [list(D.chunk_frames(k, r, 3, 12, 2)) for k in range(2) for r in range(3)]
+    assert got == [[0, 1], [2, 3], [4, 5], [6, 7], [8, 9], [10, 11]]
+    got = [list(D.chunk_frames(k, r, 2, 5, 2)) for k in range(2) for r in range(2)]
+    assert sum(got, []) == list(range(5))
