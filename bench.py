@@ -116,11 +116,14 @@ def host_info() -> dict:
 
 def cpu_baseline(cfg, frame: np.ndarray) -> dict | None:
     """The reference encoder itself (oracle/_ref/ref_harness, compiled from the reference sources
-    with OpenMP) timed on this host on a bounded sample, OMP_NUM_THREADS = nproc: time4 runs the
+    with OpenMP) timed on this host on a bounded sample, OMP_NUM_THREADS = the CPUs this process
+    may use (nproc, or the cgroup quota when lower): time4 runs the
     reference's ImageEncoder::process, time8 the same loop over its Block<8>.  Falls back to the
     oracle restatement (kind "port") only if the reference build is absent."""
     info = host_info()
-    threads = info["nproc"]
+    # every CPU this process may use: nproc, bounded by the cgroup's CPU quota where one is set
+    # (the GPU box: nproc 256, quota 16 -- 256 OpenMP threads on 16 CPUs measured 8x slower)
+    threads = min(info["nproc"], int(info["cgroup_cpu_quota"])) if info["cgroup_cpu_quota"] else info["nproc"]
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     w, h, n = cfg["w"], cfg["h"], cfg["n"]
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness_huff" if cfg["huffman"] else "ref_harness")
@@ -236,6 +239,9 @@ def main():
     backend = os.environ.get("IE_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(torch.cuda.device_count(), 1)
+        # ranks share a GPU: concurrent look-back kernels of different processes could hold each
+        # other's predecessor tiles off the CUs -- order tiles by atomic ticket (deadlock-free)
+        os.environ["IE_FORCE_TICKET"] = "1"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
@@ -416,16 +422,26 @@ def main():
         def shift(src, nbytes, start, dst):
             shifter.bitcopy(src[:nbytes], dst, start)
 
-        G = D.PipelinedGather(dist, rank, world, F, K, hdr, hb, seg_cap, root_cap, encode, shift, dev,
-                              comm_dev="cpu" if gloo else None, enc_stream=stream, comm_stream=comm)
-        wall, _ = timer.run(G.step, args.warmup, args.steps)
+        if world > 1:
+            G = D.PipelinedGather(dist, rank, world, F, K, hdr, hb, seg_cap, root_cap, encode, shift, dev,
+                                  comm_dev="cpu" if gloo else None, enc_stream=stream, comm_stream=comm)
+            wall, _ = timer.run(G.step, args.warmup, args.steps)
+            total_bits = G.total
+            segs = G.segs
+        else:  # one GPU: the whole batch in one launch straight after the header (nothing to gather)
+            out_root = torch.zeros(root_cap, dtype=torch.uint8, device=dev)
+            out_root[: hdr.size].copy_(torch.from_numpy(hdr).to(dev))
+            segs = [torch.zeros(seg_cap, dtype=torch.uint8, device=dev) for _ in range(K)]
+            wall, _ = timer.run(lambda i: codec.encode_frames(frames[i % nsets].view(nloc, h, w), w, h, out_root,
+                                                              start_bit=hb, nframes=nloc, mode=mode,
+                                                              want_sizes=False), args.warmup, args.steps)
+            total_bits = codec.encode_frames(frames[0], w, h, out_root, start_bit=hb, nframes=nloc, mode=mode)[1]
         codec.sync()
         shifter.sync()
-        total_bits = G.total
         # the encoder launches alone (no gather): the dominant kernel's time
         def enc_only(i):
             for k in range(K):
-                codec.encode_frames(frames[i % nsets, k * m:(k + 1) * m], w, h, G.segs[k], start_bit=0, nframes=m,
+                codec.encode_frames(frames[i % nsets, k * m:(k + 1) * m], w, h, segs[k], start_bit=0, nframes=m,
                                     mode=mode, want_sizes=False)
         wall_enc, gpu_enc = timer.run(enc_only, 1, args.steps)
         codec.sync()
@@ -469,7 +485,8 @@ def main():
         workload = (f"c4: {F} x {w}x{h} gop=1 video ({nloc} frames per GPU in {K} pipelined sub-batches of {m}), "
                     f"{n}x{n} {cfg['matrix']} RLE, ONE stream assembled on rank 0 (all_gather of sizes + bit "
                     f"re-shift + P2P gather, overlapped with the next sub-batch's encode)")
-        parallelism = f"frame-sharded x{world} + RCCL gather" if world > 1 else "one GPU (no collective)"
+        parallelism = (f"frame-sharded x{world} + {'RCCL' if not gloo else 'gloo (rehearsal)'} gather" if world > 1
+                       else "one GPU, whole batch in one launch (no collective)")
         cpu_frame = frames[0, 0].cpu().numpy() if rank == 0 else None
 
     value = px_total / wall / 1e6

@@ -61,7 +61,6 @@ struct ie_ctx {
     uint32_t* d_code = nullptr;        // [256] codes, then [256/4] packed lengths (one block)
     uint32_t* h_code = nullptr;        // pinned mirror
     uint32_t* d_hist = nullptr;        // [256]
-    uint32_t* d_ident = nullptr;       // identity code table of ie_bitcopy (built once)
     // batched Huffman: device + pinned staging (hist/first of every string, then the pack tables)
     uint8_t* d_batch = nullptr;
     size_t cap_batch = 0;
@@ -594,10 +593,8 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
 }
 
 // Variable-length re-encode of n bytes (Huffman.cpp:314-319) into one stream from start_bit.
-// identity: the code is the byte itself (8 bits) -- ie_bitcopy; its device table is built once per
-// context, so a device-to-device bit copy never waits for the stream.
 int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const uint8_t* len, uint8_t* out,
-         size_t out_cap, uint64_t start_bit, uint64_t* end_bit, bool identity = false) {
+         size_t out_cap, uint64_t start_bit, uint64_t* end_bit) {
     HIPCHK(c, hipSetDevice(c->device));
     int r;
     unsigned maxlen = 0;
@@ -608,23 +605,11 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
     const uint64_t end_bound = start_bit + uint64_t(maxlen) * n;
     const size_t need_bytes = size_t((end_bound + 31) / 32) * 4;
     if (out_cap < need_bytes) return fail(c, IE_ECAP, "output capacity below start_bit + max_len * n bits");
-    const uint32_t* d_code = c->d_code;
-    if (identity) {
-        if (!c->d_ident) {
-            HIPCHK(c, hipMalloc(&c->d_ident, 2 * 256 * sizeof(uint32_t)));
-            std::vector<uint32_t> t(2 * 256);
-            std::memcpy(t.data(), code, 256 * sizeof(uint32_t));
-            std::memcpy(reinterpret_cast<uint8_t*>(t.data() + 256), len, 256);
-            HIPCHK(c, hipMemcpy(c->d_ident, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        }
-        d_code = c->d_ident;
-    } else {
-        // code table through pinned memory (the caller's arrays may be gone when the copy runs)
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        std::memcpy(c->h_code, code, 256 * sizeof(uint32_t));
-        std::memcpy(reinterpret_cast<uint8_t*>(c->h_code + 256), len, 256);
-        HIPCHK(c, hipMemcpyAsync(c->d_code, c->h_code, 2 * 256 * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    }
+    // code table through pinned memory (the caller's arrays may be gone when the copy runs)
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::memcpy(c->h_code, code, 256 * sizeof(uint32_t));
+    std::memcpy(reinterpret_cast<uint8_t*>(c->h_code + 256), len, 256);
+    HIPCHK(c, hipMemcpyAsync(c->d_code, c->h_code, 2 * 256 * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     const uint8_t* din = bytes;
     if (n && !is_device_ptr(bytes)) {
         if ((r = ensure(c, c->d_in, c->cap_in, n))) return r;
@@ -653,8 +638,8 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
         ie::PackArgs a{};
         a.in = din;
         a.n = n;
-        a.code = d_code;
-        a.len = reinterpret_cast<const uint8_t*>(d_code + 256);
+        a.code = c->d_code;
+        a.len = reinterpret_cast<const uint8_t*>(c->d_code + 256);
         a.ntiles = ntiles;
         a.out = dout;
         a.start_bit = start_bit;
@@ -678,7 +663,7 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
         if (timeouts) {
             if (c->use_ticket) return fail(c, IE_EDEVICE, "tile look-back timed out");
             c->use_ticket = true;
-            return pack(c, bytes, n, code, len, out, out_cap, start_bit, end_bit, identity);
+            return pack(c, bytes, n, code, len, out, out_cap, start_bit, end_bit);
         }
     }
     if (!out_dev && end > start_bit) {
@@ -737,7 +722,6 @@ int ie_destroy(ie_ctx* c) {
     (void)hipHostFree(c->h_tab);
     (void)hipFree(c->d_state);
     (void)hipFree(c->d_ticket);
-    (void)hipFree(c->d_ident);
     (void)hipFree(c->d_frame_start);
     (void)hipFree(c->d_chain_end);
     (void)hipFree(c->d_err);
@@ -953,16 +937,39 @@ int ie_huffman_pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* c
 
 int ie_bitcopy(ie_ctx* c, const uint8_t* bytes, size_t n, uint8_t* out, size_t out_cap, uint64_t start_bit) {
     if (!c || (!bytes && n) || !out) return IE_EINVAL;
-    uint32_t code[256];
-    uint8_t len[256];
-    for (int b = 0; b < 256; b++) {
-        code[b] = uint32_t(b);
-        len[b] = 8;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t end = start_bit + 8 * uint64_t(n);
+    const size_t need_bytes = size_t((end + 31) / 32) * 4;  // whole words: the last one is zero-padded
+    if (out_cap < need_bytes) return fail(c, IE_ECAP, "output capacity below ceil((start_bit + 8n) / 32) words");
+    if (!n) return IE_OK;
+    int r;
+    const uint8_t* din = bytes;
+    if (!is_device_ptr(bytes)) {
+        if ((r = ensure(c, c->d_in, c->cap_in, n))) return r;
+        HIPCHK(c, hipMemcpyAsync(c->d_in, bytes, n, hipMemcpyHostToDevice, c->stream));
+        din = c->d_in;
     }
-    // device to device: asynchronous on the context's stream (checked at the next ie_sync)
-    uint64_t end = 0;
-    const bool async = is_device_ptr(out) && (!n || is_device_ptr(bytes));
-    return pack(c, bytes, n, code, len, out, out_cap, start_bit, async ? nullptr : &end, true);
+    const uint64_t w0 = start_bit / 32;
+    if (is_device_ptr(out)) {
+        if (reinterpret_cast<uintptr_t>(out) % 4) return fail(c, IE_EINVAL, "device output must be 4-byte aligned");
+        // device to device: asynchronous on the context's stream
+        ie::launch_bitshift(din, n, reinterpret_cast<uint32_t*>(out), start_bit, c->stream);
+        HIPCHK(c, hipGetLastError());
+        if (din == bytes) return IE_OK;
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // the staged input must outlive the copy
+        return IE_OK;
+    }
+    // host output: stage from the word holding start_bit (its leading bytes keep the caller's bits)
+    if ((r = ensure(c, c->d_out, c->cap_out, need_bytes - size_t(w0) * 4))) return r;
+    uint8_t word[4] = {0, 0, 0, 0};
+    for (int e = 0; e < 4 && size_t(w0) * 4 + e < out_cap; e++) word[e] = out[size_t(w0) * 4 + e];
+    HIPCHK(c, hipMemcpyAsync(c->d_out, word, 4, hipMemcpyHostToDevice, c->stream));
+    ie::launch_bitshift(din, n, reinterpret_cast<uint32_t*>(c->d_out) - w0, start_bit, c->stream);
+    HIPCHK(c, hipGetLastError());
+    const size_t b0 = size_t(start_bit / 8), b1 = size_t((end + 7) / 8);
+    HIPCHK(c, hipMemcpyAsync(out + b0, c->d_out + (b0 - size_t(w0) * 4), b1 - b0, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return IE_OK;
 }
 
 int ie_huffman_hist_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const uint64_t* n, int count,

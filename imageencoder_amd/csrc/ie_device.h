@@ -110,6 +110,8 @@ struct PackArgs {            // Huffman re-encode / bit copy: one variable-lengt
 // input bytes per pack tile for codes of at most maxlen bits (ie_huffman.hip)
 int pack_tile_bytes(int maxlen);
 void launch_pack(const PackArgs& a, hipStream_t s);
+// ie_bitcopy: n bytes to stream bit start_bit of out (no scan, no look-back; ie_huffman.hip)
+void launch_bitshift(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t start_bit, hipStream_t s);
 // hist / first (each optional, count*256): cleared to 0 / ~0 by the same launch
 void launch_ends_to_bytes(const uint64_t* ends, uint64_t cap, int count, uint64_t* n, hipStream_t s,
                           uint32_t* hist = nullptr, unsigned long long* first = nullptr);

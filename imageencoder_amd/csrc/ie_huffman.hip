@@ -7,8 +7,9 @@
 //                 containers (imageencoder_amd/csrc/host/Huffman.cpp);
 //   pack_kernel   re-encode every byte with its code, MSB-first (Huffman.cpp:314-319): the same
 //                 tile scan + LDS image + decoupled look-back + funnel store as the block encoder.
-// pack_kernel with the identity code (len 8) is also the shifted byte copy of the "no gain"
-// path ('0' + input, Huffman.cpp:329-341).
+// bitshift_kernel: the shifted byte copy (ie_bitcopy: the "no gain" path '0' + input,
+// Huffman.cpp:329-341, and the multi-GPU segment re-shift) -- every output word's source bits are
+// known from its index, so it needs no scan and no look-back: it can run beside any other kernel.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -323,6 +324,55 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     const uint64_t excl = chain_resolve(a.st, t, chain_pos, step, a.tag, img, A, hdr, start, a.err, misc, pr);
     if (tid == 0 && last) a.chain_end[k] = start + excl + A;
     store_image(out, img, A, start + excl, misc[7], last);
+}
+
+// Output words [w0, w1) of `out` (32-bit stream words stored as bytes, MSB-first) receive the n
+// input bytes' bits from stream bit A on: word W holds stream bits [32W, 32W + 32) = input bits
+// [32W - A, 32W - A + 32).  Bits before A (first word only) keep out's own bits -- the one thread
+// that writes word w0 reads it first; bits past the input's end are zero.  Thread t writes words
+// w0 + 4t .. +3.
+__global__ __launch_bounds__(256) void bitshift_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t* out,
+                                                       uint64_t A, uint64_t w0, uint64_t w1) {
+    const uint64_t W0 = w0 + 4ull * (uint64_t(blockIdx.x) * 256u + threadIdx.x);
+    if (W0 >= w1) return;
+    const uint64_t nw_in = (n + 3) / 4;
+    // big-endian input word q (q < 0 or past the end: 0; the last word's bytes past n: 0)
+    auto inw = [&](int64_t q) -> uint32_t {
+        if (q < 0 || uint64_t(q) >= nw_in) return 0u;
+        const uint64_t b = uint64_t(q) * 4;
+        if (b + 4 <= n && !(reinterpret_cast<uintptr_t>(in + b) & 3))
+            return bswap32(*reinterpret_cast<const uint32_t*>(in + b));
+        uint32_t v = 0;
+        for (int e = 0; e < 4; e++) v |= (b + e < n ? uint32_t(in[b + e]) : 0u) << (24 - 8 * e);
+        return v;
+    };
+    // input bit offset of word W0: d = 32*W0 - A = 32*q + r, 0 <= r < 32 (the same r for every word)
+    const int64_t d = int64_t(32 * W0) - int64_t(A);
+    const int64_t q = (d >= 0) ? (d >> 5) : -((-d + 31) >> 5);
+    const uint32_t r = uint32_t(d - 32 * q);
+    uint32_t wq[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) wq[k] = inw(q + k);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t W = W0 + k;
+        if (W >= w1) break;
+        uint32_t v = __builtin_amdgcn_alignbit(wq[k], wq[k + 1], 32u - r);  // bits [r, r+32) of wq[k]:wq[k+1]
+        if (r == 0) v = wq[k];
+        if (W == w0 && (A & 31)) {  // the caller's bits before A
+            const uint32_t keep = ~(0xFFFFFFFFu >> (A & 31));
+            v = (bswap32(out[W]) & keep) | (v & ~keep);
+        }
+        out[W] = bswap32(v);
+    }
+}
+
+void launch_bitshift(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t start_bit, hipStream_t s) {
+    const uint64_t w0 = start_bit / 32, w1 = (start_bit + 8 * n + 31) / 32;
+    if (w1 <= w0) return;
+    const uint64_t threads = (w1 - w0 + 3) / 4;
+    hipLaunchKernelGGL(bitshift_kernel, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, s, in, n, out, start_bit,
+                       w0, w1);
 }
 
 int pack_tile_bytes(int maxlen) { return maxlen <= 16 ? kTPB * 64 : kTPB * 16; }

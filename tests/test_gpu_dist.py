@@ -32,6 +32,9 @@ def _worker(rank, world, port, name, nchunks, steps, q_out):
     from tests import oracle_lib as O
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # the ranks share one GPU: order tiles by atomic ticket, so concurrent look-back kernels of the
+    # two processes can never hold each other's predecessor tiles off the CUs
+    os.environ["IE_FORCE_TICKET"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         c = {x["name"]: x for x in O.manifest()}[name]

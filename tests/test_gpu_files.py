@@ -171,6 +171,30 @@ def test_bitcopy(codec, start_bit):
     assert np.array_equal(bits[start_bit:start_bit + 8 * data.size], np.unpackbits(data))
 
 
+@pytest.mark.parametrize("start_bit,n,off", [(0, 1, 0), (3, 5, 1), (165, 100_003, 0), (210, 77_777, 3),
+                                             (31, 4, 2), (32 * 1000 + 7, 1_000_000, 1)])
+def test_bitcopy_device(codec, start_bit, n, off):
+    """Device to device (the multi-GPU segment re-shift): arbitrary start bits, input slices that
+    are not word-aligned, the caller's bits before start_bit kept, the rest of the last word zero,
+    nothing written past it (the output is pre-filled with garbage)."""
+    import torch
+    rng = np.random.default_rng(start_bit + n)
+    data = rng.integers(0, 256, n + off, dtype=np.uint8)
+    garbage = rng.integers(0, 256, (start_bit + 8 * n) // 8 + 64, dtype=np.uint8)
+    din = torch.from_numpy(data).cuda()[off:]
+    dout = torch.from_numpy(garbage).cuda()
+    codec.bitcopy(din, dout, start_bit)
+    codec.sync()
+    bits = np.unpackbits(dout.cpu().numpy())
+    g = np.unpackbits(garbage)
+    end = start_bit + 8 * n
+    wend = (end + 31) // 32 * 32
+    assert np.array_equal(bits[:start_bit], g[:start_bit])
+    assert np.array_equal(bits[start_bit:end], np.unpackbits(data[off:]))
+    assert not bits[end:wend].any()
+    assert np.array_equal(bits[wend:], g[wend:])
+
+
 def test_huffman_pack_codes(codec):
     """Variable-length codes up to 32 bits land MSB-first at arbitrary start bits."""
     rng = np.random.default_rng(3)
