@@ -516,6 +516,10 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     c->last_fix_words = (mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
     a.tab = c->d_tab;
     a.rec_bits = c->h_tab->rec_bits;
+    a.tri = (c->n == 4 && (a.rec_bits - 4) / 17 <= 11) ? 1 : 0;  // bl_max = (rec_bits - 4) / (1 + N*N)
+#ifdef IE_NOTRI  // A/B aid: pairs only
+    a.tri = 0;
+#endif
     a.coef = coef;
     a.hist = hist;
     if (hist) HIPCHK(c, hipMemsetAsync(hist, 0, size_t(nframes) * 256 * sizeof(uint32_t), c->stream));

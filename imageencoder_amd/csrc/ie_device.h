@@ -67,6 +67,7 @@ struct EncArgs {
     int ablate;              // profiling only (IE_ABLATE): 1 no FP64, 2 no emission, 4 no look-back, 8 no store, 16 no DCT, 128 no pixel loads
     uint64_t* stamps;        // profiling only (IE_STAMPS): [tile][kStamps] s_memtime per phase, thread 0
     int rec_bits;            // = tab->rec_bits (host copy): launch_encode sizes the LDS tile image from it
+    int tri;                 // 4x4: every bl <= 11 (from rec_bits): records emitted three coefficients per field
     int img_words;           // set by launch_encode
     // optional (segmented launches): per-frame byte histograms [nframes][256] of the stream bytes
     // [0, ceil(end/8)) -- header included -- ADDED to by the launch (the Huffman pass's counts)

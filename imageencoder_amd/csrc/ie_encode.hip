@@ -57,7 +57,7 @@ template <> struct ZigZagInv<8> {
 #define IE_BPT4 4
 #endif
 #ifndef IE_WAVES4
-#define IE_WAVES4 4
+#define IE_WAVES4 5
 #endif
 #ifndef IE_WAVES8
 #define IE_WAVES8 4
@@ -94,6 +94,13 @@ constexpr int image_words_for(int n, int bpt, int rec_bits) {
 #endif
 #ifndef IE_FIX_UNROLL
 #define IE_FIX_UNROLL 16
+#endif
+// FAST 4x4: the tile's pixels go straight from HBM into LDS (global_load_lds_dwordx4, no VGPR
+// destination) in the fix-up's pixel area, laid out per wave as [row r][lane][4 words] (block b
+// of a lane = word b of each row), and every block reads its four rows back when it is
+// transformed: no pixel registers live across the tile's phases.
+#ifndef IE_LDS_PIX
+#define IE_LDS_PIX 1
 #endif
 constexpr int kFixPix = 0;                               // [BPT][TPB] x 4 words: the pixels
 constexpr int kFixTasks = kFixPix + IE_BPT4 * kEncTPB * 4;  // per wave: [64] tasks, [64] results
@@ -454,6 +461,26 @@ __device__ __forceinline__ void emit_block2(uint32_t* img, uint32_t p, const uin
     }
 }
 
+// 4x4 RLE records when every bl of the matrix is <= 11 (EncArgs::tri, from the host's record
+// bound): the header, Lw and z0 in one field of 4 + 2*bl bits, then the coefficients THREE at a
+// time (3*bl <= 33 bits, within scatter_bits' 64-bit window): 6 ORed fields per block instead of
+// 9.  Past Lw the packed coefficients are zero, so a trailing triple only ORs zeros.
+__device__ __forceinline__ void emit_block3(uint32_t* img, uint32_t p, const uint32_t (&zp)[8], uint32_t blw) {
+    const uint32_t bl = blw & 0xFFu, lw = blw >> 8;
+    auto z = [&](int k) -> uint32_t {  // low bl bits of zig-zag coefficient k
+        return __builtin_amdgcn_ubfe(zp[k >> 1], (k & 1) ? 16u : 0u, bl);
+    };
+    scatter_bits(img, p, ((((bl & 0xFu) << bl) | lw) << bl) | z(0), 4u + 2u * bl);
+    p += 4u + 2u * bl;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        if (!__ballot(uint32_t(3 * j + 1) < lw)) break;  // no lane has coefficient 3j+1
+        const uint32_t v = (((z(3 * j + 1) << bl) | z(3 * j + 2)) << bl) | z(3 * j + 3);
+        scatter_bits(img, p, v, 3u * bl);
+        p += 3u * bl;
+    }
+}
+
 // The record of one sized block at bit p of the tile image (Block.cpp:372-413): bl in 4 bits,
 // [Lw in bl bits,] then the coefficients two at a time (2*bl <= 32 bits per OR pair).
 template <int N>
@@ -582,10 +609,12 @@ __device__ __forceinline__ void emit_block_sink(WordSink& k, const uint32_t (&zp
 #ifndef IE_LB_ATTR
 #define IE_LB_ATTR 0
 #endif
+// The EXACT 4x4 kernel (FP64 for every coefficient) keeps four waves per SIMD.
+template <int N, bool EXACT> constexpr int enc_waves() { return (N == 4 && EXACT) ? 4 : Geo<N>::WAVES; }
 #if IE_LB_ATTR
-#define IE_ENC_BOUNDS(N) __launch_bounds__(kEncTPB) __attribute__((amdgpu_waves_per_eu(Geo<N>::WAVES, 8)))
+#define IE_ENC_BOUNDS(N, EXACT) __launch_bounds__(kEncTPB) __attribute__((amdgpu_waves_per_eu((enc_waves<N, EXACT>()), 8)))
 #else
-#define IE_ENC_BOUNDS(N) __launch_bounds__(kEncTPB, Geo<N>::WAVES)
+#define IE_ENC_BOUNDS(N, EXACT) __launch_bounds__(kEncTPB, (enc_waves<N, EXACT>()))
 #endif
 // HIST: count the stored bytes into a per-tile LDS histogram (256 words after the misc area),
 // merged into a.hist[frame] at the end: the Huffman pass's histogram without re-reading the stream.
@@ -605,7 +634,7 @@ struct HistCount {
 };
 
 template <int N, bool EXACT, bool HIST = false>
-__global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
+__global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     constexpr int NN = N * N;
     constexpr int NP = NN / 2;
     constexpr int BPT = Geo<N>::BPT;
@@ -638,7 +667,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     if (a.ticket) {
         if (tid == 0) ctl[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
         lds_barrier();
-        t = int(ctl[4]);
+        t = __builtin_amdgcn_readfirstlane(int(ctl[4]));  // uniform: tile geometry stays in SGPRs
         if (t >= a.ntiles) return;  // ticket desync (a failed earlier launch): never touch memory
     } else {
         t = int(blockIdx.x);
@@ -653,8 +682,29 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     const TileGeo g = tile_geo<N>(a, t, tid);
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
+    constexpr bool kLdsPix = IE_LDS_PIX && N == 4 && !EXACT;
+    uint32_t* const pwave = img + kFixPix + (tid >> 6) * 1024;  // kLdsPix: this wave's [4][64][4] words
+    const int lane = tid & 63;
     uint32_t seg[N][WPR];
-    if (ablate & 128) {  // profiling: no pixel loads (synthetic pixels from the thread id)
+    if constexpr (kLdsPix) {
+        static_assert(BPT == 4 && WPR == 4 && TPB % 64 == 0, "LDS pixel layout: 16 bytes per lane per row");
+        if (!__ballot(!(a.vec_ok && nblk == BPT))) {  // every group of the wave is whole: DMA
+            const uint8_t* base =
+                a.y + size_t(frame) * a.frame_pitch + size_t(byi) * N * a.stride + size_t(bx0) * N;
+#pragma unroll
+            for (int r = 0; r < N; r++)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
+                                                 (__attribute__((address_space(3))) void*)(pwave + r * 256), 16, 0, 0);
+        } else {  // ragged (frame edge, unaligned rows): through registers
+            load_tile<N, WPR>(a, g, seg);
+#pragma unroll
+            for (int r = 0; r < N; r++) {
+                u32x4 v;
+                v.x = seg[r][0]; v.y = seg[r][1]; v.z = seg[r][2]; v.w = seg[r][3];
+                *reinterpret_cast<u32x4*>(pwave + r * 256 + lane * 4) = v;
+            }
+        }
+    } else if (ablate & 128) {  // profiling: no pixel loads (synthetic pixels from the thread id)
 #pragma unroll
         for (int r = 0; r < N; r++)
 #pragma unroll
@@ -663,6 +713,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
         load_tile<N, WPR>(a, g, seg);
     }
     if constexpr (!EXACT) lds_barrier();  // srow visible (the pixel loads stay in flight)
+    if constexpr (kLdsPix) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
 
     asm volatile("; PHASE load_done" ::: "memory");
     if (stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
@@ -695,7 +746,14 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                 zp[b][j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
         } else {
             float x[NN];
-            block_pixels<N, WPR>(seg, b, x);
+            if constexpr (kLdsPix) {
+                uint32_t rows[N][1];
+#pragma unroll
+                for (int r = 0; r < N; r++) rows[r][0] = pwave[r * 256 + lane * 4 + b];
+                block_pixels<N, 1>(rows, 0, x);
+            } else {
+                block_pixels<N, WPR>(seg, b, x);
+            }
             if (!(ablate & 16)) quotients<N>(tab, x);
             if constexpr (N == 8) {
                 static_assert(BPT == 1, "8x8: one block per lane");
@@ -741,7 +799,6 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                 pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
                 total += uint32_t(__popcll(bm)) << k;
             }
-            const int lane = tid & 63;
             uint32_t* task = img + kFix8Tasks + (tid >> 6) * 128;  // [64] tasks, then [64] results
             uint32_t* res = task + 64;
             for (uint32_t r0 = 0; r0 < total; r0 += 64) {
@@ -841,14 +898,29 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
         // evaluates task i in FP64 and the owners patch their results in.  One FP64 evaluation
         // per 64 requests instead of one per lane per request.
         if (__ballot(flags != 0)) {
-            uint32_t* pxl = img + kFixPix;  // [BPT][TPB] x 16 bytes: block b of thread tid
+            // the pixels of block b of thread `owner` (of this wave): kLdsPix reads the tile's
+            // LDS pixel layout; otherwise they are copied there first, [BPT][TPB] x 16 bytes
+            uint32_t* pxl = img + kFixPix;
+            if constexpr (!kLdsPix) {
 #pragma unroll
-            for (int bb = 0; bb < BPT; bb++) {
-                u32x4 v;
-                v.x = seg[0][(bb * N) / 4]; v.y = seg[1][(bb * N) / 4];
-                v.z = seg[2][(bb * N) / 4]; v.w = seg[3][(bb * N) / 4];
-                *reinterpret_cast<u32x4*>(pxl + 4 * (bb * TPB + tid)) = v;
+                for (int bb = 0; bb < BPT; bb++) {
+                    u32x4 v;
+                    v.x = seg[0][(bb * N) / 4]; v.y = seg[1][(bb * N) / 4];
+                    v.z = seg[2][(bb * N) / 4]; v.w = seg[3][(bb * N) / 4];
+                    *reinterpret_cast<u32x4*>(pxl + 4 * (bb * TPB + tid)) = v;
+                }
             }
+            auto block_px = [&](int b, int owner) {
+                BlockPx<N> px;
+                if constexpr (kLdsPix) {
+#pragma unroll
+                    for (int r = 0; r < N; r++) px.w[r] = pwave[r * 256 + (owner & 63) * 4 + b];
+                } else {
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
+                    px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
+                }
+                return px;
+            };
             const uint32_t sf = flags & (0x77777777u >> (32 - 4 * BPT));
             const uint32_t cnt = __popc(sf);
             uint32_t pre = 0, total = 0;
@@ -858,7 +930,6 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                 pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
                 total += uint32_t(__popcll(bm)) << k;
             }
-            const int lane = tid & 63;
             uint32_t* task = img + kFixTasks + (tid >> 6) * 128;  // [64] tasks, then [64] results
             uint32_t* res = task + 64;
             for (uint32_t r0 = 0; r0 < total; r0 += 64) {
@@ -873,9 +944,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                 if (uint32_t(lane) < total - r0) {
                     const uint32_t tk = task[lane];
                     const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
-                    const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
-                    BlockPx<N> px;
-                    px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
+                    const BlockPx<N> px = block_px(b, owner);
                     res[lane] = (ablate & 256) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
                                                  : uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s],
                                                                               srow[3 * NN + 3 + s], srow[3 * NN + 6 + s],
@@ -928,9 +997,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
                     if (uint32_t(lane >> 4) < tb - r0) {
                         const uint32_t tk = task[lane >> 4];
                         const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
-                        const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
-                        BlockPx<N> px;
-                        px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
+                        const BlockPx<N> px = block_px(b, owner);
                         res[lane] = uint32_t(exact_coef_row<N>(tab->P + k * NN, tab->S[k], tab->rq[k], tab->qd[k], px)) &
                                     0xFFFFu;
                     }
@@ -1050,7 +1117,7 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
     Probe pr{0, 0, 0};
     if (tid < 64 && chain_pos != 0 && !(ablate & 4)) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);  // in flight during emission
     const uint32_t nw = (A + 31) >> 5;
-    for (uint32_t w = tid; w < nw + 2; w += TPB) img[w] = 0u;
+    for (uint32_t w = 4 * tid; w < nw + 2; w += 4 * TPB) *reinterpret_cast<u32x4*>(img + w) = u32x4{0u, 0u, 0u, 0u};
     lds_barrier();
     asm volatile("; PHASE scan_done" ::: "memory");
     STAMP(6);
@@ -1067,7 +1134,10 @@ __global__ IE_ENC_BOUNDS(N) void encode_kernel(EncArgs a, const EncTables* __res
             uint32_t p = off;
 #pragma unroll
             for (int b = 0; b < BPT; b++) {
-                if (IE_EMIT2) {
+                if (N == 4 && a.tri && a.rle) {
+                    if constexpr (N == 4)
+                        if (rbits[b]) emit_block3(img, p, zp[b], blw[b]);
+                } else if (IE_EMIT2) {
                     if (rbits[b]) emit_block2<N>(img, p, zp[b], blw[b], a.rle);
                 } else {
                     if (rbits[b]) emit_block<N>(img, p, zp[b], blw[b], a.rle);

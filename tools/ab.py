@@ -31,7 +31,8 @@ args = ap.parse_args()
 n = args.n
 q = np.ascontiguousarray(np.asarray(O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n), dtype=np.uint16).ravel())
 w, h, nf = 3840, 2160, args.frames
-y = torch.from_numpy(synth.frames(args.kind, w, h, nf, seed=3)).cuda()
+y = (synth.uniform_device(w, h, nf, 3, "cuda", torch) if args.kind == "U"
+     else torch.from_numpy(synth.frames(args.kind, w, h, nf, seed=3)).cuda())
 stream = torch.cuda.Stream()  # a real stream handle (the default stream's handle is 0 = the ctx's own)
 torch.cuda.set_stream(stream)
 variants = []
