@@ -42,51 +42,15 @@ int block_size() {
     return (e && std::atoi(e) == 8) ? 8 : 4;
 }
 
-}  // namespace
-
-int main(int argc, char* argv[]) {
-    if (argc != 2) {
-        std::cerr << "One argument, the name of a settings file, expected!" << std::endl;
-        return 1;
-    }
-    dc::ConfigReader c;
-    if (!c.read(argv[1])) {
-        std::cerr << "Error reading file '" << argv[1] << "'!" << std::endl;
-        std::cerr << c.getErrorDescription() << std::endl;
-        return 2;
-    }
-    const bool is_image = c.verifyForImage();
-    const std::string ei = c.getErrorDescription();
-    const bool is_encvideo = c.verifyForVideo(true);
-    const std::string eev = c.getErrorDescription();
-    const bool is_decvideo = c.verifyForVideo(false);
-    const std::string edv = c.getErrorDescription();
-    if (!((is_image && !(is_encvideo || is_decvideo)) || ((is_encvideo || is_decvideo) && !is_image))) {
-        std::cerr << "Error in settings!" << std::endl;
-        if (!ei.empty()) std::cerr << ei << std::endl;
-        if (!eev.empty()) std::cerr << eev << std::endl;
-        if (!edv.empty()) std::cerr << edv << std::endl;
-        return 3;
-    }
-    util::Logger::Create(c.getValue(dc::ImageSetting::logfile));
-    util::Logger::WriteLn("Input settings:");
-    util::Logger::WriteLn("-------------------------");
-    util::Logger::WriteLn(c.toString());
-
-    const std::string encfile = c.getValue(dc::ImageSetting::encfile);
-    const std::string decfile = c.getValue(dc::ImageSetting::decfile);
-    const int n = block_size();
-    bool success = true;
-    auto start = std::chrono::steady_clock::now();
-    (void)success;
-
+// The encoder half of main.cpp:68-131 for block size N (the reference's compile-time
+// dc::BlockSize; dc::MatrixReader<N> reads the matrix).  Returns a non-zero exit code on error.
 #ifdef ENCODER
+template <size_t N>
+int encode_with(const dc::ConfigReader& c, bool is_image, bool is_encvideo, std::chrono::steady_clock::time_point start,
+                bool& success) {
     const std::string rawfile = c.getValue(dc::ImageSetting::rawfile);
-    if (rawfile == encfile) {
-        std::cerr << "Error in settings! Encoded filename must be different from raw filename!" << std::endl;
-        return 3;
-    }
-    dc::MatrixReader m(n);
+    const std::string encfile = c.getValue(dc::ImageSetting::encfile);
+    dc::MatrixReader<N> m;
     if (!m.read(c.getValue(dc::ImageSetting::quantfile))) return 4;
     util::Logger::WriteLn("Quantization matrix:");
     util::Logger::WriteLn("-------------------------");
@@ -136,6 +100,57 @@ int main(int argc, char* argv[]) {
             util::Logger::WriteLn("Error processing raw video for encoding! " + enc.error());
         }
     }
+    return 0;
+}
+#endif
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+    if (argc != 2) {
+        std::cerr << "One argument, the name of a settings file, expected!" << std::endl;
+        return 1;
+    }
+    dc::ConfigReader c;
+    if (!c.read(argv[1])) {
+        std::cerr << "Error reading file '" << argv[1] << "'!" << std::endl;
+        std::cerr << c.getErrorDescription() << std::endl;
+        return 2;
+    }
+    const bool is_image = c.verifyForImage();
+    const std::string ei = c.getErrorDescription();
+    const bool is_encvideo = c.verifyForVideo(true);
+    const std::string eev = c.getErrorDescription();
+    const bool is_decvideo = c.verifyForVideo(false);
+    const std::string edv = c.getErrorDescription();
+    if (!((is_image && !(is_encvideo || is_decvideo)) || ((is_encvideo || is_decvideo) && !is_image))) {
+        std::cerr << "Error in settings!" << std::endl;
+        if (!ei.empty()) std::cerr << ei << std::endl;
+        if (!eev.empty()) std::cerr << eev << std::endl;
+        if (!edv.empty()) std::cerr << edv << std::endl;
+        return 3;
+    }
+    util::Logger::Create(c.getValue(dc::ImageSetting::logfile));
+    util::Logger::WriteLn("Input settings:");
+    util::Logger::WriteLn("-------------------------");
+    util::Logger::WriteLn(c.toString());
+
+    const std::string encfile = c.getValue(dc::ImageSetting::encfile);
+    const std::string decfile = c.getValue(dc::ImageSetting::decfile);
+    const int n = block_size();
+    bool success = true;
+    auto start = std::chrono::steady_clock::now();
+    (void)success;
+
+#ifdef ENCODER
+    const std::string rawfile = c.getValue(dc::ImageSetting::rawfile);
+    if (rawfile == encfile) {
+        std::cerr << "Error in settings! Encoded filename must be different from raw filename!" << std::endl;
+        return 3;
+    }
+    const int rc = (n == 8) ? encode_with<8>(c, is_image, is_encvideo, start, success)
+                            : encode_with<4>(c, is_image, is_encvideo, start, success);
+    if (rc) return rc;
 #endif
 
 #ifdef DECODER

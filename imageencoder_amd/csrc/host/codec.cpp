@@ -12,6 +12,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <utility>
 
 #include "host_internal.hpp"
 #include "ie_host.hpp"
@@ -133,8 +134,13 @@ struct StreamHeader {
 static bool parse_header(const uint8_t* src, size_t len, size_t start, int n, bool video, StreamHeader& sh) {
     util::BitStreamReader rd(src, len);
     rd.set_position(start);
-    MatrixReader m = MatrixReader::fromBitstream(rd, n);  // MatrixReader.cpp:46-56
-    sh.q.assign(m.data(), m.data() + n * n);
+    if (n == 8) {  // MatrixReader<N>::fromBitstream (MatrixReader.cpp:46-56)
+        const MatrixReader<8> m = MatrixReader<8>::fromBitstream(rd);
+        sh.q.assign(m.data(), m.data() + 64);
+    } else {
+        const MatrixReader<4> m = MatrixReader<4>::fromBitstream(rd);
+        sh.q.assign(m.data(), m.data() + 16);
+    }
     sh.rle = int(rd.get(1));
     sh.w = int(rd.get(15));
     sh.h = int(rd.get(15));
@@ -174,116 +180,128 @@ static int decode_file(ie_ctx* c, const uint8_t* enc, size_t len, int n, bool vi
     return IE_OK;
 }
 
-// ------------------------------------------------------------------------------- ImageEncoder
-ImageEncoder::ImageEncoder(const std::string& source_file, const std::string& dest_file, uint16_t width,
-                           uint16_t height, bool use_rle, MatrixReader& quant_m, EncodeOptions opt)
-    : src_(source_file), dst_(dest_file), w_(width), h_(height), rle_(use_rle), q_(quant_m), opt_(opt) {
-    if (!read_file(src_, raw_)) err_ = "Could not read file '" + src_ + "'";
+// ----------------------------------------------------------------------------- ImageProcessor
+ImageProcessor::ImageProcessor(const std::string& src, const std::string& dst, uint16_t w, uint16_t h, bool rle,
+                               QuantSpec quant)
+    : width(w), height(h), use_rle(rle), quant_m(std::move(quant)), source_file(src), dest_file(dst) {
+    if (!read_file(source_file, raw)) err_ = "Could not read file '" + source_file + "'";
 }
 
+ImageProcessor::ImageProcessor(const std::string& src, const std::string& dst) : source_file(src), dest_file(dst) {
+    if (!read_file(source_file, raw)) err_ = "Could not read file '" + source_file + "'";
+}
+
+void ImageProcessor::saveResult(bool encoded) const {
+    if (!write_file(dest_file, result_)) util::Logger::WriteLn("[ImageProcessor] Could not write '" + dest_file + "'");
+    if (encoded) {
+        util::Logger::WriteLn(fmt("[ImageProcessor] Original file size: %8.0f bytes", double(raw.size())));
+        util::Logger::WriteLn(fmt("[ImageProcessor]        Encoded size: %8.0f bytes  => Ratio: %.2f%%",
+                                  double(result_.size()),
+                                  raw.empty() ? 0.0 : 100.0 * double(result_.size()) / double(raw.size())));
+    }
+    util::Logger::WriteLn("[ImageProcessor] Saved file at: " + dest_file);
+}
+
+// ------------------------------------------------------------------------------- ImageEncoder
 bool ImageEncoder::process() {
     if (!err_.empty()) return false;
     util::Logger::WriteLn("[ImageEncoder] Processing image...");
-    const int n = q_.size();
-    if (w_ % n || h_ % n) return (err_ = "width and height must be multiples of the block size", false);
-    if (raw_.size() != size_t(w_) * h_) return (err_ = "raw file size differs from width x height", false);
+    const int n = quant_m.n;
+    if (width % n || height % n) return (err_ = "width and height must be multiples of the block size", false);
+    if (raw.size() != size_t(width) * height) return (err_ = "raw file size differs from width x height", false);
     FileParams p;
-    p.w = w_;
-    p.h = h_;
+    p.w = width;
+    p.h = height;
     p.n = n;
-    p.q = q_.data();
-    p.rle = rle_;
+    p.q = quant_m.q.data();
+    p.rle = use_rle;
     p.huffman = opt_.huffman;
     p.mode = opt_.mode;
-    if (encode_file(Device::get(), raw_.data(), p, out_, err_) != IE_OK) return false;
-    return true;
-}
-
-void ImageEncoder::saveResult() const {
-    if (!write_file(dst_, out_)) util::Logger::WriteLn("[ImageEncoder] Could not write '" + dst_ + "'");
-    util::Logger::WriteLn(fmt("[ImageProcessor] Original file size: %8.0f bytes", double(raw_.size())));
-    util::Logger::WriteLn(fmt("[ImageProcessor]        Encoded size: %8.0f bytes  => Ratio: %.2f%%",
-                              double(out_.size()), raw_.empty() ? 0.0 : 100.0 * double(out_.size()) / raw_.size()));
-    util::Logger::WriteLn("[ImageProcessor] Saved file at: " + dst_);
+    return encode_file(Device::get(), raw.data(), p, result_, err_) == IE_OK;
 }
 
 // ------------------------------------------------------------------------------- ImageDecoder
 ImageDecoder::ImageDecoder(const std::string& source_file, const std::string& dest_file, int block_size)
-    : src_(source_file), dst_(dest_file), n_(block_size ? block_size : block_size_from_env()) {}
+    : ImageProcessor(source_file, dest_file), n_(block_size ? block_size : block_size_from_env()) {}
 
 bool ImageDecoder::process() {
-    std::vector<uint8_t> enc;
-    if (!read_file(src_, enc)) return (err_ = "Could not read file '" + src_ + "'", false);
+    if (!err_.empty()) return false;
     util::Logger::WriteLn("[ImageDecoder] Processing image...");
     StreamHeader sh;
-    if (decode_file(Device::get(), enc.data(), enc.size(), n_, false, sh, pix_, err_) != IE_OK) return false;
-    w_ = uint16_t(sh.w);
-    h_ = uint16_t(sh.h);
+    if (decode_file(Device::get(), raw.data(), raw.size(), n_, false, sh, result_, err_) != IE_OK) return false;
+    width = uint16_t(sh.w);
+    height = uint16_t(sh.h);
+    use_rle = sh.rle != 0;
+    quant_m.n = n_;
+    quant_m.q = sh.q;
     return true;
 }
 
-void ImageDecoder::saveResult() const {
-    if (!write_file(dst_, pix_)) util::Logger::WriteLn("[ImageDecoder] Could not write '" + dst_ + "'");
-    util::Logger::WriteLn("[ImageProcessor] Saved file at: " + dst_);
+// ----------------------------------------------------------------------------- VideoProcessor
+VideoProcessor::VideoProcessor(const std::string& src, const std::string& dst, uint16_t w, uint16_t h, bool rle,
+                               QuantSpec quant, uint16_t g, uint16_t mer)
+    : width(w), height(h), gop(g ? g : 1), merange(mer), use_rle(rle), quant_m(std::move(quant)), source_file(src),
+      dest_file(dst) {
+    if (!read_file(source_file, raw)) err_ = "Could not read file '" + source_file + "'";
+}
+
+VideoProcessor::VideoProcessor(const std::string& src, const std::string& dst, const bool& mc)
+    : motioncomp(mc), source_file(src), dest_file(dst) {
+    if (!read_file(source_file, raw)) err_ = "Could not read file '" + source_file + "'";
+}
+
+void VideoProcessor::saveResult(bool encoded) const {
+    if (!write_file(dest_file, result_)) util::Logger::WriteLn("[VideoProcessor] Could not write '" + dest_file + "'");
+    if (encoded) {
+        util::Logger::WriteLn(fmt("[VideoProcessor] Original file size: %8.0f bytes", double(raw.size())));
+        util::Logger::WriteLn(fmt("[VideoProcessor]       Encoded size: %8.0f bytes  => Ratio: %.2f%%",
+                                  double(result_.size()),
+                                  raw.empty() ? 0.0 : 100.0 * double(result_.size()) / double(raw.size())));
+    }
+    util::Logger::WriteLn("[VideoProcessor] Saved file at: " + dest_file);
 }
 
 // ------------------------------------------------------------------------------- VideoEncoder
-VideoEncoder::VideoEncoder(const std::string& source_file, const std::string& dest_file, uint16_t width,
-                           uint16_t height, bool use_rle, MatrixReader& quant_m, uint16_t gop, uint16_t merange,
-                           EncodeOptions opt)
-    : src_(source_file), dst_(dest_file), w_(width), h_(height), gop_(gop ? gop : 1), merange_(merange),
-      rle_(use_rle), q_(quant_m), opt_(opt) {
-    if (!read_file(src_, raw_)) err_ = "Could not read file '" + src_ + "'";
-}
-
 bool VideoEncoder::process() {
     if (!err_.empty()) return false;
     util::Logger::WriteLn("[VideoEncoder] Processing video...");
-    const int n = q_.size();
-    if (w_ % n || h_ % n) return (err_ = "width and height must be multiples of the block size", false);
-    if (gop_ != 1) return (err_ = "P-frames (gop > 1) need motion estimation, which this encoder does not provide", false);
-    const size_t pitch = size_t(w_) * h_ + size_t(w_) * h_ / 2;  // Y + UV (VideoBase.cpp:8-9)
-    const size_t frames = pitch ? raw_.size() / pitch : 0;
+    const int n = quant_m.n;
+    if (width % n || height % n) return (err_ = "width and height must be multiples of the block size", false);
+    if (gop != 1) return (err_ = "P-frames (gop > 1) need motion estimation, which this encoder does not provide", false);
+    const size_t pitch = size_t(width) * height + size_t(width) * height / 2;  // Y + UV (VideoBase.cpp:8-9)
+    const size_t frames = pitch ? raw.size() / pitch : 0;
     if (frames == 0 || frames > 32767) return (err_ = "frame count must be in 1..32767", false);
     FileParams p;
-    p.w = w_;
-    p.h = h_;
+    p.w = width;
+    p.h = height;
     p.n = n;
-    p.q = q_.data();
-    p.rle = rle_;
+    p.q = quant_m.q.data();
+    p.rle = use_rle;
     p.huffman = opt_.huffman;
     p.mode = opt_.mode;
     p.video = true;
     p.frames = int(frames);
-    p.gop = gop_;
-    p.merange = merange_;
+    p.gop = gop;
+    p.merange = merange;
     p.frame_pitch = pitch;
-    return encode_file(Device::get(), raw_.data(), p, out_, err_) == IE_OK;
-}
-
-void VideoEncoder::saveResult() const {
-    if (!write_file(dst_, out_)) util::Logger::WriteLn("[VideoEncoder] Could not write '" + dst_ + "'");
-    util::Logger::WriteLn(fmt("[VideoProcessor] Original file size: %8.0f bytes", double(raw_.size())));
-    util::Logger::WriteLn(fmt("[VideoProcessor]       Encoded size: %8.0f bytes  => Ratio: %.2f%%",
-                              double(out_.size()), raw_.empty() ? 0.0 : 100.0 * double(out_.size()) / raw_.size()));
-    util::Logger::WriteLn("[VideoProcessor] Saved file at: " + dst_);
+    return encode_file(Device::get(), raw.data(), p, result_, err_) == IE_OK;
 }
 
 // ------------------------------------------------------------------------------- VideoDecoder
-VideoDecoder::VideoDecoder(const std::string& source_file, const std::string& dest_file, bool, int block_size)
-    : src_(source_file), dst_(dest_file), n_(block_size ? block_size : block_size_from_env()) {}
+VideoDecoder::VideoDecoder(const std::string& source_file, const std::string& dest_file, const bool& mc,
+                           int block_size)
+    : VideoProcessor(source_file, dest_file, mc), n_(block_size ? block_size : block_size_from_env()) {}
 
 bool VideoDecoder::process() {
-    std::vector<uint8_t> enc;
-    if (!read_file(src_, enc)) return (err_ = "Could not read file '" + src_ + "'", false);
+    if (!err_.empty()) return false;
     util::Logger::WriteLn("[VideoDecoder] Processing video...");
     StreamHeader sh;
-    return decode_file(Device::get(), enc.data(), enc.size(), n_, true, sh, out_, err_) == IE_OK;
-}
-
-void VideoDecoder::saveResult() const {
-    if (!write_file(dst_, out_)) util::Logger::WriteLn("[VideoDecoder] Could not write '" + dst_ + "'");
-    util::Logger::WriteLn("[VideoProcessor] Saved file at: " + dst_);
+    if (decode_file(Device::get(), raw.data(), raw.size(), n_, true, sh, result_, err_) != IE_OK) return false;
+    width = uint16_t(sh.w);
+    height = uint16_t(sh.h);
+    gop = uint16_t(sh.gop);
+    merange = uint16_t(sh.merange);
+    return true;
 }
 
 }  // namespace dc

@@ -2,7 +2,7 @@
 // the reference's acceptance rules and messages:
 //   dc::ConfigReader   ConfigReader.cpp:75-242 (key=value lines, CR/LF stripped, empty lines
 //                      skipped; missing '=', empty key and duplicate key are errors)
-//   dc::MatrixReader   MatrixReader.cpp:46-198 (rows split on single spaces after trimming and
+//   dc::MatrixReader<N> MatrixReader.cpp:46-198 (rows split on single spaces after trimming and
 //                      squeezing runs of spaces; exactly N rows of N values, each a uint16 as
 //                      parsed by util::lexical_cast, utils.hpp:293-305)
 #include <algorithm>
@@ -132,7 +132,17 @@ std::string ConfigReader::toString() const {
 }
 
 // ---------------------------------------------------------------------------------- matrix
-bool MatrixReader::read(const std::string& fileName) {
+template <size_t size>
+MatrixReader<size>::MatrixReader() {
+    for (size_t k = 0; k < size * size; k++) {
+        matrix_[k] = 0;
+        expanded_[k] = 0.0;
+    }
+}
+
+template <size_t size>
+bool MatrixReader<size>::read(const std::string& fileName) {
+    constexpr int n_ = int(size);
     std::ifstream f(fileName, std::ios::binary);
     if (!f) {
         std::cerr << "[MatrixReader] Could not read file '" << fileName << "'" << std::endl;
@@ -183,36 +193,49 @@ bool MatrixReader::read(const std::string& fileName) {
                   << std::endl;
         return false;
     }
-    m_ = m;
+    for (size_t k = 0; k < size * size; k++) {
+        matrix_[k] = m[k];
+        expanded_[k] = double(m[k]);  // MatrixReader.cpp:195-198 hands the doubles to the blocks
+    }
     return true;
 }
 
-uint8_t MatrixReader::getMaxBitLength() const {
+template <size_t size>
+uint8_t MatrixReader<size>::getMaxBitLength() const {
     int len = 0;  // util::ffs = bit length (utils.hpp:210-216); ffs(0) = 1 as built
-    for (uint16_t v : m_) len = std::max(len, v ? 32 - __builtin_clz(uint32_t(v)) : 1);
+    for (uint16_t v : matrix_) len = std::max(len, v ? 32 - __builtin_clz(uint32_t(v)) : 1);
     return uint8_t(len);
 }
 
-void MatrixReader::write(util::BitStreamWriter& w) const {
+template <size_t size>
+void MatrixReader<size>::write(util::BitStreamWriter& w) const {
     const uint8_t qb = getMaxBitLength();
-    w.put(5, qb);
-    for (uint16_t v : m_) w.put(qb, v);
+    w.put(SIZE_LEN_BITS, qb);
+    for (uint16_t v : matrix_) w.put(qb, v);
 }
 
-MatrixReader MatrixReader::fromBitstream(util::BitStreamReader& r, int n) {
-    MatrixReader m(n);
-    const uint32_t qb = r.get(5);
-    for (auto& v : m.m_) v = uint16_t(r.get(qb));
+template <size_t size>
+MatrixReader<size> MatrixReader<size>::fromBitstream(util::BitStreamReader& r) {
+    MatrixReader<size> m;
+    const uint32_t qb = r.get(SIZE_LEN_BITS);
+    for (size_t k = 0; k < size * size; k++) {
+        m.matrix_[k] = uint16_t(r.get(qb));
+        m.expanded_[k] = double(m.matrix_[k]);
+    }
     return m;
 }
 
-std::string MatrixReader::toString() const {
+template <size_t size>
+const std::string MatrixReader<size>::toString() const {
     std::ostringstream o;
-    for (int r = 0; r < n_; r++) {
-        for (int c = 0; c < n_; c++) o << std::setw(4) << m_[size_t(r) * n_ + c];
+    for (size_t r = 0; r < size; r++) {
+        for (size_t c = 0; c < size; c++) o << std::setw(4) << matrix_[r * size + c];
         o << '\n';
     }
     return o.str();
 }
+
+template class MatrixReader<4>;
+template class MatrixReader<8>;
 
 }  // namespace dc

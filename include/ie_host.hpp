@@ -5,7 +5,9 @@
 // behaviour as the reference (cited per class), so the encoder/decoder CLIs drop onto it:
 //   util::BitStreamWriter/Reader  BitStream.hpp:91-171      MSB-first bit IO (header, Huffman dict)
 //   dc::ConfigReader              ConfigReader.hpp:41-75    key=value settings file
-//   dc::MatrixReader              MatrixReader.hpp:15-37    N x N quantisation matrix (N now runtime)
+//   dc::MatrixReader<N>           MatrixReader.hpp:15-37    N x N quantisation matrix (N = 4 or 8)
+//   dc::ImageProcessor            ImageBase.hpp:35-77       base of the image encoder / decoder
+//   dc::VideoProcessor            VideoBase.hpp:17-48       base of the video encoder / decoder
 //   algo::Huffman                 Huffman.hpp:109-142       byte Huffman post-pass (tree on the host)
 //   dc::ImageEncoder/ImageDecoder ImageEncoder.hpp, ImageDecoder.hpp
 //   dc::VideoEncoder/VideoDecoder VideoEncoder.hpp, VideoDecoder.hpp (gop = 1: I-frames only)
@@ -91,22 +93,44 @@ private:
     std::string err_;
 };
 
-// MatrixReader (MatrixReader.cpp): whitespace separated N x N uint16 values; written to the
-// stream as a 5-bit width followed by N*N values of that width.
+// The reference's default block size (Block.hpp:13); the GPU library takes 4 or 8 at run time.
+static constexpr uint16_t BlockSize = 4u;
+
+// dc::MatrixReader<size> (MatrixReader.hpp:15-37, MatrixReader.cpp:46-198): a size x size
+// quantisation matrix read from whitespace-separated text (the reference's acceptance rules and
+// messages), written to the stream as a 5-bit width followed by size*size values of that width.
+// getData() is the matrix as doubles, as the reference hands it to Block<>::processDCTDivQ;
+// data() the uint16 values for ie_set_quant.  Instantiated for 4 and 8 (config.cpp).
+template <size_t size = BlockSize>
 class MatrixReader {
 public:
-    explicit MatrixReader(int n = 4) : n_(n), m_(size_t(n) * n, 0) {}
+    MatrixReader();
+    static MatrixReader<size> fromBitstream(util::BitStreamReader& reader);
     bool read(const std::string& fileName);
-    void write(util::BitStreamWriter& w) const;
-    static MatrixReader fromBitstream(util::BitStreamReader& r, int n);
+    void write(util::BitStreamWriter& writer) const;
+    const std::string toString() const;
     uint8_t getMaxBitLength() const;
-    const uint16_t* data() const { return m_.data(); }
-    int size() const { return n_; }
-    std::string toString() const;
+    const double* getData() const { return expanded_; }
+    const uint16_t* data() const { return matrix_; }
+    static constexpr size_t SIZE_LEN_BITS = 5;
 
 private:
-    int n_;
-    std::vector<uint16_t> m_;
+    uint16_t matrix_[size * size];
+    double expanded_[size * size];
+};
+
+// What an encoder keeps of its MatrixReader<N>: the block size (a run-time parameter of the GPU
+// library) and the matrix values.
+struct QuantSpec {
+    int n = 0;
+    std::vector<uint16_t> q;
+    template <size_t N>
+    static QuantSpec from(const MatrixReader<N>& m) {
+        QuantSpec s;
+        s.n = int(N);
+        s.q.assign(m.data(), m.data() + N * N);
+        return s;
+    }
 };
 
 }  // namespace dc
@@ -138,83 +162,152 @@ public:
     static ie_ctx* get();
 };
 
+// dc::ImageProcessor (ImageBase.hpp:35-77): the image encoder / decoder base.  The encoder
+// constructor takes (source, dest, width, height, use_rle, quant matrix) and reads the raw file
+// (ImageBase.cpp:19-30, 78-88); the decoder constructor takes (source, dest) and learns every
+// setting from the stream (ImageBase.cpp:98-129).  process() / saveResult() are the reference's
+// virtual pair.  Where the reference builds one heap Block<> per block (ImageBase.cpp:175-206)
+// and loops over them, process() here hands the whole frame to the GPU library: dc::Block<N>
+// has no counterpart -- see DESIGN.md §1.
+class ImageProcessor {
+public:
+    ImageProcessor(const std::string& source_file, const std::string& dest_file, const uint16_t& width,
+                   const uint16_t& height, const bool& use_rle, MatrixReader<>& quant_m)
+        : ImageProcessor(source_file, dest_file, width, height, use_rle, QuantSpec::from(quant_m)) {}
+    template <size_t N>
+    ImageProcessor(const std::string& source_file, const std::string& dest_file, const uint16_t& width,
+                   const uint16_t& height, const bool& use_rle, MatrixReader<N>& quant_m)
+        : ImageProcessor(source_file, dest_file, width, height, use_rle, QuantSpec::from(quant_m)) {}
+    ImageProcessor(const std::string& source_file, const std::string& dest_file);
+    virtual ~ImageProcessor() = default;
+
+    virtual bool process() = 0;
+    virtual void saveResult() const {}
+
+    const std::vector<uint8_t>& result() const { return result_; }  // encoded file / decoded pixels
+    std::string error() const { return err_; }
+    uint16_t getWidth() const { return width; }
+    uint16_t getHeight() const { return height; }
+
+    static constexpr size_t RLE_BITS = 1u;   // ImageBase.hpp:75
+    static constexpr size_t DIM_BITS = 15u;  // ImageBase.hpp:76
+
+protected:
+    ImageProcessor(const std::string& source_file, const std::string& dest_file, uint16_t width, uint16_t height,
+                   bool use_rle, QuantSpec quant);
+    void saveResult(bool encoded) const;  // ImageBase.cpp:309-330: the file and the size report
+
+    uint16_t width = 0, height = 0;
+    bool use_rle = true;
+    QuantSpec quant_m;
+    std::string source_file, dest_file;
+    std::vector<uint8_t> raw;      // the input file (ImageBase::raw)
+    std::vector<uint8_t> result_;  // what saveResult writes
+    std::string err_;
+};
+
 struct EncodeOptions {
     bool huffman = true;   // the reference's ENABLE_HUFFMAN (makefile:13)
     int mode = IE_MODE_FAST;
 };
 
-class ImageEncoder {
+// dc::ImageEncoder (ImageEncoder.hpp:12-23, ImageEncoder.cpp:19-180).
+class ImageEncoder : public ImageProcessor {
 public:
-    ImageEncoder(const std::string& source_file, const std::string& dest_file, uint16_t width, uint16_t height,
-                 bool use_rle, MatrixReader& quant_m, EncodeOptions opt = EncodeOptions());
-    bool process();
-    void saveResult() const;
-    const std::vector<uint8_t>& result() const { return out_; }
-    std::string error() const { return err_; }
+    ImageEncoder(const std::string& source_file, const std::string& dest_file, const uint16_t& width,
+                 const uint16_t& height, const bool& use_rle, MatrixReader<>& m, EncodeOptions opt = EncodeOptions())
+        : ImageProcessor(source_file, dest_file, width, height, use_rle, m), opt_(opt) {}
+    template <size_t N>
+    ImageEncoder(const std::string& source_file, const std::string& dest_file, const uint16_t& width,
+                 const uint16_t& height, const bool& use_rle, MatrixReader<N>& m, EncodeOptions opt = EncodeOptions())
+        : ImageProcessor(source_file, dest_file, width, height, use_rle, m), opt_(opt) {}
+    bool process() override;
+    void saveResult() const override { ImageProcessor::saveResult(true); }
 
 private:
-    std::string src_, dst_;
-    uint16_t w_, h_;
-    bool rle_;
-    MatrixReader q_;
     EncodeOptions opt_;
-    std::vector<uint8_t> raw_, out_;
-    std::string err_;
 };
 
-class ImageDecoder {
+// dc::ImageDecoder (ImageDecoder.hpp:11-21, ImageDecoder.cpp:17-129).  The block size of the
+// stream is the reference's compile-time BlockSize; here block_size (0: IE_BLOCKSIZE, default 4).
+class ImageDecoder : public ImageProcessor {
 public:
-    ImageDecoder(const std::string& source_file, const std::string& dest_file, int block_size = 4);
-    bool process();
-    void saveResult() const;
-    const std::vector<uint8_t>& result() const { return pix_; }
-    uint16_t width() const { return w_; }
-    uint16_t height() const { return h_; }
-    std::string error() const { return err_; }
+    ImageDecoder(const std::string& source_file, const std::string& dest_file, int block_size = 0);
+    bool process() override;
+    void saveResult() const override { ImageProcessor::saveResult(false); }
+    uint16_t width_px() const { return width; }
 
 private:
-    std::string src_, dst_;
     int n_;
-    uint16_t w_ = 0, h_ = 0;
-    std::vector<uint8_t> pix_;
+};
+
+// dc::VideoProcessor (VideoBase.hpp:17-48): the video encoder / decoder base; frames are YUV420
+// (Y + W*H/2 bytes, VideoBase.cpp:6-19).  gop = 1 only: every frame an I-frame, payloads
+// concatenated bit-contiguously after a 210-bit header (VideoEncoder.cpp:22-107, Frame.cpp:31-45).
+// gop > 1 needs motion estimation (P-frames), outside this library's scope: process() then fails
+// with an explanatory error.
+class VideoProcessor {
+public:
+    VideoProcessor(const std::string& source_file, const std::string& dest_file, const uint16_t& width,
+                   const uint16_t& height, const bool& use_rle, MatrixReader<>& quant_m, const uint16_t& gop,
+                   const uint16_t& merange)
+        : VideoProcessor(source_file, dest_file, width, height, use_rle, QuantSpec::from(quant_m), gop, merange) {}
+    template <size_t N>
+    VideoProcessor(const std::string& source_file, const std::string& dest_file, const uint16_t& width,
+                   const uint16_t& height, const bool& use_rle, MatrixReader<N>& quant_m, const uint16_t& gop,
+                   const uint16_t& merange)
+        : VideoProcessor(source_file, dest_file, width, height, use_rle, QuantSpec::from(quant_m), gop, merange) {}
+    VideoProcessor(const std::string& source_file, const std::string& dest_file, const bool& motioncomp);
+    virtual ~VideoProcessor() = default;
+
+    virtual bool process() = 0;
+    virtual void saveResult() const {}
+
+    const std::vector<uint8_t>& result() const { return result_; }
+    std::string error() const { return err_; }
+
+protected:
+    VideoProcessor(const std::string& source_file, const std::string& dest_file, uint16_t width, uint16_t height,
+                   bool use_rle, QuantSpec quant, uint16_t gop, uint16_t merange);
+    void saveResult(bool encoded) const;
+
+    uint16_t width = 0, height = 0, gop = 1, merange = 0;
+    bool use_rle = true, motioncomp = false;
+    QuantSpec quant_m;
+    std::string source_file, dest_file;
+    std::vector<uint8_t> raw, result_;
     std::string err_;
 };
 
-// gop = 1 video: every frame an I-frame, payloads concatenated bit-contiguously after a 210-bit
-// header (VideoEncoder.cpp:22-107, Frame.cpp:31-45).  gop > 1 needs motion estimation (P-frames),
-// which is outside this library's scope: process() then fails with an explanatory error.
-class VideoEncoder {
+// dc::VideoEncoder (VideoEncoder.hpp:11-21).
+class VideoEncoder : public VideoProcessor {
 public:
-    VideoEncoder(const std::string& source_file, const std::string& dest_file, uint16_t width, uint16_t height,
-                 bool use_rle, MatrixReader& quant_m, uint16_t gop, uint16_t merange,
-                 EncodeOptions opt = EncodeOptions());
-    bool process();
-    void saveResult() const;
-    const std::vector<uint8_t>& result() const { return out_; }
-    std::string error() const { return err_; }
+    VideoEncoder(const std::string& source_file, const std::string& dest_file, const uint16_t& width,
+                 const uint16_t& height, const bool& use_rle, MatrixReader<>& m, const uint16_t& gop,
+                 const uint16_t& merange, EncodeOptions opt = EncodeOptions())
+        : VideoProcessor(source_file, dest_file, width, height, use_rle, m, gop, merange), opt_(opt) {}
+    template <size_t N>
+    VideoEncoder(const std::string& source_file, const std::string& dest_file, const uint16_t& width,
+                 const uint16_t& height, const bool& use_rle, MatrixReader<N>& m, const uint16_t& gop,
+                 const uint16_t& merange, EncodeOptions opt = EncodeOptions())
+        : VideoProcessor(source_file, dest_file, width, height, use_rle, m, gop, merange), opt_(opt) {}
+    bool process() override;
+    void saveResult() const override { VideoProcessor::saveResult(true); }
 
 private:
-    std::string src_, dst_;
-    uint16_t w_, h_, gop_, merange_;
-    bool rle_;
-    MatrixReader q_;
     EncodeOptions opt_;
-    std::vector<uint8_t> raw_, out_;
-    std::string err_;
 };
 
-class VideoDecoder {
+// dc::VideoDecoder (VideoDecoder.hpp): frames of Y + W*H/2 bytes of 0x80 (Frame.cpp:121-124).
+class VideoDecoder : public VideoProcessor {
 public:
-    VideoDecoder(const std::string& source_file, const std::string& dest_file, bool motioncomp, int block_size = 4);
-    bool process();
-    void saveResult() const;
-    std::string error() const { return err_; }
+    VideoDecoder(const std::string& source_file, const std::string& dest_file, const bool& motioncomp,
+                 int block_size = 0);
+    bool process() override;
+    void saveResult() const override { VideoProcessor::saveResult(false); }
 
 private:
-    std::string src_, dst_;
     int n_;
-    std::vector<uint8_t> out_;
-    std::string err_;
 };
 
 }  // namespace dc
