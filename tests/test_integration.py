@@ -52,4 +52,14 @@ def test_dropin_encoder_matches_reference_files(tmp_path, c):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     got = out.read_bytes()
-    assert hashlib.md5(got).hexdigest() == c["md5"] and len(got) == c["size"], c["name"]
+    assert len(got) == c["size"], c["name"]
+    if c["huffman"] and got[:1] < b"\x80":
+        # Huffman "no gain" file ('0' + the record bytes, Huffman.cpp:326-338): the reference
+        # writes 8*n+1 bits into an n-byte BitStreamWriter, and put_bit never grows it
+        # (BitStream.cpp:61-71), so the last byte's low 7 bits are whatever heap memory follows
+        # the allocation -- zero in the golden's process, anything in this one.  Every defined bit
+        # must match.
+        want = open(os.path.join(O.GOLDEN, c["file"]), "rb").read()
+        assert got[:-1] == want[:-1] and (got[-1] & 0x80) == (want[-1] & 0x80), c["name"]
+        return
+    assert hashlib.md5(got).hexdigest() == c["md5"], c["name"]
