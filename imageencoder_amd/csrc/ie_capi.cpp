@@ -498,6 +498,9 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     a.gpr_magic = (g.gpr > 1) ? uint32_t(((uint64_t(1) << 32) + uint64_t(g.gpr) - 1) / uint64_t(g.gpr)) : 0u;
     a.groups_per_frame = g.gpf;
     a.tiles_per_frame = g.tpf;
+    a.div_frames = ie::make_fastdiv(uint32_t(nframes));
+    a.div_tpf = ie::make_fastdiv(uint32_t(g.tpf));
+    a.div_gpr = ie::make_fastdiv(uint32_t(g.gpr));
     a.ntiles = g.ntiles;
     a.rle = use_rle ? 1 : 0;
     a.segmented = segmented;

@@ -35,6 +35,22 @@ struct EncTables {
     double R[64 * 64];
 };
 
+// Division by a launch constant d (1 <= d < 2^31) for dividends n < 2^31, by a multiply-high:
+// floor(n / d) = (mulhi(n, mul) + n) >> shr with shr = ceil(log2 d), mul = floor(2^32 (2^shr - d) / d) + 1
+// (Granlund-Montgomery).  Built on the host (make_fastdiv), evaluated in scalar registers.
+struct FastDiv {
+    uint32_t d, mul, shr;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f{d, 0u, 0u};
+    while ((1ull << f.shr) < d) f.shr++;
+    f.mul = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << f.shr) - d)) / d + 1);
+    return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    return (__umulhi(n, f.mul) + n) >> f.shr;
+}
+
 // One encode launch.  Tiles (workgroups) never straddle frames; a "chain" is the sequence of
 // tiles whose bit offsets accumulate: the whole batch (concatenated stream) or one frame
 // (independent images, segmented = 1).
@@ -48,6 +64,7 @@ struct EncArgs {
     int groups_per_frame;    // gpr * by
     int tiles_per_frame;     // ceil(groups_per_frame / encode_threads_per_tile())
     int ntiles;
+    FastDiv div_frames, div_tpf, div_gpr;  // by nframes, tiles_per_frame, gpr
     int rle;
     int segmented;
     int vec_ok;              // rows may be read with 16-/8-byte loads

@@ -461,6 +461,12 @@ __device__ __forceinline__ void emit_block2(uint32_t* img, uint32_t p, const uin
     }
 }
 
+// IE_EMIT_ALL: every triple is ORed in, without a wave-wide "any lane still has one" exit per
+// field (past Lw the coefficients are zero): the v_cmp + branch per field cost more than the
+// skipped fields save unless every lane of the wave has a short record (measured -2 % on C2).
+#ifndef IE_EMIT_ALL
+#define IE_EMIT_ALL 1
+#endif
 // 4x4 RLE records when every bl of the matrix is <= 11 (EncArgs::tri, from the host's record
 // bound): the header, Lw and z0 in one field of 4 + 2*bl bits, then the coefficients THREE at a
 // time (3*bl <= 33 bits, within scatter_bits' 64-bit window): 6 ORed fields per block instead of
@@ -474,7 +480,7 @@ __device__ __forceinline__ void emit_block3(uint32_t* img, uint32_t p, const uin
     p += 4u + 2u * bl;
 #pragma unroll
     for (int j = 0; j < 5; j++) {
-        if (!__ballot(uint32_t(3 * j + 1) < lw)) break;  // no lane has coefficient 3j+1
+        if (!IE_EMIT_ALL && !__ballot(uint32_t(3 * j + 1) < lw)) break;  // no lane has coefficient 3j+1
         const uint32_t v = (((z(3 * j + 1) << bl) | z(3 * j + 2)) << bl) | z(3 * j + 3);
         scatter_bits(img, p, v, 3u * bl);
         p += 3u * bl;
@@ -517,12 +523,13 @@ __device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
     TileGeo g;
     // Independent images interleave their tiles (frame = t % nframes), so every frame's chain
     // advances together; a concatenated stream keeps chain order = tile order.
+    // (wave-uniform divisions by launch constants: multiply-highs, FastDiv)
     if (a.segmented) {
-        g.frame = t % a.nframes;
-        g.tif = t / a.nframes;
+        g.tif = int(fdiv(uint32_t(t), a.div_frames));
+        g.frame = t - g.tif * a.nframes;
         g.step = a.nframes;
     } else {
-        g.frame = t / a.tiles_per_frame;
+        g.frame = int(fdiv(uint32_t(t), a.div_tpf));
         g.tif = t - g.frame * a.tiles_per_frame;
         g.step = 1;
     }
@@ -530,7 +537,7 @@ __device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
     // group gi = base + tid: the division by gpr is split into a wave-uniform (scalar) part and a
     // per-lane remainder r < gpr + kEncTPB, divided by a multiply-high with ceil(2^32 / gpr)
     const int base = g.tif * kEncTPB;
-    const int q0 = base / a.gpr, r0 = base - q0 * a.gpr;
+    const int q0 = int(fdiv(uint32_t(base), a.div_gpr)), r0 = base - q0 * a.gpr;
     const uint32_t r = uint32_t(r0 + tid);
     const uint32_t dq = (a.gpr == 1) ? r : __umulhi(r, a.gpr_magic);  // (2^32 does not fit the magic)
     const int gi = base + tid;
@@ -641,15 +648,17 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     constexpr int WPR = BPT * N / 4;
     constexpr int TPB = kEncTPB;
 #ifdef IE_STATIC_IMG4  // A/B aid: a static image of this many bits per block (4x4 only)
-    __shared__ __attribute__((aligned(16))) uint32_t smem[image_words_for(4, 4, IE_STATIC_IMG4) + 32];
+    __shared__ __attribute__((aligned(16))) uint32_t smem[image_words_for(4, 4, IE_STATIC_IMG4) + 32 + 2 * (3 * NN + 9)];
 #else
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // [a.img_words + 32]
 #endif
-    // FAST mode: the structural coefficients' FP64 rows (P[3][NN], then S[3], rq[3], qd[3])
-    __shared__ double srow[3 * NN + 9];
+    // Dynamic LDS: [tile image: img_words][misc: 32 words][HIST: 256 words][srow]; the image at
+    // LDS address 0, so its addresses need no base.
     uint32_t* img = smem;
     uint32_t* misc = smem + a.img_words;  // [0..15] scan scratch (one word per wave)
     uint32_t* ctl = misc + 16;     // [4] ticket, [5..6] exclusive prefix, [7] predecessor tail
+    // FAST mode: the structural coefficients' FP64 rows (P[3][NN], then S[3], rq[3], qd[3])
+    double* const srow = reinterpret_cast<double*>(misc + 32 + (HIST ? 256 : 0));
 
     const int tid = threadIdx.x;
     // Profiling hooks (IE_ABLATE / IE_STAMPS) exist only in IE_PROFILE builds (tools/variants.sh):
@@ -674,7 +683,8 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     }
     STAMP(0);
     uint32_t* const hl = misc + 32;  // HIST: the tile's byte histogram
-    if constexpr (HIST) hl[tid] = 0u;  // (visible after the scan's barriers)
+    if constexpr (HIST)
+        for (int i = tid; i < 256; i += TPB) hl[i] = 0u;  // (visible after the scan's barriers)
     if constexpr (!EXACT) {
         // issued before the pixel loads, so waiting for it does not wait for them
         for (int i = tid; i < 3 * NN + 9; i += TPB) srow[i] = tab->srow[i];
@@ -1176,7 +1186,6 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
 
     // ---------------------------------------------------------------- 4. store
     if constexpr (HIST) {
-        static_assert(TPB == 256, "one histogram bin per thread");
         if (tif == 0)  // the words before the first record word hold only the caller's header
             for (uint32_t i = tid; i < uint32_t(a.start_bit >> 5); i += TPB) {
                 const uint32_t v = out[i];
@@ -1187,7 +1196,8 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         const HistCount cnt{hl, chain_last ? (end + 7) / 8 : ~0ull};
         store_tile<TPB>(out, img, A, a.start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err, cnt);
         lds_barrier();
-        if (hl[tid]) atomicAdd(&a.hist[size_t(frame) * 256 + tid], hl[tid]);
+        for (int i = tid; i < 256; i += TPB)
+            if (hl[i]) atomicAdd(&a.hist[size_t(frame) * 256 + i], hl[i]);
     } else if (!(ablate & 8)) {
         store_tile<TPB>(out, img, A, a.start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err);
     }
@@ -1208,7 +1218,8 @@ void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s) {
     a.img_words = image_words_for(4, 4, IE_STATIC_IMG4);
     const size_t lds = 0;
 #else
-    const size_t lds = (size_t(a.img_words) + 32 + (a.hist ? 256 : 0)) * sizeof(uint32_t);
+    const size_t lds = (size_t(a.img_words) + 32 + (a.hist ? 256 : 0)) * sizeof(uint32_t) +
+                       (exact ? 0 : size_t(3 * n * n + 9) * sizeof(double));
 #endif
     const dim3 grid(a.ntiles), block(kEncTPB);
     if (a.hist) {  // segmented 4x4 FAST launches only (ie_encode_images_counted; 8x8 would spill)
