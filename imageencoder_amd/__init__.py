@@ -89,6 +89,16 @@ def load_library(path: str | None = None) -> C.CDLL:
     if hasattr(L, "ie_decode_frames"):
         L.ie_decode_frames.argtypes = [vp, u8p, C.c_size_t, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
                                        u8p, C.c_size_t, C.c_size_t, u64p]
+    L.ie_host_alloc.argtypes = [vp, C.c_size_t, C.POINTER(C.c_void_p)]
+    L.ie_host_free.argtypes = [vp, vp]
+    L.ie_vstream_open.argtypes = [vp, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, u8p, C.c_uint64,
+                                  C.c_int, C.POINTER(C.c_void_p)]
+    L.ie_vstream_push.argtypes = [vp, u8p, C.c_int]
+    L.ie_vstream_pull.argtypes = [vp, u8p, C.c_size_t, C.POINTER(C.c_size_t)]
+    L.ie_vstream_finish.argtypes = [vp, u8p, C.c_size_t, C.POINTER(C.c_size_t), u64p, u64p]
+    L.ie_vstream_device.argtypes = [vp]
+    L.ie_vstream_device.restype = C.c_void_p
+    L.ie_vstream_close.argtypes = [vp]
     L.ie_malloc.argtypes = [vp, C.c_size_t, C.POINTER(C.c_void_p)]
     L.ie_free.argtypes = [vp, vp]
     L.ie_memcpy.argtypes = [vp, vp, vp, C.c_size_t]
@@ -178,6 +188,76 @@ def read_matrix(path: str, n: int) -> np.ndarray:
 
 def stream_bound(w: int, h: int, n: int, nframes: int = 1, start_bit: int = 0) -> int:
     return int(load_library().ie_stream_bound(w, h, n, nframes, start_bit))
+
+
+class _PinnedOwner:
+    """Frees an ie_host_alloc block when the numpy array viewing it is collected."""
+    _live = {}
+
+    @classmethod
+    def attach(cls, arr, codec, addr):
+        import weakref
+        key = id(arr)
+        cls._live[key] = weakref.finalize(arr, cls._free, codec, addr, key)
+
+    @classmethod
+    def _free(cls, codec, addr, key):
+        cls._live.pop(key, None)
+        if getattr(codec, "h", None):
+            codec.L.ie_host_free(codec.h, C.c_void_p(addr))
+
+
+class VideoStream:
+    """ie_vstream_*: push host frames, pull finished stream bytes, finish (see include/ie_hip.h)."""
+
+    def __init__(self, codec, w, h, head, start_bit, max_frames, stride, frame_pitch, rle, mode):
+        self.c = codec
+        self.w, self.h = w, h
+        self.stride = w if stride is None else stride
+        self.frame_pitch = self.stride * h if frame_pitch is None else frame_pitch
+        head = np.zeros(1, dtype=np.uint8) if head is None else np.ascontiguousarray(head, dtype=np.uint8)
+        self._head = head
+        v = C.c_void_p()
+        codec._chk(codec.L.ie_vstream_open(codec.h, w, h, self.stride, self.frame_pitch, int(rle), mode,
+                                           head.ctypes.data, start_bit, max_frames, C.byref(v)))
+        self.v = v
+        self.max_frames = max_frames
+        self.pushed = 0
+        self.cap = stream_bound(w, h, codec.n, max_frames, start_bit)
+
+    def push(self, frames, nframes: int):
+        self.c._chk(self.c.L.ie_vstream_push(self.v, _ptr(frames), nframes))
+        self.pushed += nframes
+
+    def pull(self, dst: np.ndarray, offset: int) -> int:
+        """Finished bytes into dst[offset:]; returns how many."""
+        n = C.c_size_t(0)
+        self.c._chk(self.c.L.ie_vstream_pull(self.v, dst.ctypes.data + offset, dst.size - offset, C.byref(n)))
+        return int(n.value)
+
+    def finish(self, dst: np.ndarray | None = None, offset: int = 0):
+        """Remaining bytes into dst[offset:] (if given); returns (nbytes, end_bit, frame_bits)."""
+        n, end = C.c_size_t(0), C.c_uint64(0)
+        fb = np.zeros(max(self.pushed, 1), dtype=np.uint64)
+        dp = dst.ctypes.data + offset if dst is not None else None
+        cap = dst.size - offset if dst is not None else 0
+        self.c._chk(self.c.L.ie_vstream_finish(self.v, dp, cap, C.byref(n), C.byref(end),
+                                               fb.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return int(n.value), int(end.value), fb[: self.pushed]
+
+    def device_ptr(self) -> int:
+        return int(self.c.L.ie_vstream_device(self.v) or 0)
+
+    def close(self):
+        if getattr(self, "v", None):
+            self.c.L.ie_vstream_close(self.v)
+            self.v = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Codec:
@@ -271,6 +351,23 @@ class Codec:
         self._chk(self.L.ie_quantize_frames(self.h, _ptr(y), w, h, stride, frame_pitch, nframes, mode,
                                             coef.ctypes.data))
         return coef
+
+    def host_array(self, nbytes: int) -> np.ndarray:
+        """A uint8 numpy array in page-locked host memory (ie_host_alloc): host buffers the
+        streamed path DMAs directly.  Freed when the array (and the codec) are gone."""
+        p = C.c_void_p()
+        self._chk(self.L.ie_host_alloc(self.h, nbytes, C.byref(p)))
+        buf = (C.c_uint8 * nbytes).from_address(p.value)
+        arr = np.frombuffer(buf, dtype=np.uint8)
+        _PinnedOwner.attach(arr, self, p.value)
+        return arr
+
+    def open_video_stream(self, w: int, h: int, head=None, start_bit: int = 0, max_frames: int = 1,
+                          stride: int | None = None, frame_pitch: int | None = None, rle: bool = True,
+                          mode: int = MODE_FAST) -> "VideoStream":
+        """ie_vstream_open: a gop=1 video payload grown on the device from host frames pushed over
+        time (Frame.cpp:31-45 / VideoEncoder.cpp:83-91)."""
+        return VideoStream(self, w, h, head, start_bit, max_frames, stride, frame_pitch, rle, mode)
 
     def end_bits_into(self, dst, count: int = 1):
         """Stream-ordered device copy of the last encode's end bit(s) (one per chain) into the

@@ -9,10 +9,15 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ie_device.h"
+
+struct ie_pipe;  // streamed host path (below)
 
 struct ie_ctx {
     int device = 0;
@@ -96,6 +101,7 @@ struct ie_ctx {
     size_t cap_pix = 0;
     int last_rounds = 0;
     unsigned long long* d_first = nullptr;  // [256]
+    ie_pipe* pipe = nullptr;           // streamed host path of image batches (created on first use)
 };
 
 namespace {
@@ -428,104 +434,74 @@ int check_dims(ie_ctx* c, int w, int h, int nframes) {
 
 size_t bound_bits_per_block(int n) { return 4 + 16 * size_t(n * n + 1); }
 
-// Common driver of ie_encode_frames (segmented = 0) and ie_encode_images (segmented = 1).
-int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
-           int use_rle, int mode, uint8_t* out, size_t out_cap, size_t out_pitch, uint64_t start_bit,
-           int segmented, uint64_t* frame_bits, uint64_t* end_bits, int16_t* coef = nullptr,
-           uint32_t* hist = nullptr) {
-    c->fused_count = 0;  // any encode replaces the batch scratch's meaning
-    int r = check_dims(c, w, h, nframes);
-    if (r) return r;
-    if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
-    if (nframes > 1 && frame_pitch < stride * size_t(h - 1) + size_t(w))
-        return fail(c, IE_EINVAL, "frame_pitch smaller than a frame");
-    if (segmented && (out_pitch % 4)) return fail(c, IE_EINVAL, "out_pitch must be a multiple of 4");
-    HIPCHK(c, hipSetDevice(c->device));
-    const Geometry g = geometry(w, h, c->n, nframes);
-    const int nchains = segmented ? nframes : 1;
+// One encode launch over device-resident frames (no staging, no synchronisation): the EncArgs
+// of ie_device.h, the chain state's epoch and the launch.  start_dev (optional) makes the chain
+// start at a device-resident bit position (the previous launch's chain end, ie_vstream_*);
+// chain_end (optional) receives the chain end(s) instead of the context's d_chain_end.
+struct Launch {
+    const uint8_t* dy = nullptr;
+    int w = 0, h = 0;
+    size_t stride = 0, frame_pitch = 0;
+    int nframes = 0, use_rle = 1, mode = IE_MODE_FAST;
+    uint32_t* dout = nullptr;  // word 0 = stream bytes [0, 4) (may point before the allocation)
+    size_t out_pitch = 0;      // segmented: bytes between images
+    uint64_t start_bit = 0;
+    const uint64_t* start_dev = nullptr;
+    uint64_t* chain_end = nullptr;
+    int segmented = 0;
+    int16_t* coef = nullptr;
+    uint32_t* hist = nullptr;
+};
 
-    // input
-    const size_t in_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
-    const uint8_t* dy = y;
-    if (!is_device_ptr(y)) {
-        if ((r = ensure(c, c->d_in, c->cap_in, in_bytes))) return r;
-        HIPCHK(c, hipMemcpyAsync(c->d_in, y, in_bytes, hipMemcpyHostToDevice, c->stream));
-        dy = c->d_in;
-    }
+int launch_chain(ie_ctx* c, const Launch& L) {
+    const Geometry g = geometry(L.w, L.h, c->n, L.nframes);
     const int bpt = ie::encode_blocks_per_thread(c->n);
-    const bool vec_ok = (reinterpret_cast<uintptr_t>(dy) % size_t(bpt * c->n) == 0) && (stride % (bpt * c->n) == 0) &&
-                        (nframes == 1 || frame_pitch % (bpt * c->n) == 0);
-
-    // output
-    const uint64_t payload_bound = uint64_t(g.bx) * g.by * bound_bits_per_block(c->n) * (segmented ? 1 : nframes);
-    const uint64_t end_bound = start_bit + payload_bound;
-    const size_t need_bytes = size_t((end_bound + 31) / 32) * 4;
-    const size_t span = segmented ? out_pitch * size_t(nframes - 1) + need_bytes : need_bytes;
-    if (segmented && out_pitch < need_bytes) return fail(c, IE_ECAP, "out_pitch below ie_stream_bound");
-    if (out_cap < span) return fail(c, IE_ECAP, "output capacity below ie_stream_bound");
-    const bool out_dev = is_device_ptr(out);
-    uint32_t* dout;
-    const uint64_t w0 = start_bit / 32;
-    if (out_dev) {
-        if (reinterpret_cast<uintptr_t>(out) % 4) return fail(c, IE_EINVAL, "device output must be 4-byte aligned");
-        dout = reinterpret_cast<uint32_t*>(out);
-    } else {
-        // stage from the word holding start_bit; its leading bytes carry the caller's header
-        const size_t stage = span - size_t(w0) * 4;
-        if ((r = ensure(c, c->d_out, c->cap_out, stage))) return r;
-        for (int f = 0; f < (segmented ? nframes : 1); f++) {
-            const size_t hb = size_t(f) * out_pitch + size_t(w0) * 4;
-            uint8_t word[4] = {0, 0, 0, 0};
-            for (int e = 0; e < 4 && hb + e < out_cap; e++) word[e] = out[hb + e];
-            // keep only the bytes before start_bit's byte plus its leading bits
-            HIPCHK(c, hipMemcpyAsync(c->d_out + size_t(f) * out_pitch, word, 4, hipMemcpyHostToDevice, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-        }
-        dout = reinterpret_cast<uint32_t*>(c->d_out) - w0;
-    }
-
-    if ((r = prepare_state(c, g.ntiles, nframes))) return r;
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(L.dy) % size_t(bpt * c->n) == 0) &&
+                        (L.stride % (bpt * c->n) == 0) && (L.nframes == 1 || L.frame_pitch % (bpt * c->n) == 0);
+    int r;
+    if ((r = prepare_state(c, g.ntiles, L.nframes))) return r;
     ie::EncArgs a{};
-    a.y = dy;
-    a.stride = stride;
-    a.frame_pitch = frame_pitch;
-    a.w = w;
-    a.h = h;
-    a.nframes = nframes;
+    a.y = L.dy;
+    a.stride = L.stride;
+    a.frame_pitch = L.frame_pitch;
+    a.w = L.w;
+    a.h = L.h;
+    a.nframes = L.nframes;
     a.bx = g.bx;
     a.by = g.by;
     a.gpr = g.gpr;
     a.gpr_magic = (g.gpr > 1) ? uint32_t(((uint64_t(1) << 32) + uint64_t(g.gpr) - 1) / uint64_t(g.gpr)) : 0u;
     a.groups_per_frame = g.gpf;
     a.tiles_per_frame = g.tpf;
-    a.div_frames = ie::make_fastdiv(uint32_t(nframes));
+    a.div_frames = ie::make_fastdiv(uint32_t(L.nframes));
     a.div_tpf = ie::make_fastdiv(uint32_t(g.tpf));
     a.div_gpr = ie::make_fastdiv(uint32_t(g.gpr));
     a.ntiles = g.ntiles;
-    a.rle = use_rle ? 1 : 0;
-    a.segmented = segmented;
+    a.rle = L.use_rle ? 1 : 0;
+    a.segmented = L.segmented;
     a.vec_ok = vec_ok ? 1 : 0;
-    a.out = dout;
-    a.out_pitch_words = segmented ? out_pitch / 4 : 0;
-    a.start_bit = start_bit;
+    a.out = L.dout;
+    a.out_pitch_words = L.segmented ? L.out_pitch / 4 : 0;
+    a.start_bit = L.start_bit;
+    a.start_dev = L.start_dev;
     a.st = c->d_state;
     a.ticket = c->use_ticket ? c->d_ticket : nullptr;
     a.ticket_base = c->ticket_base;
     a.tag = c->tag;
     a.frame_start = c->d_frame_start;
-    a.chain_end = c->d_chain_end;
+    a.chain_end = L.chain_end ? L.chain_end : c->d_chain_end;
     a.err = c->d_err;
     a.wave_fix = c->d_wave_fix;
-    c->last_fix_words = (mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
+    c->last_fix_words = (L.mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
     a.tab = c->d_tab;
     a.rec_bits = c->h_tab->rec_bits;
     a.tri = (c->n == 4 && (a.rec_bits - 4) / 17 <= 11) ? 1 : 0;  // bl_max = (rec_bits - 4) / (1 + N*N)
 #ifdef IE_NOTRI  // A/B aid: pairs only
     a.tri = 0;
 #endif
-    a.coef = coef;
-    a.hist = hist;
-    if (hist) HIPCHK(c, hipMemsetAsync(hist, 0, size_t(nframes) * 256 * sizeof(uint32_t), c->stream));
+    a.coef = L.coef;
+    a.hist = L.hist;
+    if (L.hist) HIPCHK(c, hipMemsetAsync(L.hist, 0, size_t(L.nframes) * 256 * sizeof(uint32_t), c->stream));
 #ifndef IE_PROFILE
 #define IE_PROFILE 0
 #endif
@@ -548,19 +524,108 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
         HIPCHK(c, hipMemsetAsync(d_stamps, 0, size_t(g.ntiles) * ie::kStamps * sizeof(uint64_t), c->stream));
     }
     a.stamps = d_stamps;
-    ie::launch_encode(a, c->n, mode == IE_MODE_EXACT, c->stream);
+    ie::launch_encode(a, c->n, L.mode == IE_MODE_EXACT, c->stream);
     HIPCHK(c, hipGetLastError());
     if (d_stamps) {
-        std::vector<uint64_t> h(size_t(g.ntiles) * ie::kStamps);
-        HIPCHK(c, hipMemcpyAsync(h.data(), d_stamps, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        std::vector<uint64_t> hs(size_t(g.ntiles) * ie::kStamps);
+        HIPCHK(c, hipMemcpyAsync(hs.data(), d_stamps, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         HIPCHK(c, hipFree(d_stamps));
         if (FILE* f = std::fopen(stamp_file, "wb")) {
-            std::fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+            std::fwrite(hs.data(), sizeof(uint64_t), hs.size(), f);
             std::fclose(f);
         }
     }
     if (c->use_ticket) c->ticket_base += uint64_t(g.ntiles);
+    return IE_OK;
+}
+
+int streamed_images(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
+                    int use_rle, int mode, uint8_t* out, size_t out_pitch, uint64_t start_bit, uint64_t* end_bits);
+int streamed_frames(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
+                    int use_rle, int mode, uint8_t* out, size_t out_cap, uint64_t start_bit, uint64_t* frame_bits,
+                    uint64_t* end_bit);
+
+// Common driver of ie_encode_frames (segmented = 0) and ie_encode_images (segmented = 1).
+int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
+           int use_rle, int mode, uint8_t* out, size_t out_cap, size_t out_pitch, uint64_t start_bit,
+           int segmented, uint64_t* frame_bits, uint64_t* end_bits, int16_t* coef = nullptr,
+           uint32_t* hist = nullptr) {
+    c->fused_count = 0;  // any encode replaces the batch scratch's meaning
+    int r = check_dims(c, w, h, nframes);
+    if (r) return r;
+    if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
+    if (nframes > 1 && frame_pitch < stride * size_t(h - 1) + size_t(w))
+        return fail(c, IE_EINVAL, "frame_pitch smaller than a frame");
+    if (segmented && (out_pitch % 4)) return fail(c, IE_EINVAL, "out_pitch must be a multiple of 4");
+    HIPCHK(c, hipSetDevice(c->device));
+    const Geometry g = geometry(w, h, c->n, nframes);
+    const int nchains = segmented ? nframes : 1;
+
+    // output bound
+    const uint64_t payload_bound = uint64_t(g.bx) * g.by * bound_bits_per_block(c->n) * (segmented ? 1 : nframes);
+    const uint64_t end_bound = start_bit + payload_bound;
+    const size_t need_bytes = size_t((end_bound + 31) / 32) * 4;
+    const size_t span = segmented ? out_pitch * size_t(nframes - 1) + need_bytes : need_bytes;
+    if (segmented && out_pitch < need_bytes) return fail(c, IE_ECAP, "out_pitch below ie_stream_bound");
+    if (out_cap < span) return fail(c, IE_ECAP, "output capacity below ie_stream_bound");
+    const bool in_dev = is_device_ptr(y), out_dev = is_device_ptr(out);
+
+    // Host frames in AND host streams out, several frames: the streamed path (pinned double
+    // buffering, H2D / encode / D2H on three streams; ie_vstream for the concatenated chain).
+    if (!in_dev && !out_dev && nframes > 1 && !coef && !hist && !c->use_ticket) {
+        return segmented ? streamed_images(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_pitch,
+                                           start_bit, end_bits)
+                         : streamed_frames(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_cap,
+                                           start_bit, frame_bits, end_bits);
+    }
+
+    // input
+    const size_t in_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
+    const uint8_t* dy = y;
+    if (!in_dev) {
+        if ((r = ensure(c, c->d_in, c->cap_in, in_bytes))) return r;
+        HIPCHK(c, hipMemcpyAsync(c->d_in, y, in_bytes, hipMemcpyHostToDevice, c->stream));
+        dy = c->d_in;
+    }
+
+    // output
+    uint32_t* dout;
+    const uint64_t w0 = start_bit / 32;
+    if (out_dev) {
+        if (reinterpret_cast<uintptr_t>(out) % 4) return fail(c, IE_EINVAL, "device output must be 4-byte aligned");
+        dout = reinterpret_cast<uint32_t*>(out);
+    } else {
+        // stage from the word holding start_bit; its leading bytes carry the caller's header
+        const size_t stage = span - size_t(w0) * 4;
+        if ((r = ensure(c, c->d_out, c->cap_out, stage))) return r;
+        for (int f = 0; f < (segmented ? nframes : 1); f++) {
+            const size_t hb = size_t(f) * out_pitch + size_t(w0) * 4;
+            uint8_t word[4] = {0, 0, 0, 0};
+            for (int e = 0; e < 4 && hb + e < out_cap; e++) word[e] = out[hb + e];
+            // keep only the bytes before start_bit's byte plus its leading bits
+            HIPCHK(c, hipMemcpyAsync(c->d_out + size_t(f) * out_pitch, word, 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
+        dout = reinterpret_cast<uint32_t*>(c->d_out) - w0;
+    }
+
+    Launch L;
+    L.dy = dy;
+    L.w = w;
+    L.h = h;
+    L.stride = stride;
+    L.frame_pitch = frame_pitch;
+    L.nframes = nframes;
+    L.use_rle = use_rle;
+    L.mode = mode;
+    L.dout = dout;
+    L.out_pitch = out_pitch;
+    L.start_bit = start_bit;
+    L.segmented = segmented;
+    L.coef = coef;
+    L.hist = hist;
+    if ((r = launch_chain(c, L))) return r;
 
     const bool want = frame_bits || end_bits || !out_dev;
     if (!want) {
@@ -598,6 +663,614 @@ int encode(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t fram
     }
     return IE_OK;
 }
+
+// ---- streamed host path ---------------------------------------------------------------------
+// Host frames in, host streams out (the reference reads and writes whole files, utils.hpp:352-402,
+// VideoBase.cpp:6-19): the batch flows through the device in sub-batches ("chunks") of a few
+// frames.  Three HIP streams -- H2D (c->pipe->h2d), encode (c->stream), D2H (c->pipe->d2h) --
+// with two device slots and two pinned host slots per direction: the H2D of chunk k+1, the encode
+// of chunk k and the D2H of chunk k-1 run at the same time (PCIe is full duplex).  Pinned caller
+// buffers (ie_host_alloc / hipHostMalloc / hipHostRegister) are DMA'd directly; pageable ones go
+// through the pinned slots with a multi-threaded host copy.
+
+bool is_pinned_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+// memcpy split over a few threads (a single core copies ~10 GB/s, PCIe moves ~50 GB/s).
+void par_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    constexpr size_t kPart = size_t(4) << 20;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t parts = std::min<size_t>(std::min<size_t>(hw, 8), (n + kPart - 1) / kPart);
+    if (parts <= 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = (n + parts - 1) / parts;
+    std::vector<std::thread> th;
+    th.reserve(parts - 1);
+    for (size_t i = 1; i < parts; i++) {
+        const size_t b = i * per, e = std::min(n, b + per);
+        if (b < e) th.emplace_back([=] { std::memcpy(dst + b, src + b, e - b); });
+    }
+    std::memcpy(dst, src, std::min(n, per));
+    for (auto& t : th) t.join();
+}
+
+}  // namespace
+
+struct ie_pipe {
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    hipEvent_t ev_h2d[2] = {}, ev_enc[2] = {}, ev_d2h[2] = {};
+    bool rec_enc[2] = {}, rec_d2h[2] = {}, rec_h2d[2] = {};
+    uint8_t* d_in[2] = {};
+    size_t cap_din[2] = {};
+    uint8_t* d_out[2] = {};
+    size_t cap_dout[2] = {};
+    uint8_t* h_in[2] = {};
+    size_t cap_hin[2] = {};
+    uint8_t* h_out[2] = {};
+    size_t cap_hout[2] = {};
+    uint64_t* h_ends = nullptr;    // pinned [2][kMaxChunk + 1]: images: each image's chain end;
+                                   // video chunks: the frame starts, then [kMaxChunk] the chain end
+    uint32_t* h_hdr = nullptr;     // pinned [2][kMaxChunk] header words (the word holding start_bit)
+    uint64_t* d_ends = nullptr;    // device [2]: chained launches read the previous end here
+};
+namespace {
+
+using Pipe = ie_pipe;
+constexpr int kMaxChunk = 64;
+
+int pipe_new(ie_ctx* c, Pipe*& P) {
+    P = new Pipe();
+    HIPCHK(c, hipStreamCreateWithFlags(&P->h2d, hipStreamNonBlocking));
+    HIPCHK(c, hipStreamCreateWithFlags(&P->d2h, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+        HIPCHK(c, hipEventCreateWithFlags(&P->ev_h2d[i], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&P->ev_enc[i], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&P->ev_d2h[i], hipEventDisableTiming));
+    }
+    HIPCHK(c, hipHostMalloc(&P->h_ends, 2 * (kMaxChunk + 1) * sizeof(uint64_t)));
+    HIPCHK(c, hipHostMalloc(&P->h_hdr, 2 * kMaxChunk * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&P->d_ends, 2 * sizeof(uint64_t)));
+    return IE_OK;
+}
+
+void pipe_free(Pipe* p) {
+    if (!p) return;
+    if (p->h2d) (void)hipStreamSynchronize(p->h2d);
+    if (p->d2h) (void)hipStreamSynchronize(p->d2h);
+    for (int i = 0; i < 2; i++) {
+        (void)hipFree(p->d_in[i]);
+        (void)hipFree(p->d_out[i]);
+        if (p->h_in[i]) (void)hipHostFree(p->h_in[i]);
+        if (p->h_out[i]) (void)hipHostFree(p->h_out[i]);
+        if (p->ev_h2d[i]) (void)hipEventDestroy(p->ev_h2d[i]);
+        if (p->ev_enc[i]) (void)hipEventDestroy(p->ev_enc[i]);
+        if (p->ev_d2h[i]) (void)hipEventDestroy(p->ev_d2h[i]);
+    }
+    if (p->h_ends) (void)hipHostFree(p->h_ends);
+    if (p->h_hdr) (void)hipHostFree(p->h_hdr);
+    (void)hipFree(p->d_ends);
+    if (p->h2d) (void)hipStreamDestroy(p->h2d);
+    if (p->d2h) (void)hipStreamDestroy(p->d2h);
+    delete p;
+}
+
+// The context's pipeline for streamed image batches; a new run starts with nothing pending (the
+// previous one ended with a full synchronisation).
+int pipe_get(ie_ctx* c, Pipe*& P) {
+    if (!c->pipe) {
+        int r = pipe_new(c, c->pipe);
+        if (r) {
+            pipe_free(c->pipe);
+            c->pipe = nullptr;
+            return r;
+        }
+    }
+    P = c->pipe;
+    for (int i = 0; i < 2; i++) P->rec_enc[i] = P->rec_d2h[i] = P->rec_h2d[i] = false;
+    return IE_OK;
+}
+
+// device / pinned slot buffers (a slot is only resized when nothing of this run uses it yet)
+int slot_dev(ie_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
+    if (cap >= need && p) return IE_OK;
+    if (p) HIPCHK(c, hipFree(p));
+    p = nullptr;
+    HIPCHK(c, hipMalloc(&p, need));
+    cap = need;
+    return IE_OK;
+}
+int slot_pinned(ie_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
+    if (cap >= need && p) return IE_OK;
+    if (p) HIPCHK(c, hipHostFree(p));
+    p = nullptr;
+    HIPCHK(c, hipHostMalloc(&p, need));
+    cap = need;
+    return IE_OK;
+}
+
+// frames per chunk: ~8 MiB of pixels (at least 1, at most kMaxChunk), and at least two chunks
+// (IE_CHUNK_MB overrides the target: a tuning aid, the output does not depend on it)
+int chunk_frames(size_t frame_bytes, int nframes) {
+    const char* e = getenv("IE_CHUNK_MB");
+    const size_t target = (e && atof(e) > 0) ? size_t(atof(e) * 1048576.0) : size_t(8) << 20;
+    int k = int(std::max<size_t>(1, target / std::max<size_t>(1, frame_bytes)));
+    k = std::min(k, kMaxChunk);
+    k = std::min(k, (nframes + 1) / 2);
+    return std::max(k, 1);
+}
+
+// Upload chunk `k` (frames f0 .. f0+nf-1) into device slot s on the H2D stream.
+int pipe_upload(ie_ctx* c, Pipe* P, int s, const uint8_t* y, size_t frame_pitch, size_t in_bytes, int f0,
+                bool pinned_in) {
+    // d_in[s] is free once the encode of the chunk that last used it is done
+    if (P->rec_enc[s]) HIPCHK(c, hipStreamWaitEvent(P->h2d, P->ev_enc[s], 0));
+    const uint8_t* src = y + size_t(f0) * frame_pitch;
+    if (pinned_in) {
+        HIPCHK(c, hipMemcpyAsync(P->d_in[s], src, in_bytes, hipMemcpyHostToDevice, P->h2d));
+    } else {
+        if (P->rec_h2d[s]) HIPCHK(c, hipEventSynchronize(P->ev_h2d[s]));  // h_in[s] drained
+        par_copy(P->h_in[s], src, in_bytes);
+        HIPCHK(c, hipMemcpyAsync(P->d_in[s], P->h_in[s], in_bytes, hipMemcpyHostToDevice, P->h2d));
+    }
+    HIPCHK(c, hipEventRecord(P->ev_h2d[s], P->h2d));
+    P->rec_h2d[s] = true;
+    return IE_OK;
+}
+
+int streamed_images(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
+                    int use_rle, int mode, uint8_t* out, size_t out_pitch, uint64_t start_bit, uint64_t* end_bits) {
+    // Three host threads keep the three streams busy: the uploader issues chunk k's H2D, this
+    // thread chunk k's encode, the downloader chunk k's stream D2H.  A copy from or to PAGEABLE
+    // memory is synchronous for its calling thread (the runtime stages it), so each direction has
+    // its own thread and both PCIe directions stay busy; pinned memory is DMA'd directly.
+    Pipe* P;
+    int r;
+    if ((r = pipe_get(c, P))) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int K = chunk_frames(stride * size_t(h), nframes);
+    const int nchunks = (nframes + K - 1) / K;
+    const size_t in_bytes = size_t(K - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
+    const uint64_t w0 = start_bit / 32;
+    const size_t b0 = size_t(start_bit / 8);
+    const size_t stage = out_pitch * size_t(K - 1) + (out_pitch - size_t(w0) * 4);  // slot: from word w0 of image 0
+    for (int s = 0; s < 2; s++) {
+        if ((r = slot_dev(c, P->d_in[s], P->cap_din[s], in_bytes))) return r;
+        if ((r = slot_dev(c, P->d_out[s], P->cap_dout[s], stage))) return r;
+    }
+    std::vector<uint64_t> ends(size_t(nframes), 0);
+    // hand-offs between the three threads: counters of chunks whose H2D / encode / D2H are
+    // issued, waited on by spinning (a condition variable's wake-up costs tens of microseconds
+    // per hand-off, several per chunk)
+    std::atomic<int> uploaded{0}, enqueued{0}, downloaded{0};
+    std::atomic<int> err{IE_OK};
+    std::mutex mu;
+    std::string msg;
+    auto set_err = [&](int code, const std::string& m) {
+        std::lock_guard<std::mutex> lk(mu);
+        int ok = IE_OK;
+        if (err.compare_exchange_strong(ok, code)) msg = m;
+    };
+    auto wait_for = [&](const std::atomic<int>& counter, int value) {  // false: another thread failed
+        while (counter.load(std::memory_order_acquire) < value) {
+            if (err.load(std::memory_order_relaxed) != IE_OK) return false;
+            std::this_thread::yield();
+        }
+        return err.load(std::memory_order_relaxed) == IE_OK;
+    };
+    auto publish = [&](std::atomic<int>& counter) { counter.fetch_add(1, std::memory_order_release); };
+#define TCHK(expr)                                                                   \
+    do {                                                                             \
+        hipError_t e_ = (expr);                                                      \
+        if (e_ != hipSuccess) {                                                      \
+            set_err(IE_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+            return;                                                                  \
+        }                                                                            \
+    } while (0)
+    // the three roles, per chunk
+    auto upload = [&](int k) {
+        const int s = k & 1, f0 = k * K, nf = std::min(K, nframes - f0);
+        if (!wait_for(enqueued, k - 1)) return;  // d_in[s]'s previous reader (chunk k-2) is launched
+        if (k >= 2) TCHK(hipStreamWaitEvent(P->h2d, P->ev_enc[s], 0));
+        const size_t ib = size_t(nf - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
+        TCHK(hipMemcpyAsync(P->d_in[s], y + size_t(f0) * frame_pitch, ib, hipMemcpyHostToDevice, P->h2d));
+        TCHK(hipEventRecord(P->ev_h2d[s], P->h2d));
+        publish(uploaded);
+    };
+    auto download = [&](int j) {
+        const int s = j & 1, f0 = j * K, nf = std::min(K, nframes - f0);
+        if (!wait_for(enqueued, j + 1)) return;
+        TCHK(hipEventSynchronize(P->ev_enc[s]));  // its end bits are in h_ends[s] (written by the encoder)
+        const uint64_t* he = P->h_ends + s * (kMaxChunk + 1);
+        for (int i = 0; i < nf; i++) {
+            const uint64_t e = he[i];
+            ends[size_t(f0 + i)] = e;
+            const size_t n = size_t((e + 7) / 8) - b0;
+            const uint8_t* src = P->d_out[s] + size_t(i) * out_pitch + (b0 - size_t(w0) * 4);
+            if (n) TCHK(hipMemcpyAsync(out + size_t(f0 + i) * out_pitch + b0, src, n, hipMemcpyDeviceToHost, P->d2h));
+        }
+        TCHK(hipEventRecord(P->ev_d2h[s], P->d2h));
+        publish(downloaded);
+    };
+    auto encode_chunk = [&](int k) {
+        const int s = k & 1, f0 = k * K, nf = std::min(K, nframes - f0);
+        // chunk k-2 (slot s) fully out: its streams downloaded (d_out[s]) and its ends read (h_ends[s])
+        if (!wait_for(uploaded, k + 1) || !wait_for(downloaded, k - 1)) return;
+        TCHK(hipStreamWaitEvent(c->stream, P->ev_h2d[s], 0));
+        if (k >= 2) TCHK(hipStreamWaitEvent(c->stream, P->ev_d2h[s], 0));
+        // each image's word holding start_bit (the caller's header bits), read by the device from
+        // page-locked memory (h_hdr[s] is free: chunk k-2's encode has completed)
+        uint32_t* hw = P->h_hdr + s * kMaxChunk;
+        for (int i = 0; i < nf; i++) std::memcpy(&hw[i], out + size_t(f0 + i) * out_pitch + size_t(w0) * 4, 4);
+        ie::launch_word_scatter(hw, reinterpret_cast<uint32_t*>(P->d_out[s]), out_pitch / 4, nf, c->stream);
+        Launch L;
+        L.dy = P->d_in[s];
+        L.w = w;
+        L.h = h;
+        L.stride = stride;
+        L.frame_pitch = frame_pitch;
+        L.nframes = nf;
+        L.use_rle = use_rle;
+        L.mode = mode;
+        L.dout = reinterpret_cast<uint32_t*>(P->d_out[s]) - w0;
+        L.out_pitch = out_pitch;
+        L.start_bit = start_bit;
+        L.segmented = 1;
+        // each image's end bit goes straight to page-locked host memory (no small SDMA read-back
+        // queued behind the stream downloads)
+        L.chain_end = P->h_ends + s * (kMaxChunk + 1);
+        const int rl = launch_chain(c, L);
+        if (rl != IE_OK) return set_err(rl, c->err);
+        TCHK(hipEventRecord(P->ev_enc[s], c->stream));
+        note_async(c, "streamed encode");
+        publish(enqueued);
+    };
+    if (is_pinned_ptr(y) && is_pinned_ptr(out)) {
+        // pinned both ways: every copy is asynchronous, one thread issues everything in order
+        for (int k = 0; k < nchunks && err.load() == IE_OK; k++) {
+            upload(k);
+            encode_chunk(k);
+            if (k >= 1) download(k - 1);
+        }
+        if (err.load() == IE_OK) download(nchunks - 1);
+    } else {
+        const int dev = c->device;
+        std::thread uploader([&] {
+            if (hipSetDevice(dev) != hipSuccess) return set_err(IE_EHIP, "hipSetDevice (uploader)");
+            for (int k = 0; k < nchunks && err.load() == IE_OK; k++) upload(k);
+        });
+        std::thread downloader([&] {
+            if (hipSetDevice(dev) != hipSuccess) return set_err(IE_EHIP, "hipSetDevice (downloader)");
+            for (int j = 0; j < nchunks && err.load() == IE_OK; j++) download(j);
+        });
+        for (int k = 0; k < nchunks && err.load() == IE_OK; k++) encode_chunk(k);
+        uploader.join();
+        downloader.join();
+    }
+#undef TCHK
+    (void)hipStreamSynchronize(P->h2d);
+    (void)hipStreamSynchronize(P->d2h);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (err.load() != IE_OK) return fail(c, err.load(), msg);
+    unsigned timeouts = 0;
+    r = read_errors(c, &timeouts, &c->last_fallbacks);
+    if (r == IE_EDEVICE || (r == IE_OK && timeouts)) {
+        // a tile look-back timed out (dispatch order did not hold): redo the batch through the
+        // staged path with ticket-ordered tiles
+        c->use_ticket = true;
+        return encode(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_pitch * size_t(nframes),
+                      out_pitch, start_bit, 1, nullptr, end_bits);
+    }
+    if (r) return r;
+    if (end_bits) std::memcpy(end_bits, ends.data(), ends.size() * sizeof(uint64_t));
+    return IE_OK;
+}
+
+}  // namespace
+
+// ---- streamed gop=1 video (ie_vstream_*) ----------------------------------------------------
+// One bit-contiguous chain (Frame.cpp:31-45, VideoEncoder.cpp:83-91) grown chunk by chunk on the
+// device: chunk k's launch starts at chunk k-1's chain end read on the device (start_dev), so the
+// host never waits for an encode before launching the next; the finished bytes leave through the
+// D2H stream while later chunks encode.
+struct ie_vstream {
+    ie_ctx* c = nullptr;
+    int w = 0, h = 0, rle = 1, mode = IE_MODE_FAST;
+    size_t stride = 0, frame_pitch = 0;
+    uint64_t start_bit = 0;
+    int max_frames = 0, frames = 0;  // capacity, frames pushed
+    int K = 1;                       // frames per chunk
+    uint8_t* d_stream = nullptr;     // the whole stream from byte 0 (the caller's head included)
+    size_t cap = 0;
+    int chunks = 0;                  // chunks launched
+    int harvested = 0;               // chunks whose frame starts / end are known on the host
+    uint64_t done_bits = 0;          // chain end of the last harvested chunk
+    uint64_t pulled = 0;             // bytes [0, pulled) handed out by ie_vstream_pull
+    int chunk_f0[2] = {}, chunk_nf[2] = {};
+    std::vector<uint64_t> fs;        // absolute start bit of every harvested frame
+    ie_pipe* P = nullptr;            // its own streams, events and slots
+};
+
+namespace {
+
+// The host side of chunk j (the oldest unharvested one): its frame starts and chain end.
+int vs_harvest(ie_vstream* v) {
+    ie_ctx* c = v->c;
+    Pipe* P = v->P;
+    const int j = v->harvested, s = j & 1;
+    HIPCHK(c, hipEventSynchronize(P->ev_enc[s]));
+    const uint64_t* hs = P->h_ends + s * (kMaxChunk + 1);
+    for (int i = 0; i < v->chunk_nf[s]; i++) v->fs[size_t(v->chunk_f0[s] + i)] = hs[i];
+    v->done_bits = hs[kMaxChunk];
+    v->harvested = j + 1;
+    return IE_OK;
+}
+
+// One chunk: upload, then a launch continuing the chain on the device.
+int vs_chunk(ie_vstream* v, const uint8_t* frames, int nf, bool pinned_in) {
+    ie_ctx* c = v->c;
+    Pipe* P = v->P;
+    const int k = v->chunks, s = k & 1;
+    while (k - v->harvested >= 2) {  // slot s's read-back area still holds chunk k-2's ends
+        int r = vs_harvest(v);
+        if (r) return r;
+    }
+    const size_t ib = size_t(nf - 1) * v->frame_pitch + v->stride * size_t(v->h - 1) + size_t(v->w);
+    int r;
+    if ((r = pipe_upload(c, P, s, frames, v->frame_pitch, ib, 0, pinned_in))) return r;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, P->ev_h2d[s], 0));
+    Launch L;
+    L.dy = P->d_in[s];
+    L.w = v->w;
+    L.h = v->h;
+    L.stride = v->stride;
+    L.frame_pitch = v->frame_pitch;
+    L.nframes = nf;
+    L.use_rle = v->rle;
+    L.mode = v->mode;
+    L.dout = reinterpret_cast<uint32_t*>(v->d_stream);
+    L.start_bit = v->start_bit;
+    L.start_dev = k ? P->d_ends + ((k - 1) & 1) : nullptr;
+    L.chain_end = P->d_ends + s;
+    if ((r = launch_chain(c, L))) return r;
+    uint64_t* hs = P->h_ends + s * (kMaxChunk + 1);
+    HIPCHK(c, hipMemcpyAsync(hs, c->d_frame_start, size_t(nf) * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(hs + kMaxChunk, P->d_ends + s, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(P->ev_enc[s], c->stream));
+    P->rec_enc[s] = true;
+    note_async(c, "streamed video encode");
+    v->chunk_f0[s] = v->frames;
+    v->chunk_nf[s] = nf;
+    v->frames += nf;
+    v->chunks = k + 1;
+    return IE_OK;
+}
+
+// Copy stream bytes [v->pulled, b1) to dst (host, pinned or pageable) through the D2H stream:
+// pinned destinations directly, pageable ones in 16 MiB pieces through two pinned slots (the
+// host copies piece i out while piece i+1 is in flight).
+int vs_copy_out(ie_vstream* v, uint8_t* dst, uint64_t b1) {
+    ie_ctx* c = v->c;
+    Pipe* P = v->P;
+    if (b1 <= v->pulled) return IE_OK;
+    const size_t n = size_t(b1 - v->pulled);
+    const uint8_t* src = v->d_stream + v->pulled;
+    // the bytes were written by the launches up to the last harvested chunk (on c->stream)
+    HIPCHK(c, hipStreamWaitEvent(P->d2h, P->ev_enc[(v->harvested - 1) & 1], 0));
+    if (is_pinned_ptr(dst)) {
+        HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, P->d2h));
+        HIPCHK(c, hipStreamSynchronize(P->d2h));
+    } else {
+        constexpr size_t kPiece = size_t(16) << 20;
+        int r;
+        for (int s = 0; s < 2; s++)
+            if ((r = slot_pinned(c, P->h_out[s], P->cap_hout[s], std::min(n, kPiece)))) return r;
+        const size_t pieces = (n + kPiece - 1) / kPiece;
+        for (size_t i = 0; i <= pieces; i++) {
+            if (i < pieces) {  // slot i&1 was emptied at step i-1
+                const size_t o = i * kPiece, len = std::min(kPiece, n - o);
+                HIPCHK(c, hipMemcpyAsync(P->h_out[i & 1], src + o, len, hipMemcpyDeviceToHost, P->d2h));
+                HIPCHK(c, hipEventRecord(P->ev_d2h[i & 1], P->d2h));
+            }
+            if (i >= 1) {
+                const size_t j = i - 1, o = j * kPiece, len = std::min(kPiece, n - o);
+                HIPCHK(c, hipEventSynchronize(P->ev_d2h[j & 1]));
+                par_copy(dst + o, P->h_out[j & 1], len);
+            }
+        }
+    }
+    v->pulled = b1;
+    return IE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ie_vstream_open(ie_ctx* c, int w, int h, size_t stride, size_t frame_pitch, int use_rle, int mode,
+                    const uint8_t* head, uint64_t start_bit, int max_frames, ie_vstream** out) {
+    if (!c || !out || max_frames <= 0 || (start_bit && !head)) return IE_EINVAL;
+    *out = nullptr;
+    int r = check_dims(c, w, h, max_frames);
+    if (r) return r;
+    if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
+    if (frame_pitch < stride * size_t(h - 1) + size_t(w)) return fail(c, IE_EINVAL, "frame_pitch smaller than a frame");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    ie_vstream* v = new ie_vstream();
+    if ((r = pipe_new(c, v->P))) {
+        pipe_free(v->P);
+        delete v;
+        return r;
+    }
+    Pipe* P = v->P;
+    v->c = c;
+    v->w = w;
+    v->h = h;
+    v->stride = stride;
+    v->frame_pitch = frame_pitch;
+    v->rle = use_rle ? 1 : 0;
+    v->mode = mode;
+    v->start_bit = start_bit;
+    v->max_frames = max_frames;
+    v->K = chunk_frames(stride * size_t(h), 1 << 20);
+    v->fs.assign(size_t(max_frames), 0);
+    v->done_bits = start_bit;
+    v->cap = ie_stream_bound(w, h, c->n, max_frames, start_bit);
+    const size_t in_bytes = size_t(v->K - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
+    auto bad = [&](int code) {
+        (void)hipFree(v->d_stream);
+        pipe_free(v->P);
+        delete v;
+        return code;
+    };
+    if (hipMalloc(&v->d_stream, v->cap) != hipSuccess) return bad(fail(c, IE_EHIP, "hipMalloc(video stream)"));
+    for (int s = 0; s < 2; s++) {
+        if ((r = slot_dev(c, P->d_in[s], P->cap_din[s], in_bytes))) return bad(r);
+        if ((r = slot_pinned(c, P->h_in[s], P->cap_hin[s], in_bytes))) return bad(r);
+    }
+    // the caller's head: bytes [0, ceil(start_bit/8)), bits from start_bit on cleared; the word
+    // holding start_bit is completed by the first chunk's first tile
+    const size_t hb = size_t((start_bit + 7) / 8);
+    std::vector<uint8_t> hd(hb + 8, 0);
+    if (hb) std::memcpy(hd.data(), head, hb);
+    if (start_bit % 8) hd[hb - 1] &= uint8_t(0xFF00u >> (start_bit % 8));
+    if (hipMemsetAsync(v->d_stream, 0, std::min(v->cap, hb + 8), c->stream) != hipSuccess ||
+        (hb && hipMemcpyAsync(v->d_stream, hd.data(), hb, hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return bad(fail(c, IE_EHIP, "video stream head upload"));
+    *out = v;
+    return IE_OK;
+}
+
+int ie_vstream_push(ie_vstream* v, const uint8_t* frames, int nframes) {
+    if (!v || (!frames && nframes)) return IE_EINVAL;
+    ie_ctx* c = v->c;
+    if (nframes < 0 || v->frames + nframes > v->max_frames)
+        return fail(c, IE_ECAP, "more frames pushed than ie_vstream_open's max_frames");
+    if (ie_is_device_ptr(frames)) return fail(c, IE_EINVAL, "ie_vstream_push takes host frames");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool pinned = is_pinned_ptr(frames);
+    for (int f = 0; f < nframes; f += v->K) {
+        const int r = vs_chunk(v, frames + size_t(f) * v->frame_pitch, std::min(v->K, nframes - f), pinned);
+        if (r) return r;
+    }
+    return IE_OK;
+}
+
+int ie_vstream_pull(ie_vstream* v, uint8_t* dst, size_t cap, size_t* nbytes) {
+    if (!v || !nbytes || (!dst && cap)) return IE_EINVAL;
+    *nbytes = 0;
+    // every chunk but the newest is complete or nearly so: harvest them (the newest keeps encoding)
+    while (v->harvested < v->chunks - 1) {
+        const int r = vs_harvest(v);
+        if (r) return r;
+    }
+    const uint64_t b1 = v->done_bits / 8;  // whole bytes (the partial one follows with the next chunk)
+    if (b1 <= v->pulled) return IE_OK;
+    if (b1 - v->pulled > cap) return fail(v->c, IE_ECAP, "pull buffer smaller than the finished bytes");
+    const uint64_t b0 = v->pulled;
+    const int r = vs_copy_out(v, dst, b1);
+    if (r) return r;
+    *nbytes = size_t(b1 - b0);
+    return IE_OK;
+}
+
+int ie_vstream_finish(ie_vstream* v, uint8_t* dst, size_t cap, size_t* nbytes, uint64_t* end_bit,
+                      uint64_t* frame_bits) {
+    if (!v || (!dst && cap)) return IE_EINVAL;
+    ie_ctx* c = v->c;
+    if (nbytes) *nbytes = 0;
+    int r;
+    while (v->harvested < v->chunks)
+        if ((r = vs_harvest(v))) return r;
+    unsigned timeouts = 0;
+    if ((r = read_errors(c, &timeouts, &c->last_fallbacks))) return r;
+    if (timeouts) return fail(c, IE_EDEVICE, "tile look-back timed out in a streamed video chunk");
+    const uint64_t end = v->done_bits, b1 = (end + 7) / 8;
+    if (dst) {
+        if (b1 - v->pulled > cap) return fail(c, IE_ECAP, "finish buffer smaller than the remaining bytes");
+        const uint64_t b0 = v->pulled;
+        if ((r = vs_copy_out(v, dst, b1))) return r;
+        if (nbytes) *nbytes = size_t(b1 - b0);
+    }
+    if (end_bit) *end_bit = end;
+    if (frame_bits)
+        for (int f = 0; f < v->frames; f++)
+            frame_bits[f] = ((f + 1 < v->frames) ? v->fs[size_t(f + 1)] : end) - v->fs[size_t(f)];
+    return IE_OK;
+}
+
+const uint8_t* ie_vstream_device(const ie_vstream* v) { return v ? v->d_stream : nullptr; }
+
+int ie_vstream_close(ie_vstream* v) {
+    if (!v) return IE_OK;
+    ie_ctx* c = v->c;
+    (void)hipStreamSynchronize(c->stream);
+    pipe_free(v->P);
+    (void)hipFree(v->d_stream);
+    delete v;
+    return IE_OK;
+}
+
+int ie_host_alloc(ie_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return IE_EINVAL;
+    *out = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipHostMalloc(out, bytes ? bytes : 4));
+    return IE_OK;
+}
+
+int ie_host_free(ie_ctx* c, void* p) {
+    if (!c) return IE_EINVAL;
+    if (!p) return IE_OK;
+    HIPCHK(c, hipHostFree(p));
+    return IE_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// ie_encode_frames with host frames and a host stream: the video stream pipeline, pulled into the
+// caller's buffer as the chunks finish.
+int streamed_frames(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
+                    int use_rle, int mode, uint8_t* out, size_t out_cap, uint64_t start_bit, uint64_t* frame_bits,
+                    uint64_t* end_bit) {
+    ie_vstream* v = nullptr;
+    int r = ie_vstream_open(c, w, h, stride, frame_pitch, use_rle, mode, out, start_bit, nframes, &v);
+    if (r) return r;
+    size_t got = 0;
+    for (int f = 0; f < nframes && r == IE_OK; f += v->K) {
+        const int nf = std::min(v->K, nframes - f);
+        if ((r = ie_vstream_push(v, y + size_t(f) * frame_pitch, nf))) break;
+        const uint64_t b0 = v->pulled;
+        if ((r = ie_vstream_pull(v, out + b0, out_cap - size_t(b0), &got))) break;
+    }
+    uint64_t end = 0;
+    if (r == IE_OK) {
+        const uint64_t b0 = v->pulled;
+        r = ie_vstream_finish(v, out + b0, out_cap - size_t(b0), &got, &end, frame_bits);
+    }
+    ie_vstream_close(v);
+    if (r == IE_EDEVICE && !c->use_ticket) {  // a look-back timeout: redo through the staged path
+        c->use_ticket = true;
+        return encode(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_cap, 0, start_bit, 0,
+                      frame_bits, end_bit);
+    }
+    if (r) return r;
+    if (end_bit) *end_bit = end;
+    return IE_OK;
+}
+
 
 // Variable-length re-encode of n bytes (Huffman.cpp:314-319) into one stream from start_bit.
 int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const uint8_t* len, uint8_t* out,
@@ -757,6 +1430,7 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_hout);
     (void)hipFree(c->d_pix);
     (void)hipFree(c->d_coef);
+    pipe_free(c->pipe);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
     return IE_OK;

@@ -71,6 +71,7 @@ struct EncArgs {
     uint32_t* out;           // 4-byte aligned, word w = stream bytes [4w, 4w+4)
     uint64_t out_pitch_words;
     uint64_t start_bit;
+    const uint64_t* start_dev;  // non-null: the chain starts at *start_dev (device; overrides start_bit)
     uint64_t* st;            // [3*ntiles] tile chain granules (ie_common.hpp)
     unsigned long long* ticket;  // nullptr: tiles in blockIdx order; else an atomic ticket
     unsigned long long ticket_base;
@@ -95,7 +96,8 @@ constexpr int kStamps = 16;
 // chain-state words per tile (the host allocates; ie_common.hpp kGran must not exceed it)
 constexpr int kStateWordsPerTile = 16;
 void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s);
-int encode_blocks_per_thread(int n);  // horizontally adjacent blocks per lane (Geo<N>::BPT)
+int encode_blocks_per_thread(int n);
+void launch_word_scatter(const uint32_t* src, uint32_t* dst, uint64_t pitch_words, int n, hipStream_t s);  // horizontally adjacent blocks per lane (Geo<N>::BPT)
 int encode_threads_per_tile();       // threads per encoder workgroup (= tile)
 
 struct PackArgs {            // Huffman re-encode / bit copy: one variable-length code per byte

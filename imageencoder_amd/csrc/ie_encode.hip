@@ -690,6 +690,9 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         for (int i = tid; i < 3 * NN + 9; i += TPB) srow[i] = tab->srow[i];
     }
     const TileGeo g = tile_geo<N>(a, t, tid);
+    // the chain's first bit: the host's value, or (streamed video, ie_vstream_*) the previous
+    // launch's chain end on the device, written before this launch started (stream order)
+    const uint64_t start_bit = a.start_dev ? *a.start_dev : a.start_bit;
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
     constexpr bool kLdsPix = IE_LDS_PIX && N == 4 && !EXACT;
@@ -1173,11 +1176,11 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         lds_barrier();
         excl = uint64_t(tif) * (110u * TPB);
     } else {
-        excl = chain_resolve(a.st, t, chain_pos, step, a.tag, img, A, out, a.start_bit, a.err, ctl, pr,
+        excl = chain_resolve(a.st, t, chain_pos, step, a.tag, img, A, out, start_bit, a.err, ctl, pr,
                              stamps ? &stamps[size_t(t) * kStamps + 1] : nullptr, true);
     }
     if (tid == 0) {
-        const uint64_t P = a.start_bit + excl;
+        const uint64_t P = start_bit + excl;
         if (tif == 0) a.frame_start[frame] = P;
         if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
     }
@@ -1187,21 +1190,34 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     // ---------------------------------------------------------------- 4. store
     if constexpr (HIST) {
         if (tif == 0)  // the words before the first record word hold only the caller's header
-            for (uint32_t i = tid; i < uint32_t(a.start_bit >> 5); i += TPB) {
+            for (uint32_t i = tid; i < uint32_t(start_bit >> 5); i += TPB) {
                 const uint32_t v = out[i];
 #pragma unroll
                 for (int k = 0; k < 4; k++) atomicAdd(&hl[(v >> (8 * k)) & 0xFFu], 1u);
             }
-        const uint64_t end = a.start_bit + excl + A;
+        const uint64_t end = start_bit + excl + A;
         const HistCount cnt{hl, chain_last ? (end + 7) / 8 : ~0ull};
-        store_tile<TPB>(out, img, A, a.start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err, cnt);
+        store_tile<TPB>(out, img, A, start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err, cnt);
         lds_barrier();
         for (int i = tid; i < 256; i += TPB)
             if (hl[i]) atomicAdd(&a.hist[size_t(frame) * 256 + i], hl[i]);
     } else if (!(ablate & 8)) {
-        store_tile<TPB>(out, img, A, a.start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err);
+        store_tile<TPB>(out, img, A, start_bit + excl, ctl, chain_last, a.st, t - step, a.tag, a.err);
     }
     STAMP(9);
+}
+
+// The streamed host path's per-image header words: word i (read from page-locked host memory
+// the device maps, one PCIe read per image) to dst[i * pitch_words] -- instead of an SDMA copy
+// that would queue behind the chunk's pixel upload on the copy engine.
+__global__ void word_scatter_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint64_t pitch_words,
+                                    int n) {
+    const int i = int(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) dst[size_t(i) * pitch_words] = src[i];
+}
+
+void launch_word_scatter(const uint32_t* src, uint32_t* dst, uint64_t pitch_words, int n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(word_scatter_kernel, dim3(unsigned((n + 63) / 64)), dim3(64), 0, s, src, dst, pitch_words, n);
 }
 
 int encode_blocks_per_thread(int n) { return n == 4 ? Geo<4>::BPT : Geo<8>::BPT; }

@@ -125,6 +125,38 @@ int ie_memset(ie_ctx* ctx, void* dst, int value, size_t bytes);
 /* 1 if p is device (hipMalloc) memory, 0 otherwise. */
 int ie_is_device_ptr(const void* p);
 
+/* ---- Streamed host path (the reference reads / writes whole files: utils.hpp:352-402,
+ * VideoBase.cpp:6-19) -------------------------------------------------------------------------
+ * ie_encode_images / ie_encode_frames with host frames AND a host stream buffer and nframes > 1
+ * stream the batch through the device in chunks of a few frames: the H2D of chunk k+1, the encode
+ * of chunk k and the D2H of chunk k-1 run concurrently on three HIP streams (PCIe full duplex),
+ * through two device and two pinned host slots per direction.  Pinned caller buffers are DMA'd
+ * directly, pageable ones through the pinned slots.  Page-locked host memory for such buffers: */
+int ie_host_alloc(ie_ctx* ctx, size_t bytes, void** out);
+int ie_host_free(ie_ctx* ctx, void* p);
+
+/* Streamed gop=1 video payload (Frame.cpp:31-45 / VideoEncoder.cpp:83-91 for frames that arrive
+ * over time, e.g. read from a .raw/YUV420 file chunk by chunk): ONE bit-contiguous stream grown on
+ * the device.  open: `head` holds the caller's bytes [0, ceil(start_bit/8)) (the settings header;
+ * bits from start_bit on are ignored), max_frames bounds the device stream.  push: host frames
+ * (frame f row r at frames + f*frame_pitch + r*stride), copied and encoded asynchronously, each
+ * chunk continuing the chain from the previous chunk's end ON THE DEVICE (no host round trip).
+ * pull: the whole bytes finished so far that were not pulled yet (from byte 0, the head included)
+ * into dst (*nbytes of them), while later chunks still encode.  finish: waits, checks the device
+ * error counters, copies the remaining bytes (last byte zero-padded) to dst when dst != NULL, and
+ * returns the end bit and optionally each frame's payload bits.  ie_vstream_device: the device
+ * stream (valid until close; complete after finish), e.g. for the device Huffman pass.  One open
+ * stream per context at a time; other calls on the context between pushes are allowed. */
+typedef struct ie_vstream ie_vstream;
+int ie_vstream_open(ie_ctx* ctx, int w, int h, size_t stride, size_t frame_pitch, int use_rle, int mode,
+                    const uint8_t* head, uint64_t start_bit, int max_frames, ie_vstream** out);
+int ie_vstream_push(ie_vstream* v, const uint8_t* frames, int nframes);
+int ie_vstream_pull(ie_vstream* v, uint8_t* dst, size_t cap, size_t* nbytes);
+int ie_vstream_finish(ie_vstream* v, uint8_t* dst, size_t cap, size_t* nbytes, uint64_t* end_bit,
+                      uint64_t* frame_bits);
+const uint8_t* ie_vstream_device(const ie_vstream* v);
+int ie_vstream_close(ie_vstream* v);
+
 /* ---- Huffman post-pass (config 5; Huffman.cpp:233-344) ----------------------------------
  * hist[b] = occurrences of byte value b; first_pos[b] = index of its first occurrence
  * (UINT64_MAX if absent).  The first-occurrence order is the insertion order of the reference's
