@@ -124,6 +124,82 @@ int encode_file(ie_ctx* c, const uint8_t* y, const FileParams& p, std::vector<ui
     return IE_OK;
 }
 
+// A gop=1 video file encoded while it is read: frame chunks go from the .raw/YUV420 file into two
+// page-locked buffers in turn (VideoBase.cpp:6-19 and utils.hpp:352-376 read the whole file
+// first), each chunk is pushed to an ie_vstream -- copied to the device and encoded behind the
+// previous chunk on the device's chain -- while the host reads the next one, and the finished
+// bytes are pulled out as the chunks complete.  With Huffman the stream stays on the device for
+// the Huffman pass over the whole file (Huffman.cpp:233-344 needs every byte's count first).
+int encode_video_streamed(ie_ctx* c, const std::string& path, const FileParams& p, std::vector<uint8_t>& out,
+                          std::string& err) {
+    if (!c) return (err = "no GPU context", IE_EHIP);
+    int r;
+    if ((r = ie_set_quant(c, p.q, p.n))) return (err = ie_last_error(c), r);
+    util::BitStreamWriter hdr(64);
+    write_header(hdr, p);
+    const uint64_t H = hdr.get_position();
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return (err = "Could not read file '" + path + "'", IE_EINVAL);
+    ie_vstream* v = nullptr;
+    if ((r = ie_vstream_open(c, p.w, p.h, size_t(p.w), p.frame_pitch, p.rle ? 1 : 0, p.mode, hdr.get_buffer(), H,
+                             p.frames, &v))) {
+        std::fclose(f);
+        return (err = ie_last_error(c), r);
+    }
+    // ~32 MiB of frames per read (IE_CHUNK_MB: a tuning aid; the output does not depend on it)
+    const char* ce = std::getenv("IE_CHUNK_MB");
+    const size_t target = (ce && std::atof(ce) > 0) ? size_t(std::atof(ce) * 1048576.0) : (size_t(32) << 20);
+    const int K = int(std::max<size_t>(1, std::min<size_t>(size_t(p.frames), target / p.frame_pitch)));
+    uint8_t* buf[2] = {nullptr, nullptr};
+    for (int i = 0; i < 2 && r == IE_OK; i++) {
+        void* b = nullptr;
+        r = ie_host_alloc(c, size_t(K) * p.frame_pitch, &b);
+        buf[i] = static_cast<uint8_t*>(b);
+    }
+    if (!p.huffman) out.assign(ie_stream_bound(p.w, p.h, p.n, p.frames, H), 0);
+    size_t got = 0, nb = 0;
+    auto read_chunk = [&](int i, int nf) {
+        return std::fread(buf[i], p.frame_pitch, size_t(nf), f) == size_t(nf);
+    };
+    int f0 = 0, slot = 0;
+    int nf = std::min(K, p.frames);
+    if (r == IE_OK && !read_chunk(0, nf)) r = (err = "short read of '" + path + "'", IE_EINVAL);
+    while (r == IE_OK && f0 < p.frames) {
+        // the push DMAs from buf[slot] asynchronously; buf[slot^1] was released by this push
+        if ((r = ie_vstream_push(v, buf[slot], nf))) break;
+        const int f1 = f0 + nf, nf1 = std::min(K, p.frames - f1);
+        if (nf1 > 0 && !read_chunk(slot ^ 1, nf1)) {
+            r = (err = "short read of '" + path + "'", IE_EINVAL);
+            break;
+        }
+        if (!p.huffman && (r = ie_vstream_pull(v, out.data() + got, out.size() - got, &nb))) break;
+        got += nb;
+        f0 = f1;
+        nf = nf1;
+        slot ^= 1;
+    }
+    uint64_t end = 0;
+    if (r == IE_OK)
+        r = p.huffman ? ie_vstream_finish(v, nullptr, 0, nullptr, &end, nullptr)
+                      : ie_vstream_finish(v, out.data() + got, out.size() - got, &nb, &end, nullptr);
+    if (r == IE_OK && !p.huffman) out.resize(got + nb);
+    if (r == IE_OK && p.huffman) {
+        Scratch& s = scratch(c);
+        const int64_t hl = algo::huffman_device(c, ie_vstream_device(v), size_t((end + 7) / 8), s.huf, err);
+        if (hl < 0) r = int(hl);
+        else {
+            out.resize(size_t(hl));
+            if ((r = ie_memcpy(c, out.data(), s.huf.p, size_t(hl)))) err = ie_last_error(c);
+        }
+    } else if (r != IE_OK && err.empty()) {
+        err = ie_last_error(c);
+    }
+    ie_vstream_close(v);
+    for (uint8_t* b : buf) ie_host_free(c, b);
+    std::fclose(f);
+    return r;
+}
+
 // Parse a (Huffman-decoded) image or video stream header.  Returns false on a short stream.
 struct StreamHeader {
     std::vector<uint16_t> q;
@@ -242,21 +318,25 @@ VideoProcessor::VideoProcessor(const std::string& src, const std::string& dst, u
                                QuantSpec quant, uint16_t g, uint16_t mer)
     : width(w), height(h), gop(g ? g : 1), merange(mer), use_rle(rle), quant_m(std::move(quant)), source_file(src),
       dest_file(dst) {
-    if (!read_file(source_file, raw)) err_ = "Could not read file '" + source_file + "'";
+    // (VideoBase.cpp:6-19 reads the whole file here; the encoder streams it in process())
+    std::ifstream f(source_file, std::ios::binary | std::ios::ate);
+    if (!f) err_ = "Could not read file '" + source_file + "'";
+    else raw_size = size_t(f.tellg());
 }
 
 VideoProcessor::VideoProcessor(const std::string& src, const std::string& dst, const bool& mc)
     : motioncomp(mc), source_file(src), dest_file(dst) {
     if (!read_file(source_file, raw)) err_ = "Could not read file '" + source_file + "'";
+    raw_size = raw.size();
 }
 
 void VideoProcessor::saveResult(bool encoded) const {
     if (!write_file(dest_file, result_)) util::Logger::WriteLn("[VideoProcessor] Could not write '" + dest_file + "'");
     if (encoded) {
-        util::Logger::WriteLn(fmt("[VideoProcessor] Original file size: %8.0f bytes", double(raw.size())));
+        util::Logger::WriteLn(fmt("[VideoProcessor] Original file size: %8.0f bytes", double(raw_size)));
         util::Logger::WriteLn(fmt("[VideoProcessor]       Encoded size: %8.0f bytes  => Ratio: %.2f%%",
                                   double(result_.size()),
-                                  raw.empty() ? 0.0 : 100.0 * double(result_.size()) / double(raw.size())));
+                                  raw_size ? 100.0 * double(result_.size()) / double(raw_size) : 0.0));
     }
     util::Logger::WriteLn("[VideoProcessor] Saved file at: " + dest_file);
 }
@@ -269,7 +349,7 @@ bool VideoEncoder::process() {
     if (width % n || height % n) return (err_ = "width and height must be multiples of the block size", false);
     if (gop != 1) return (err_ = "P-frames (gop > 1) need motion estimation, which this encoder does not provide", false);
     const size_t pitch = size_t(width) * height + size_t(width) * height / 2;  // Y + UV (VideoBase.cpp:8-9)
-    const size_t frames = pitch ? raw.size() / pitch : 0;
+    const size_t frames = pitch ? raw_size / pitch : 0;
     if (frames == 0 || frames > 32767) return (err_ = "frame count must be in 1..32767", false);
     FileParams p;
     p.w = width;
@@ -284,7 +364,7 @@ bool VideoEncoder::process() {
     p.gop = gop;
     p.merange = merange;
     p.frame_pitch = pitch;
-    return encode_file(Device::get(), raw.data(), p, result_, err_) == IE_OK;
+    return encode_video_streamed(Device::get(), source_file, p, result_, err_) == IE_OK;
 }
 
 // ------------------------------------------------------------------------------- VideoDecoder

@@ -71,5 +71,8 @@ void write_header(util::BitStreamWriter& hdr, const FileParams& p);
 // Encode into `out` (host).  y may be host or device memory.  Returns IE_OK or an IE_E* code
 // with the reason in `err`.
 int encode_file(ie_ctx* c, const uint8_t* y, const FileParams& p, std::vector<uint8_t>& out, std::string& err);
+// A video file encoded while it is read from `path` (ie_vstream; see codec.cpp).
+int encode_video_streamed(ie_ctx* c, const std::string& path, const FileParams& p, std::vector<uint8_t>& out,
+                          std::string& err);
 
 }  // namespace dc

@@ -1158,6 +1158,8 @@ int ie_vstream_push(ie_vstream* v, const uint8_t* frames, int nframes) {
         return fail(c, IE_ECAP, "more frames pushed than ie_vstream_open's max_frames");
     if (ie_is_device_ptr(frames)) return fail(c, IE_EINVAL, "ie_vstream_push takes host frames");
     HIPCHK(c, hipSetDevice(c->device));
+    // the previous push's pinned frames may still be in flight: they are released now
+    HIPCHK(c, hipStreamSynchronize(v->P->h2d));
     const bool pinned = is_pinned_ptr(frames);
     for (int f = 0; f < nframes; f += v->K) {
         const int r = vs_chunk(v, frames + size_t(f) * v->frame_pitch, std::min(v->K, nframes - f), pinned);

@@ -140,7 +140,9 @@ int ie_host_free(ie_ctx* ctx, void* p);
  * the device.  open: `head` holds the caller's bytes [0, ceil(start_bit/8)) (the settings header;
  * bits from start_bit on are ignored), max_frames bounds the device stream.  push: host frames
  * (frame f row r at frames + f*frame_pitch + r*stride), copied and encoded asynchronously, each
- * chunk continuing the chain from the previous chunk's end ON THE DEVICE (no host round trip).
+ * chunk continuing the chain from the previous chunk's end ON THE DEVICE (no host round trip);
+ * pageable frames may be reused when push returns, pinned ones are DMA'd asynchronously and may
+ * be reused once the NEXT push (or finish) returns (double-buffered readers alternate two).
  * pull: the whole bytes finished so far that were not pulled yet (from byte 0, the head included)
  * into dst (*nbytes of them), while later chunks still encode.  finish: waits, checks the device
  * error counters, copies the remaining bytes (last byte zero-padded) to dst when dst != NULL, and

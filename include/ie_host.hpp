@@ -275,7 +275,10 @@ protected:
     bool use_rle = true, motioncomp = false;
     QuantSpec quant_m;
     std::string source_file, dest_file;
+    // the decoder reads its (encoded) input whole; the encoder STREAMS its .raw/YUV420 input
+    // (VideoEncoder::process reads it frame chunk by frame chunk), so raw stays empty there
     std::vector<uint8_t> raw, result_;
+    size_t raw_size = 0;  // input file size
     std::string err_;
 };
 
