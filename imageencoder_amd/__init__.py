@@ -99,6 +99,8 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.ie_vstream_device.argtypes = [vp]
     L.ie_vstream_device.restype = C.c_void_p
     L.ie_vstream_close.argtypes = [vp]
+    L.ie_huffman_decode.argtypes = [vp, u8p, C.c_size_t, C.c_uint64, vp, u8p, C.c_size_t, C.POINTER(C.c_size_t)]
+    L.ie_last_decode_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.ie_malloc.argtypes = [vp, C.c_size_t, C.POINTER(C.c_void_p)]
     L.ie_free.argtypes = [vp, vp]
     L.ie_memcpy.argtypes = [vp, vp, vp, C.c_size_t]
@@ -126,6 +128,8 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
     H.ieh_decode_video.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip, ip]
     H.ieh_huffman_encode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t]
     H.ieh_huffman_decode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, ip]
+    H.ieh_huffman_table.argtypes = [vp, C.c_size_t, vp, C.POINTER(C.c_uint64)]
+    H.ieh_huffman_table.restype = C.c_int
     H.ieh_huffman_encode_after_encode.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, vp]
     H.ieh_huffman_encode_after_encode.restype = C.c_int
     H.ieh_huffman_begin_after_encode.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_int]
@@ -375,6 +379,13 @@ class Codec:
         src = self.L.ie_last_end_bits(self.h)
         self._chk(self.L.ie_memcpy(self.h, C.c_void_p(_ptr(dst)), C.c_void_p(src), 8 * count))
 
+    def last_decode_info(self) -> tuple[bool, int]:
+        """(fused, rounds) of the last decode: the one-launch path, or the multi-kernel fallback
+        with its fix-up rounds."""
+        f, r = C.c_int(0), C.c_int(0)
+        self._chk(self.L.ie_last_decode_info(self.h, C.byref(f), C.byref(r)))
+        return bool(f.value), int(r.value)
+
     def last_fallbacks(self) -> int:
         v = C.c_uint64(0)
         self._chk(self.L.ie_last_fallbacks(self.h, C.byref(v)))
@@ -523,6 +534,26 @@ class Codec:
         first = np.zeros((count, 256), dtype=np.uint64)
         self._chk(self.L.ie_huffman_hist_batch_wait(self.h, 0, hist.ctypes.data, first.ctypes.data))
         return hist, first
+
+    def huffman_table(self, data: bytes):
+        """(lut uint16[32768], start_bit) of a Huffman-coded stream's dictionary, or None when the
+        stream has none (passthrough)."""
+        H = load_host_library()
+        src = np.frombuffer(data, dtype=np.uint8)
+        lut = np.zeros(32768, dtype=np.uint16)
+        sb = C.c_uint64(0)
+        r = H.ieh_huffman_table(src.ctypes.data, src.size, lut.ctypes.data, C.byref(sb))
+        if r < 0:
+            raise IEError(r, "ieh_huffman_table")
+        return None if r == 1 else (lut, int(sb.value))
+
+    def huffman_decode_device(self, stream, nbytes: int, lut, start_bit: int, out) -> int:
+        """ie_huffman_decode with device-resident stream / table / output (torch tensors): the
+        symbol count (raises on IE_ECAP / malformed streams)."""
+        n = C.c_size_t(0)
+        self._chk(self.L.ie_huffman_decode(self.h, _ptr(stream), nbytes, start_bit, _ptr(lut), _ptr(out),
+                                           _nbytes(out), C.byref(n)))
+        return int(n.value)
 
     def huffman_decode(self, data: bytes):
         """The Huffman decode alone (device bit walk): (decoded bytes, passthrough)."""

@@ -539,6 +539,18 @@ void ieh_release(ie_ctx* c) {
 
 // The Huffman decode alone (Huffman.cpp:354-402): returns the decoded byte count, or 0 with
 // *passthrough = 1 for a stream without a dictionary; IE_ECAP if cap is too small.
+// The dictionary of a Huffman-coded stream as the device decode's prefix table (32768 entries) and
+// the code stream's first bit; returns 1 when the stream carries no dictionary (passthrough).
+int ieh_huffman_table(const uint8_t* in, size_t n, uint16_t* lut, uint64_t* start_bit) {
+    if ((!in && n) || !lut || !start_bit) return IE_EINVAL;
+    bool pass = false;
+    size_t from = 0;
+    const int r = algo::Huffman::decode_table(in, n, lut, pass, from);
+    if (r) return r;
+    *start_bit = from;
+    return pass ? 1 : 0;
+}
+
 int64_t ieh_huffman_decode(ie_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap, int* passthrough) {
     if (!c || (!in && n) || !out) return IE_EINVAL;
     std::vector<uint8_t> v;

@@ -300,8 +300,7 @@ int Huffman::encode(ie_ctx* c, const uint8_t* in, size_t n, std::vector<uint8_t>
 // by leaf on the host (<= 256 leaves); no dictionary entry = passthrough (the stream continues
 // after the stop bit).  The bit walk -- O(stream bits), serial in the reference -- runs on the
 // device (ie_huffman_decode) over a 15-bit prefix table built from the tree.
-int Huffman::decode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
-                    size_t& start_bit) {
+int Huffman::decode_table(const uint8_t* in, size_t n, uint16_t* lut, bool& passthrough, size_t& start_bit) {
     util::BitStreamReader rd(in, n);
     struct T {
         int child[2] = {-1, -1};
@@ -329,17 +328,13 @@ int Huffman::decode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_
             tree[cur].sym = int(key);
         }
     }
-    if (!any) {
-        passthrough = true;
-        start_bit = rd.get_position();
-        return IE_OK;
-    }
-    passthrough = false;
-    start_bit = 0;
+    passthrough = !any;
+    start_bit = rd.get_position();
+    if (!any) return IE_OK;
     // lut[p] = sym | len << 8 for the leaf reached by the 15-bit string p (codes are <= 15 bits:
     // 4-bit lengths in the dictionary); 0 where the walk falls off the tree or needs more bits
     constexpr int K = 15;
-    std::vector<uint16_t> lut(size_t(1) << K, 0);
+    std::fill(lut, lut + (size_t(1) << K), uint16_t(0));
     std::vector<std::pair<int, int>> stack{{0, 0}};  // (node, depth); prefix filled per leaf
     std::vector<uint32_t> path(tree.size(), 0);
     while (!stack.empty()) {
@@ -359,11 +354,28 @@ int Huffman::decode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_
                 stack.push_back({t.child[d], depth + 1});
             }
     }
-    // the walk ends at the end of the buffer (padding bits included), so at most one symbol per bit
-    const uint64_t nbits = uint64_t(n) * 8, from = rd.get_position();
-    out.resize(size_t(nbits - from) + 1);
+    return IE_OK;
+}
+
+int Huffman::decode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
+                    size_t& start_bit) {
+    std::vector<uint16_t> lut(size_t(1) << 15);
+    size_t from = 0;
+    int r = decode_table(in, n, lut.data(), passthrough, from);
+    if (r) return r;
+    if (passthrough) {
+        start_bit = from;
+        return IE_OK;
+    }
+    start_bit = 0;
+    // the symbol count first (the walk ends at the end of the buffer, padding bits included), then
+    // the symbols into a buffer of exactly that size
     size_t got = 0;
-    const int r = ie_huffman_decode(ctx, in, n, from, lut.data(), out.data(), out.size(), &got);
+    r = ie_huffman_decode(ctx, in, n, from, lut.data(), nullptr, 0, &got);
+    if (r != IE_OK && r != IE_ECAP) return r;
+    out.resize(got);
+    if (!got) return IE_OK;
+    r = ie_huffman_decode(ctx, in, n, from, lut.data(), out.data(), out.size(), &got);
     if (r) return r;
     out.resize(got);
     return IE_OK;

@@ -99,7 +99,8 @@ struct ie_ctx {
     size_t cap_hout = 0;
     uint8_t* d_pix = nullptr;
     size_t cap_pix = 0;
-    int last_rounds = 0;
+    int last_rounds = 0;               // fix-up rounds of the last multi-kernel decode
+    int last_fused = 0;                // the last decode ran the fused one-launch path
     unsigned long long* d_first = nullptr;  // [256]
     ie_pipe* pipe = nullptr;           // streamed host path of image batches (created on first use)
 };
@@ -1211,6 +1212,13 @@ int ie_vstream_finish(ie_vstream* v, uint8_t* dst, size_t cap, size_t* nbytes, u
     return IE_OK;
 }
 
+int ie_last_decode_info(ie_ctx* c, int* fused, int* rounds) {
+    if (!c) return IE_EINVAL;
+    if (fused) *fused = c->last_fused;
+    if (rounds) *rounds = c->last_rounds;
+    return IE_OK;
+}
+
 const uint8_t* ie_vstream_device(const ie_vstream* v) { return v ? v->d_stream : nullptr; }
 
 int ie_vstream_close(ie_vstream* v) {
@@ -1932,6 +1940,24 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
     return IE_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// host pixel destinations: copy only the pixel rows (bytes between rows / frames belong to the caller)
+int finish_decode(ie_ctx* c, uint8_t* out, const uint8_t* dpix, bool out_dev, int nframes, int w, int h, size_t stride,
+                  size_t frame_pitch, uint64_t end, uint64_t* end_bit) {
+    if (!out_dev) {
+        for (int f = 0; f < nframes; f++)
+            HIPCHK(c, hipMemcpy2D(out + size_t(f) * frame_pitch, stride, dpix + size_t(f) * frame_pitch, stride,
+                                  size_t(w), size_t(h), hipMemcpyDeviceToHost));
+    }
+    if (end_bit) *end_bit = end;
+    return IE_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,
                      int use_rle, uint8_t* out, size_t stride, size_t frame_pitch, uint64_t* end_bit) {
     if (!c || !in || !out) return IE_EINVAL;
@@ -1976,6 +2002,28 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     da.stride = stride;
     da.frame_pitch = frame_pitch;
     da.tab = c->d_tab;
+    // One fused launch (segments parsed in LDS, see parse_decode_kernel); should it report a
+    // segment whose true path did not merge with its speculative one (or a spin time-out), the
+    // multi-kernel path below decodes the stream instead.
+    static const bool no_fused = getenv("IE_DEC_NOFUSED") != nullptr;  // A/B aid
+    if (!no_fused && !c->use_ticket) {
+        const uint64_t sb = ie::parse_decode_segment_bits(n);
+        const int nseg = int((nbits - start_bit + sb - 1) / sb);
+        if ((r = prepare_state(c, std::max(nseg, 1), 1))) return r;
+        HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 4 * sizeof(uint64_t), c->stream));
+        ie::launch_parse_decode(reinterpret_cast<const uint32_t*>(c->d_dec), nbits, start_bit, da, n, c->d_state,
+                                c->tag, reinterpret_cast<unsigned*>(c->d_misc + 1), c->d_misc, c->stream);
+        HIPCHK(c, hipGetLastError());
+        uint64_t hm[2] = {0, 0};
+        HIPCHK(c, hipMemcpyAsync(hm, c->d_misc, sizeof(hm), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (hm[1] == 0) {  // err[0] (time-outs) and err[1] (fallback) both clear
+            c->last_rounds = 0;
+            c->last_fused = 1;
+            if (hm[0] > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
+            return finish_decode(c, out, dpix, out_dev, nframes, w, h, stride, frame_pitch, hm[0], end_bit);
+        }
+    }
     uint64_t* wk = c->d_walk;
     const size_t cap = c->cap_walk / 4;
     HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 4 * sizeof(uint64_t), c->stream));
@@ -1986,18 +2034,12 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     if (rounds < 0) return fail(c, IE_EHIP, "decode index walk failed");
     HIPCHK(c, hipGetLastError());
     c->last_rounds = rounds;
+    c->last_fused = 0;
     uint64_t end = 0;
     HIPCHK(c, hipMemcpyAsync(&end, c->d_misc, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
-    if (!out_dev) {
-        // copy only the pixel rows: bytes between rows / frames belong to the caller
-        for (int f = 0; f < nframes; f++)
-            HIPCHK(c, hipMemcpy2D(out + size_t(f) * frame_pitch, stride, dpix + size_t(f) * frame_pitch, stride,
-                                  size_t(w), size_t(h), hipMemcpyDeviceToHost));
-    }
-    if (end_bit) *end_bit = end;
-    return IE_OK;
+    return finish_decode(c, out, dpix, out_dev, nframes, w, h, stride, frame_pitch, end, end_bit);
 }
 
 }  // extern "C"

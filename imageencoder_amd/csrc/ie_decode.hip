@@ -339,28 +339,335 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
         hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
         uint64_t* cur = exA;
         uint64_t* nxt = exB;
-        int rounds = 0;
-        for (; rounds < max_rounds; rounds++) {
+        // fix-up rounds in growing groups (1, 2, 4, 8, 8, ...) between host checks of the
+        // "changed" flag (a round after convergence is a near-empty launch; a host round trip per
+        // round costs more)
+        int rounds = 0, group = 1;
+        bool done = false;
+        while (!done && rounds < max_rounds + 8) {
             unsigned h = 0;
             if (hipMemsetAsync(changed, 0, sizeof(unsigned), s) != hipSuccess) return -1;
-            a.first = 0;
-            a.exit_in = cur;
-            a.exit_out = nxt;
-            hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
+            for (int r = 0; r < group; r++) {
+                a.first = 0;
+                a.exit_in = cur;
+                a.exit_out = nxt;
+                hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
+                uint64_t* t = cur;
+                cur = nxt;
+                nxt = t;
+            }
+            rounds += group;
+            group = group < 8 ? 2 * group : 8;
             if (hipMemcpyAsync(&h, changed, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
             if (hipStreamSynchronize(s) != hipSuccess) return -1;
-            uint64_t* t = cur;
-            cur = nxt;
-            nxt = t;
-            if (!h) break;
+            done = (h == 0);
         }
-        if (rounds == max_rounds) return -2;
+        if (!done) return -2;
         hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
         hipLaunchKernelGGL(huf_total_kernel, dim3(1), dim3(1), 0, s, base, count, nchunks, total);
         return rounds;
     }
     hipLaunchKernelGGL(huf_emit_kernel, g, blk, 0, s, a);
     return 0;
+}
+
+// ---- fused record parse + decode (one launch) ---------------------------------------------------
+// The stream is cut into SEGMENTS of kDecTPB * C bits, one workgroup each, staged in LDS with
+// coalesced loads (plus a margin covering the longest record).  Inside a segment every lane walks
+// C bits from a speculative entry, from LDS; local fix-up rounds (entry := the left neighbour's
+// exit) make the segment's path consistent from its first bit; that path's record starts are
+// marked in an LDS bitmap.  A record stream resynchronises within a few records, so the path
+// from the segment's TRUE entry (the predecessor's exit) merges with the marked path after a few
+// records and the segment's exit does not depend on its entry: every segment publishes its exit
+// at once, and its successor walks from it only up to the merge.  The true record count then
+// feeds a decoupled look-back (ie_common.hpp) for the global block index, and the lanes decode
+// their records straight from LDS: dequantise (Block.cpp:163-169), FP64 IDCT in the reference's
+// order (algo.cpp:343-363), +128, clamp, truncate (Block.cpp:100-107).  Should a walk from the
+// true entry not merge inside its segment (or a spin time out), the launch reports it in err[1]
+// and the host re-runs the multi-kernel path above.
+constexpr int kDecTPB = 256;
+template <int N> struct DecSeg {
+    static constexpr int C = (N == 4) ? 256 : 512;    // bits per lane
+    static constexpr int S = kDecTPB * C;              // bits per segment
+    static constexpr int MARGIN = 1024 + 64;           // > longest record (4 + 15 * 65) + 64-bit reads
+    static constexpr int WORDS = (S + MARGIN) / 32 + 2;
+    static constexpr int MAXPRE = 64;                  // records walked from the true entry before merging
+};
+
+struct FusedArgs {
+    const uint32_t* words;  // stream as stored (big-endian bytes), zero-padded
+    uint64_t nbits, start_bit;
+    int nseg;
+    int rle;
+    uint64_t* st;           // chain state (kGran words per segment): 0 count aggregate, 1 inclusive, 3 exit
+    uint32_t tag;
+    unsigned* err;          // [0] spin timeouts, [1] fallback needed (no merge / malformed)
+    uint64_t* end_out;      // end bit of the last block's record
+    DecArgs d;
+};
+
+// bits [p, p+l) of the LDS stream copy L (MSB-first words), l <= 32, p relative to the copy
+__device__ __forceinline__ uint32_t lbits(const uint32_t* L, uint32_t p, int l) {
+    const uint32_t w = p >> 5, s = p & 31u;
+    const uint64_t v = (uint64_t(L[w]) << 32) | L[w + 1];
+    return l ? uint32_t((v << s) >> (64 - l)) : 0u;
+}
+
+// length of the record whose header is at p, 0 if no record can start there
+template <int N>
+__device__ __forceinline__ uint32_t rec_len(const uint32_t* L, uint32_t p, int rle) {
+    constexpr int NN = N * N;
+    const uint32_t head = lbits(L, p, 20);
+    const uint32_t bl = head >> 16;
+    if (!bl) return 0;
+    if (!rle) return 4u + bl * NN;
+    const uint32_t lw = (head & 0xFFFFu) >> (16 - bl);
+    return lw <= uint32_t(NN) ? 4u + bl * (lw + 1u) : 0u;
+}
+
+// speculative walk of [e, end): exit position and record count (invalid headers slide one bit)
+template <int N>
+__device__ __forceinline__ uint32_t spec_walk(const uint32_t* L, uint32_t e, uint32_t end, uint32_t lim, int rle,
+                                              uint32_t* cnt, uint32_t* bitmap) {
+    uint32_t c = 0;
+    while (e < end && e < lim) {
+        const uint32_t len = rec_len<N>(L, e, rle);
+        if (!len) {
+            e++;
+            continue;
+        }
+        if (bitmap) atomicOr(&bitmap[e >> 5], 1u << (e & 31u));
+        c++;
+        e += len;
+    }
+    *cnt = c;
+    return e;
+}
+
+// decode the record at p (relative to L) as block g; returns the bit after it
+template <int N>
+__device__ __forceinline__ uint32_t decode_record(const uint32_t* L, uint32_t p, uint64_t g, const DecArgs& a) {
+    constexpr int NN = N * N;
+    const EncTables* __restrict__ tab = a.tab;
+    const int bl = int(lbits(L, p, 4));
+    p += 4;
+    int length = NN;
+    if (a.rle) {
+        length = int(lbits(L, p, bl));
+        p += bl;
+    }
+    if (length > NN) length = NN;
+    double Y[NN];
+#pragma unroll
+    for (int k = 0; k < NN; k++) Y[k] = 0.0;
+    const int* zz = (N == 4) ? kZZ4 : kZZ8;
+    for (int k = 0; k < length; k++) {
+        const uint32_t raw = lbits(L, p, bl);
+        p += bl;
+        const int sh = 16 - bl;
+        Y[zz[k]] = double(int16_t(int16_t(uint16_t(raw << sh)) >> sh));
+    }
+    double t[NN];
+#pragma unroll
+    for (int k = 0; k < NN; k++) t[k] = 0.0;
+#pragma unroll
+    for (int uv = 0; uv < NN; uv++) {
+        const double y = Y[uv] * tab->qd[uv];
+        if (y != 0.0) {
+            const double* R = &tab->R[uv * NN];
+#pragma unroll
+            for (int ij = 0; ij < NN; ij++) t[ij] = t[ij] + R[ij] * y;
+        }
+    }
+    const uint64_t bpf = uint64_t(a.bx) * a.by;
+    const uint64_t f = g / bpf, r = g - f * bpf;
+    const int byi = int(r / a.bx), bxi = int(r - uint64_t(byi) * a.bx);
+    uint8_t* o = a.out + f * a.frame_pitch + uint64_t(byi) * N * a.stride + uint64_t(bxi) * N;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        uint32_t wv[N / 4];
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            double x = t[i * N + j] + 128.0;
+            x = x < 0.0 ? 0.0 : (x > 255.0 ? 255.0 : x);
+            const uint32_t b = uint32_t(uint8_t(x));
+            if (j % 4 == 0) wv[j / 4] = b;
+            else wv[j / 4] |= b << (8 * (j % 4));
+        }
+        uint8_t* row = o + uint64_t(i) * a.stride;
+        if ((reinterpret_cast<uintptr_t>(row) & 3u) == 0) {
+#pragma unroll
+            for (int m = 0; m < N / 4; m++) reinterpret_cast<uint32_t*>(row)[m] = wv[m];
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; j++) row[j] = uint8_t(wv[j / 4] >> (8 * (j % 4)));
+        }
+    }
+    return p;
+}
+
+template <int N>
+__global__ __launch_bounds__(kDecTPB) void parse_decode_kernel(FusedArgs a) {
+    using G = DecSeg<N>;
+    __shared__ uint32_t L[G::WORDS];
+    __shared__ uint32_t mark[G::S / 32 + 1];
+    __shared__ uint32_t X[kDecTPB];
+    __shared__ uint32_t pre[G::MAXPRE];
+    __shared__ uint32_t misc[24];  // [0..3] scan scratch, [4] any, [5] merge, [6] c_pre, [8..9] excl, [10] fail
+    const int tid = threadIdx.x, k = blockIdx.x;
+    const uint64_t seg0 = a.start_bit + uint64_t(k) * G::S;  // the segment's first bit
+    const uint64_t base = seg0 & ~31ull;                       // bit 0 of L
+    const uint32_t s0 = uint32_t(seg0 - base);                 // segment start, relative
+    const uint32_t s1 = s0 + G::S;                             // segment end (exclusive), relative
+    const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(G::WORDS - 2) * 32));  // readable bits
+    // 1. stage the segment's bits (MSB-first words), zeros past the stream
+    const uint64_t w0 = base >> 5, nw = (a.nbits + 31) >> 5;
+    for (int i = tid; i < G::WORDS; i += kDecTPB)
+        L[i] = (w0 + i < nw) ? bswap32(__builtin_nontemporal_load(a.words + w0 + i)) : 0u;
+    for (int i = tid; i < G::S / 32 + 1; i += kDecTPB) mark[i] = 0u;
+    __syncthreads();
+    // 2. speculative lane walks, then local rounds until every lane continues its neighbour's path
+    const uint32_t lane_end = s0 + uint32_t(tid + 1) * G::C;
+    uint32_t entry = s0 + uint32_t(tid) * G::C, cnt;
+    uint32_t ex = spec_walk<N>(L, entry, lane_end, lim, a.rle, &cnt, nullptr);
+    for (int round = 0; round <= kDecTPB; round++) {
+        X[tid] = ex;
+        __syncthreads();
+        const uint32_t ne = tid ? X[tid - 1] : s0;
+        const bool ch = ne != entry;
+        if (ch) {
+            entry = ne;
+            ex = spec_walk<N>(L, entry, lane_end, lim, a.rle, &cnt, nullptr);
+        }
+        if (!__syncthreads_or(ch)) break;
+    }
+    // 3. mark the segment's path; its exit is published at once (entry-independent, see above)
+    spec_walk<N>(L, entry, lane_end, lim, a.rle, &cnt, mark);
+    __syncthreads();  // marks visible
+    if (tid == kDecTPB - 1) st_state(&a.st[kGran * k + 3], (uint64_t(a.tag) << 56) | ((base + ex) & kMask56));
+    // 4. the true entry (predecessor's exit) and the walk from it to the merge with the marked path
+    if (tid == 0) {
+        uint64_t e = a.start_bit;
+        bool ok = true;
+        if (k > 0) {
+            unsigned sp = 0;
+            for (;;) {
+                const uint64_t g = ld_state(&a.st[kGran * (k - 1) + 3]);
+                if (uint32_t(g >> 56) == a.tag) {
+                    e = g & kMask56;
+                    break;
+                }
+                if (++sp > kSpinLimit) {
+                    atomicAdd(&a.err[0], 1u);
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        uint32_t p = uint32_t(e - base), c = 0;
+        // walk until a marked record start (the merge), the segment's end or the stream's end
+        while (ok && p < s1 && p < lim && !((mark[p >> 5] >> (p & 31u)) & 1u)) {
+            const uint32_t len = rec_len<N>(L, p, a.rle);
+            if (!len || c == G::MAXPRE) {  // malformed, or no merge within reach: fall back
+                ok = false;
+                break;
+            }
+            pre[c++] = p;
+            p += len;
+        }
+        // no merge inside the segment: its true exit must be the published one, else fall back
+        if (ok && p >= s1 && k != a.nseg - 1 && p != X[kDecTPB - 1]) ok = false;
+        misc[10] = ok ? 0u : 1u;
+        misc[5] = p;
+        misc[6] = c;
+    }
+    __syncthreads();
+    // (a fallback still publishes a count below, so successors' look-backs terminate; the host
+    // discards this launch's output)
+    if (misc[10] && tid == 0) atomicOr(&a.err[1], 1u);
+    const uint32_t m = misc[5], c_pre = misc[6];
+    // 5. true count = records before the merge + marked records from the merge on
+    uint32_t mine = 0;  // this lane's path records at or after m (the true records among them)
+    for (uint32_t e2 = entry; e2 < lane_end && e2 < lim;) {
+        const uint32_t len = rec_len<N>(L, e2, a.rle);
+        if (!len) {
+            e2++;
+            continue;
+        }
+        mine += (e2 >= m) ? 1u : 0u;
+        e2 += len;
+    }
+    uint32_t tot2;
+    const uint32_t off = block_excl_scan<kDecTPB>(mine, misc, &tot2);
+    const uint32_t A = c_pre + tot2;
+    // 6. global index of the segment's first block: decoupled look-back over the counts
+    if (tid == 0) chain_publish_count(a.st, k, k, a.tag, A);
+    if (tid < 64 && k > 0) {
+        const Probe pr = probe_issue(a.st, k, k, 1, 0, kProbe0);
+        const uint64_t excl = lookback_wave(pr, a.st, k, k, 1, a.tag, a.err);
+        if (tid == 0) {
+            publish(a.st, k, 1, a.tag, excl + A);
+            misc[8] = uint32_t(excl);
+            misc[9] = uint32_t(excl >> 32);
+        }
+    } else if (tid == 0) {
+        misc[8] = 0u;
+        misc[9] = 0u;
+    }
+    __syncthreads();
+    const uint64_t excl = uint64_t(misc[8]) | (uint64_t(misc[9]) << 32);
+    // 7. decode: the pre-merge records (thread 0), then every lane's records from the merge on
+    const uint64_t nblocks = uint64_t(a.d.nframes) * a.d.bx * a.d.by;
+    if (tid == 0) {
+        for (uint32_t i = 0; i < c_pre; i++) {
+            const uint64_t g = excl + i;
+            if (g < nblocks) {
+                const uint32_t q = decode_record<N>(L, pre[i], g, a.d);
+                if (g == nblocks - 1) *a.end_out = base + q;
+            }
+        }
+    }
+    uint64_t g = excl + c_pre + off;
+    uint32_t e3 = entry;
+    while (e3 < lane_end && e3 < lim && g < nblocks) {
+        const uint32_t len = rec_len<N>(L, e3, a.rle);
+        if (!len) {
+            e3++;
+            continue;
+        }
+        if (e3 >= m) {
+            const uint32_t q = decode_record<N>(L, e3, g, a.d);
+            if (g == nblocks - 1) *a.end_out = base + q;
+            g++;
+        }
+        e3 += len;
+    }
+}
+
+uint64_t parse_decode_segment_bits(int n) { return (n == 4) ? DecSeg<4>::S : DecSeg<8>::S; }
+
+// One launch: returns the number of segments (the host checks err[1] afterwards).
+int launch_parse_decode(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& d, int n,
+                        uint64_t* st, uint32_t tag, unsigned* err, uint64_t* end_out, hipStream_t s) {
+    const uint64_t S = (n == 4) ? DecSeg<4>::S : DecSeg<8>::S;
+    const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
+    const int nseg = int((span + S - 1) / S);
+    if (nseg == 0) return 0;
+    FusedArgs a{};
+    a.words = W;
+    a.nbits = nbits;
+    a.start_bit = start_bit;
+    a.nseg = nseg;
+    a.rle = d.rle;
+    a.st = st;
+    a.tag = tag;
+    a.err = err;
+    a.end_out = end_out;
+    a.d = d;
+    if (n == 4) hipLaunchKernelGGL((parse_decode_kernel<4>), dim3(nseg), dim3(kDecTPB), 0, s, a);
+    else hipLaunchKernelGGL((parse_decode_kernel<8>), dim3(nseg), dim3(kDecTPB), 0, s, a);
+    return nseg;
 }
 
 // Host-driven decode sequence (ie_capi.cpp::decode calls this).

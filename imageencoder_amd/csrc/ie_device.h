@@ -159,6 +159,14 @@ int decode_frames_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, 
                          uint64_t* base, uint64_t* block_bit, unsigned* changed, uint64_t* end_out, hipStream_t s,
                          int max_rounds);
 
+// Fused parse + decode in one launch (segments in LDS, speculative walks merged with the true
+// path, decoupled look-back over record counts).  err[1] != 0 afterwards: re-run the path above.
+// st / tag: the encoder's chain state (granules 0, 1 and 3 of every segment).  Returns the
+// number of segments.
+int launch_parse_decode(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& d, int n,
+                        uint64_t* st, uint32_t tag, unsigned* err, uint64_t* end_out, hipStream_t s);
+uint64_t parse_decode_segment_bits(int n);
+
 // Huffman decode (ie_decode.hip): write = false runs the walk + fix-up rounds + scan and leaves the
 // symbol count in *total (device); write = true then emits the symbols into out.
 int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,

@@ -232,6 +232,11 @@ int ie_decode_frames(ie_ctx* ctx, const uint8_t* in, size_t len, uint64_t start_
                      int nframes, int use_rle, uint8_t* out, size_t stride, size_t frame_pitch,
                      uint64_t* end_bit);
 
+/* How the last ie_decode_frames ran: fused = 1 for the one-launch parse + decode (stream segments
+ * in LDS, speculative walks merged with the true path); 0 for the multi-kernel fallback (chunk
+ * walks with `rounds` fix-up rounds), taken when a segment's true path did not merge. */
+int ie_last_decode_info(ie_ctx* ctx, int* fused, int* rounds);
+
 #ifdef __cplusplus
 }
 #endif

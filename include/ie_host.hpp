@@ -148,6 +148,9 @@ public:
     // Decode a stream that starts with the Huffman flag bit.  passthrough = true: no table, the
     // payload starts at *start_bit of `in` itself; else `out` receives the decoded bytes (the bit
     // walk runs on ctx's device, ie_huffman_decode).  Returns IE_OK or an ie_hip.h error code.
+    // The dictionary part alone: the 15-bit prefix table ie_huffman_decode walks with (lut: 32768
+    // entries), and where the code stream starts; passthrough when the stream holds no dictionary.
+    static int decode_table(const uint8_t* in, size_t n, uint16_t* lut, bool& passthrough, size_t& start_bit);
     static int decode(ie_ctx* ctx, const uint8_t* in, size_t n, std::vector<uint8_t>& out, bool& passthrough,
                       size_t& start_bit);
 };
@@ -358,4 +361,8 @@ int ieh_huffman_finish_after_encode(ie_ctx* ctx, const uint8_t* din, size_t in_p
 // Huffman<uint8_t>::decode alone (Huffman.cpp:354-402; the bit walk on the device): decoded byte
 // count, or 0 with *passthrough = 1 when the stream has no dictionary.
 int64_t ieh_huffman_decode(ie_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap, int* passthrough);
+// The dictionary of a Huffman-coded stream (host bytes) as ie_huffman_decode's 15-bit prefix table
+// (lut: 32768 entries) and the code stream's first bit: a caller with the stream in device memory
+// then decodes it device-resident.  Returns 1 when there is no dictionary (passthrough), 0, or < 0.
+int ieh_huffman_table(const uint8_t* in, size_t n, uint16_t* lut, uint64_t* start_bit);
 }

@@ -4,6 +4,7 @@ inverse path (ie_decode_frames), against the reference's golden files and the CP
 Bit-exact is the bar for every byte and pixel.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -441,3 +442,48 @@ def test_counted_encode_histogram(codec, w, h, f, start_bit, kind):
         np.testing.assert_array_equal(h_pass[k], want)
         np.testing.assert_array_equal(h_fused[k], want)
     np.testing.assert_array_equal(f_fused, f_pass)
+
+
+# ------------------------------------------------- fused parse + decode (one launch) vs fallback
+@pytest.mark.parametrize("n", [4, 8])
+@pytest.mark.parametrize("kind", ["flat", "U", "M", "grad"])
+def test_decode_multi_segment_vs_oracle(codec, n, kind):
+    """Streams spanning many parse segments (4x4: 65536 bits, 8x8: 131072 bits each), with
+    records from 5 bits (flat blocks) to the longest: the fused decode == the oracle's."""
+    w, h = 648, 488
+    if kind == "flat":
+        y = np.full((h, w), 77, dtype=np.uint8)
+    elif kind == "grad":
+        yy, xx = np.mgrid[0:h, 0:w]
+        y = ((xx * 3 + yy * 5) % 256).astype(np.uint8)
+    else:
+        y = synth.frame(kind, w, h, seed=99 + n)
+    q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+    enc = codec.encode_image_file(y, w, h, q, n, rle=True, huffman=False)
+    pix = codec.decode_image_file(enc, n)
+    # A stream of identical records (flat image, regular gradient) is periodic: a speculative walk can lock into a
+    # wrong phase that never meets the true path, and the one-launch decode hands such a stream to
+    # the multi-kernel path (ie_last_decode_info reports which ran).  Every other kind must stay fused.
+    if kind not in ("flat", "grad"):
+        assert codec.last_decode_info()[0], "the fused decode fell back"
+    assert np.array_equal(pix, O.load().decode_image(enc, n))
+
+
+def test_decode_fallback_path_matches(codec, tmp_path):
+    """The multi-kernel decode (IE_DEC_NOFUSED, the fused launch's fallback) gives the same
+    pixels as the fused launch, in a fresh process."""
+    import subprocess
+    import sys
+    c = next(c for c in O.manifest() if c["name"] == "synM4k_4x4")
+    enc = _encode_case(codec, c)
+    fused = codec.decode_image_file(enc, 4)
+    (tmp_path / "s.enc").write_bytes(enc)
+    code = ("import sys, hashlib; sys.path.insert(0, %r)\n"
+            "from imageencoder_amd import Codec\n"
+            "c = Codec(0)\n"
+            "pix = c.decode_image_file(open(%r, 'rb').read(), 4)\n"
+            "print(hashlib.md5(pix.tobytes()).hexdigest())\n") % (O.ROOT, str(tmp_path / "s.enc"))
+    env = dict(os.environ, IE_DEC_NOFUSED="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == _md5(fused.tobytes()) == c["dec_md5"]
