@@ -426,11 +426,24 @@ __device__ __forceinline__ uint32_t size_block(uint32_t (&zp)[N * N / 2], int rl
 }
 
 // OR the low `len` bits of v (MSB first) into the LDS bit image at bit p (len + p%32 <= 64).
+#ifndef IE_ASM_OR
+#define IE_ASM_OR 1
+#endif
 __device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t v, uint32_t len) {
     const uint32_t w = p >> 5, s = p & 31u;
     const uint64_t x = uint64_t(v) << (64u - len - s);
+#if IE_ASM_OR
+    // The image is the dynamic LDS area at LDS byte address 0 (the encode kernels allocate no static
+    // LDS; tools/asmcheck.py checks their group_segment_fixed_size): the word pair's byte address
+    // straight from p, the second word through the instruction's offset field.
+    (void)img;
+    const uint32_t a = (p >> 3) & ~3u;
+    asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a), "v"(uint32_t(x >> 32)), "v"(uint32_t(x))
+                 : "memory");
+#else
     atomicOr(&img[w], uint32_t(x >> 32));
     atomicOr(&img[w + 1], uint32_t(x));
+#endif
 }
 
 // Branch-free variant: every pair is written (past Lw the packed coefficients are zero, so
@@ -745,7 +758,9 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     uint64_t near8 = 0;  // 8x8: per-coefficient requests of the lane's one block
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
+#if !IE_NO_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);  // one block at a time: keeps the live set small
+#endif
         if constexpr (EXACT) {
             BlockPx<N> px;
 #pragma unroll

@@ -46,9 +46,28 @@ def scan(path):
     return bad, kernels
 
 
+def static_lds(path):
+    """{kernel: group_segment_fixed_size} from the code object metadata."""
+    txt = open(path).read()
+    k = txt.find("amdhsa.kernels")
+    out = {}
+    for ent in txt[k:].split("\n  - ")[1:] if k >= 0 else []:
+        m = re.search(r"\.name:\s+(\S+)", ent)
+        g = re.search(r"\.group_segment_fixed_size:\s+(\d+)", ent)
+        if m and g:
+            out[m.group(1)] = int(g.group(1))
+    return out
+
+
 def main(paths):
     rc = 0
     for p in paths:
+        # the encoder's bit image is addressed from LDS byte 0 (scatter_bits' inline ds_or): its
+        # kernels must allocate no static LDS, so the dynamic area starts there
+        for name, size in static_lds(p).items():
+            if "encode_kernel" in name and size != 0:
+                rc = 1
+                print(f"{p}: {name} allocates {size} B of static LDS (scatter_bits assumes 0)", file=sys.stderr)
         bad, kernels = scan(p)
         for name, info in kernels.items():
             if info:
