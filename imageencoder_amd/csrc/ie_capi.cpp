@@ -1378,7 +1378,10 @@ int ie_create(int device, ie_ctx** out) {
         if (e != hipSuccess && r == IE_OK) r = fail(c, IE_EHIP, std::string(what) + ": " + hipGetErrorString(e));
     };
     chk(hipSetDevice(device), "hipSetDevice");
-    if (r == IE_OK) chk(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking), "hipStreamCreate");
+    // A BLOCKING stream: it orders with the legacy default (NULL) stream, so device buffers a caller
+    // (e.g. PyTorch's default stream) filled just before a call are complete when the call's kernels
+    // read them, and vice versa.  (Callers with their own streams use ie_set_stream.)
+    if (r == IE_OK) chk(hipStreamCreateWithFlags(&c->own, hipStreamDefault), "hipStreamCreate");
     c->stream = c->own;
     // Debug switch: order tiles by the atomic ticket from the first launch (exercises the
     // timeout-recovery path, which dispatch order otherwise never needs)
@@ -2002,11 +2005,13 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     da.stride = stride;
     da.frame_pitch = frame_pitch;
     da.tab = c->d_tab;
-    // One fused launch (segments parsed in LDS, see parse_decode_kernel); should it report a
-    // segment whose true path did not merge with its speculative one (or a spin time-out), the
-    // multi-kernel path below decodes the stream instead.
-    static const bool no_fused = getenv("IE_DEC_NOFUSED") != nullptr;  // A/B aid
-    if (!no_fused && !c->use_ticket) {
+    // One fused launch (segments parsed in LDS, see parse_decode_kernel; IE_DEC_FUSED=1); should it
+    // report a segment whose true path did not merge with its speculative one (or a spin
+    // time-out), the multi-kernel path below decodes the stream instead.
+    // (measured slower than the multi-kernel path on 4x4 noise and falling back on 8x8 streams,
+    // opt-in until the exact parse of §9 replaces both)
+    static const bool fused = getenv("IE_DEC_FUSED") != nullptr && getenv("IE_DEC_NOFUSED") == nullptr;
+    if (fused && !c->use_ticket) {
         const uint64_t sb = ie::parse_decode_segment_bits(n);
         const int nseg = int((nbits - start_bit + sb - 1) / sb);
         if ((r = prepare_state(c, std::max(nseg, 1), 1))) return r;

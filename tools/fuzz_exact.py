@@ -81,9 +81,13 @@ while done < args.blocks and time.time() - t0 < args.budget:
         # locate the differing frames
         for f in range(B):
             nb = (int(max(ef[f], ee[f])) + 7) // 8
-            if ef[f] != ee[f] or not torch.equal(o_fast[f * pitch:f * pitch + nb], o_exact[f * pitch:f * pitch + nb]):
+            a_, b_ = o_fast[f * pitch:f * pitch + nb], o_exact[f * pitch:f * pitch + nb]
+            if ef[f] != ee[f] or not torch.equal(a_, b_):
                 mism += 1
-                bad.append({"kind": kind, "batch_seed": 1000 + it, "frame": f})
+                diff = torch.nonzero(a_ != b_)
+                first = int(diff[0]) if diff.numel() else -1
+                bad.append({"kind": kind, "batch_seed": 1000 + it, "frame": f, "end_fast": int(ef[f]),
+                            "end_exact": int(ee[f]), "first_diff_byte": first, "ndiff": int(diff.numel())})
     done += B * blocks_per_frame
     per_kind[kind] += B * blocks_per_frame
     it += 1
