@@ -407,9 +407,10 @@ def main():
                 codec.decode_frames(one, w, h, pix, start_bit=hdr_bits, length=nb0)
             torch.cuda.synchronize(dev)
             td = (time.perf_counter() - t0) / kd
-            fused, _ = codec.last_decode_info()
+            chunks, groups = codec.last_decode_info()
             extra["decode_one_image"] = {"us": round(td * 1e6, 1), "Mpx_s": round(w * h / td / 1e6, 1),
-                                         "path": "fused one-launch parse+decode" if fused else "multi-kernel fallback"}
+                                         "path": f"exact table parse ({chunks} chunks, {groups} groups), "
+                                                 "3 launches, host sync at the end only"}
         workload = (f"{wl}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
                     f"{' +Huffman' if cfg['huffman'] else ''}, batch of {B} independent images per step, "
                     f"{R} distinct resident frames per GPU ({R * w * h / 2**20:.0f} MiB)")

@@ -379,12 +379,11 @@ class Codec:
         src = self.L.ie_last_end_bits(self.h)
         self._chk(self.L.ie_memcpy(self.h, C.c_void_p(_ptr(dst)), C.c_void_p(src), 8 * count))
 
-    def last_decode_info(self) -> tuple[bool, int]:
-        """(fused, rounds) of the last decode: the one-launch path, or the multi-kernel fallback
-        with its fix-up rounds."""
+    def last_decode_info(self) -> tuple[int, int]:
+        """(chunks, composition levels) of the last record decode's exact parse (ie_last_decode_info)."""
         f, r = C.c_int(0), C.c_int(0)
         self._chk(self.L.ie_last_decode_info(self.h, C.byref(f), C.byref(r)))
-        return bool(f.value), int(r.value)
+        return int(f.value), int(r.value)
 
     def last_fallbacks(self) -> int:
         v = C.c_uint64(0)

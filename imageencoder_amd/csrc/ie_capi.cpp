@@ -90,17 +90,20 @@ struct ie_ctx {
     size_t cap_walk = 0;
     uint32_t* d_count = nullptr;
     size_t cap_count = 0;
-    uint64_t* d_bb = nullptr;          // block start bits
-    size_t cap_bb = 0;
-    uint64_t* d_misc = nullptr;        // [0] end bit, [1] changed / invalid flags, [2] symbol count
+    uint16_t* d_rtab = nullptr;        // record parse: chunk transfer tables and the composites of every level
+    size_t cap_rtab = 0;
+    uint16_t* d_rpos = nullptr;        // record parse: record positions per chunk
+    size_t cap_rpos = 0;
+    uint64_t* d_misc = nullptr;        // [0] end bit, [1] changed / invalid flags or decode tickets, [2] symbol /
+                                       // record count, [3] histogram ticket
     uint16_t* d_hlut = nullptr;        // Huffman decode prefix table (32768 entries)
     size_t cap_hlut = 0;
     uint8_t* d_hout = nullptr;         // Huffman decode output staging (host destinations)
     size_t cap_hout = 0;
     uint8_t* d_pix = nullptr;
     size_t cap_pix = 0;
-    int last_rounds = 0;               // fix-up rounds of the last multi-kernel decode
-    int last_fused = 0;                // the last decode ran the fused one-launch path
+    int last_chunks = 0;               // chunks of the last record decode
+    int last_groups = 0;               // and their groups
     unsigned long long* d_first = nullptr;  // [256]
     ie_pipe* pipe = nullptr;           // streamed host path of image batches (created on first use)
 };
@@ -1212,10 +1215,10 @@ int ie_vstream_finish(ie_vstream* v, uint8_t* dst, size_t cap, size_t* nbytes, u
     return IE_OK;
 }
 
-int ie_last_decode_info(ie_ctx* c, int* fused, int* rounds) {
+int ie_last_decode_info(ie_ctx* c, int* chunks, int* levels) {
     if (!c) return IE_EINVAL;
-    if (fused) *fused = c->last_fused;
-    if (rounds) *rounds = c->last_rounds;
+    if (chunks) *chunks = c->last_chunks;
+    if (levels) *levels = c->last_groups;
     return IE_OK;
 }
 
@@ -1395,7 +1398,7 @@ int ie_create(int device, ie_ctx** out) {
     if (r == IE_OK) chk(hipMalloc(&c->d_code, 2 * 256 * sizeof(uint32_t)), "hipMalloc(code)");
     if (r == IE_OK) chk(hipHostMalloc(&c->h_code, 2 * 256 * sizeof(uint32_t)), "hipHostMalloc(code)");
     if (r == IE_OK) chk(hipMalloc(&c->d_hist, 256 * sizeof(uint32_t)), "hipMalloc(hist)");
-    if (r == IE_OK) chk(hipMalloc(&c->d_misc, 4 * sizeof(uint64_t)), "hipMalloc(misc)");
+    if (r == IE_OK) chk(hipMalloc(&c->d_misc, 8 * sizeof(uint64_t)), "hipMalloc(misc)");
     if (r == IE_OK) chk(hipMalloc(&c->d_first, 256 * sizeof(unsigned long long)), "hipMalloc(first)");
     if (r != IE_OK) {
         std::fprintf(stderr, "ie_create: %s\n", c->err.c_str());
@@ -1437,7 +1440,8 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_dec);
     (void)hipFree(c->d_walk);
     (void)hipFree(c->d_count);
-    (void)hipFree(c->d_bb);
+    (void)hipFree(c->d_rtab);
+    (void)hipFree(c->d_rpos);
     (void)hipFree(c->d_misc);
     (void)hipFree(c->d_hlut);
     (void)hipFree(c->d_hout);
@@ -1979,16 +1983,38 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     HIPCHK(c, hipMemcpyAsync(c->d_dec, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                              c->stream));
     const uint64_t nbits = uint64_t(len) * 8;
-    // walk chunk (measured on 4K: 4x4 4096 bits, 8x8 16384 -- its wrong-phase walks couple late,
-    // so longer chunks mean fewer fix-up rounds); IE_DEC_CHUNK4 / IE_DEC_CHUNK8 override (tuning aid)
-    static const uint64_t chunk4 = getenv("IE_DEC_CHUNK4") ? strtoull(getenv("IE_DEC_CHUNK4"), nullptr, 10) : 4096;
-    static const uint64_t chunk8 = getenv("IE_DEC_CHUNK8") ? strtoull(getenv("IE_DEC_CHUNK8"), nullptr, 10) : 16384;
-    const uint64_t chunk_bits = std::max<uint64_t>(256, n == 4 ? chunk4 : chunk8);
-    const size_t nchunks = size_t((nbits - start_bit) / chunk_bits + 1);
-    if ((r = ensure(c, c->d_walk, c->cap_walk, 4 * nchunks))) return r;
-    if ((r = ensure(c, c->d_count, c->cap_count, nchunks))) return r;
+    const uint64_t span = nbits - start_bit;
     const uint64_t nblocks = uint64_t(nframes) * (w / n) * (h / n);
-    if ((r = ensure(c, c->d_bb, c->cap_bb, size_t(nblocks)))) return r;
+    // chunking: about R records per chunk (IE_DEC_R, default 32: measured on 4K streams against
+    // 16, 64 and 128) so that every chunk's walks are short; C a multiple of 32, at least
+    // 256 bits, at most 2^13 (a table wave's LDS -- M chunks' bits, valid-header bitmap, 16-bit
+    // claims -- within 80 KB)
+    const int G = ie::rec_group_chunks(n), D = ie::rec_entry_span(n);
+    static const char* rs = getenv("IE_DEC_R");
+    const uint64_t recs = rs ? std::max<uint64_t>(1, strtoull(rs, nullptr, 10)) : 32;
+    const uint64_t want = std::max<uint64_t>((nblocks + recs - 1) / recs, 1);
+    uint64_t C = (span + want - 1) / want;
+    C = std::min<uint64_t>(std::max<uint64_t>((C + 31) / 32 * 32, 256), uint64_t(1) << 13);
+    const uint64_t nch = std::max<uint64_t>((span + C - 1) / C, 1);
+    // levels: ceil(n / G) composites per level until at most G remain (G^4 chunks at most)
+    size_t tab_rows = 0;
+    int levels = 0;
+    for (uint64_t cur = nch;; cur = (cur + G - 1) / G) {
+        tab_rows += cur;
+        levels++;
+        if ((cur + G - 1) / G <= uint64_t(G)) {
+            tab_rows += (cur + G - 1) / G;
+            break;
+        }
+    }
+    if (levels > ie::kRecMaxLevels || nch > uint64_t(INT32_MAX))
+        return fail(c, IE_EINVAL, "stream too long for one decode call");
+    const int nchunks = int(nch);
+    if ((r = ensure(c, c->d_rtab, c->cap_rtab, tab_rows * D))) return r;
+    // d_walk: [nchunks] record bases, [G / 2] top-level entries, [nchunks / 2] chunk counts
+    const size_t e_at = size_t(nchunks), cnt_at = e_at + size_t(G) / 2 + 1;
+    if ((r = ensure(c, c->d_walk, c->cap_walk, cnt_at + size_t(nchunks) / 2 + 1))) return r;
+    if ((r = ensure(c, c->d_rpos, c->cap_rpos, size_t(nchunks) * ie::kRecPosCap))) return r;
     const size_t pix_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
     const bool out_dev = is_device_ptr(out);
     uint8_t* dpix = out;
@@ -2005,45 +2031,44 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     da.stride = stride;
     da.frame_pitch = frame_pitch;
     da.tab = c->d_tab;
-    // One fused launch (segments parsed in LDS, see parse_decode_kernel; IE_DEC_FUSED=1); should it
-    // report a segment whose true path did not merge with its speculative one (or a spin
-    // time-out), the multi-kernel path below decodes the stream instead.
-    // (measured slower than the multi-kernel path on 4x4 noise and falling back on 8x8 streams,
-    // opt-in until the exact parse of §9 replaces both)
-    static const bool fused = getenv("IE_DEC_FUSED") != nullptr && getenv("IE_DEC_NOFUSED") == nullptr;
-    if (fused && !c->use_ticket) {
-        const uint64_t sb = ie::parse_decode_segment_bits(n);
-        const int nseg = int((nbits - start_bit + sb - 1) / sb);
-        if ((r = prepare_state(c, std::max(nseg, 1), 1))) return r;
-        HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 4 * sizeof(uint64_t), c->stream));
-        ie::launch_parse_decode(reinterpret_cast<const uint32_t*>(c->d_dec), nbits, start_bit, da, n, c->d_state,
-                                c->tag, reinterpret_cast<unsigned*>(c->d_misc + 1), c->d_misc, c->stream);
-        HIPCHK(c, hipGetLastError());
-        uint64_t hm[2] = {0, 0};
-        HIPCHK(c, hipMemcpyAsync(hm, c->d_misc, sizeof(hm), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (hm[1] == 0) {  // err[0] (time-outs) and err[1] (fallback) both clear
-            c->last_rounds = 0;
-            c->last_fused = 1;
-            if (hm[0] > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
-            return finish_decode(c, out, dpix, out_dev, nframes, w, h, stride, frame_pitch, hm[0], end_bit);
-        }
+    ie::RecParseArgs pa{};
+    pa.words = reinterpret_cast<const uint32_t*>(c->d_dec);
+    pa.nbits = nbits;
+    pa.start_bit = start_bit;
+    pa.C = uint32_t(C);
+    pa.nchunks = nchunks;
+    pa.rle = da.rle;
+    pa.tab = c->d_rtab;
+    pa.base = c->d_walk;
+    pa.E = reinterpret_cast<uint32_t*>(c->d_walk + e_at);
+    pa.cnt = reinterpret_cast<uint32_t*>(c->d_walk + cnt_at);
+    pa.pos = c->d_rpos;
+    pa.ticket = reinterpret_cast<unsigned*>(c->d_misc + 1);
+    pa.total = c->d_misc + 2;
+    pa.end_out = c->d_misc;
+    HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 3 * sizeof(uint64_t), c->stream));
+    static const bool dstats = getenv("IE_DEC_STATS") != nullptr;
+    if (dstats) {
+        pa.stats = reinterpret_cast<unsigned long long*>(c->d_misc + 3);  // [3..7]
+        HIPCHK(c, hipMemsetAsync(c->d_misc + 3, 0, 5 * sizeof(uint64_t), c->stream));
     }
-    uint64_t* wk = c->d_walk;
-    const size_t cap = c->cap_walk / 4;
-    HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 4 * sizeof(uint64_t), c->stream));
-    const int rounds = ie::decode_frames_device(reinterpret_cast<const uint32_t*>(c->d_dec), nbits, start_bit, da, n,
-                                                chunk_bits, wk, wk + cap, wk + 2 * cap, c->d_count, wk + 3 * cap,
-                                                c->d_bb, reinterpret_cast<unsigned*>(c->d_misc + 1), c->d_misc,
-                                                c->stream, int(nchunks) + 2);
-    if (rounds < 0) return fail(c, IE_EHIP, "decode index walk failed");
+    if (ie::launch_rec_parse_decode(pa, da, n, c->stream) < 0) return fail(c, IE_EINVAL, "stream too long for one decode call");
     HIPCHK(c, hipGetLastError());
-    c->last_rounds = rounds;
-    c->last_fused = 0;
-    uint64_t end = 0;
-    HIPCHK(c, hipMemcpyAsync(&end, c->d_misc, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    c->last_chunks = nchunks;
+    c->last_groups = levels;
+    uint64_t hm[3] = {0, 0, 0};
+    HIPCHK(c, hipMemcpyAsync(hm, c->d_misc, sizeof(hm), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
+    const uint64_t end = hm[0];
+    if (dstats) {
+        uint64_t st[5];
+        HIPCHK(c, hipMemcpy(st, c->d_misc + 3, sizeof(st), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[dec] chunks %d C %u: lane-steps %.1f/chunk, beyond-window %.1f/chunk, unmerged walks %.2f/chunk, "
+                "wave max steps avg %.1f max %llu\n", nchunks, unsigned(C), double(st[0]) / nchunks, double(st[1]) / nchunks,
+                double(st[2]) / nchunks, double(st[3]) / nchunks, (unsigned long long)st[4]);
+        HIPCHK(c, hipMemsetAsync(c->d_misc + 3, 0, sizeof(uint64_t), c->stream));
+    }
+    if (hm[2] < nblocks || end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
     return finish_decode(c, out, dpix, out_dev, nframes, w, h, stride, frame_pitch, end, end_bit);
 }
 

@@ -32,22 +32,6 @@ constexpr int kZZ8[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11
                           58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 }  // namespace
 
-struct WalkArgs {
-    const uint32_t* words;  // stream as stored (big-endian bytes), zero-padded by >= 2 words
-    uint64_t nbits;         // stream length in bits
-    uint64_t start_bit;
-    uint64_t chunk_bits;
-    int nchunks;
-    int nn;                 // N*N
-    int rle;
-    uint64_t* entry;        // [nchunks]
-    const uint64_t* exit_in;
-    uint64_t* exit_out;
-    uint32_t* count;
-    unsigned* changed;
-    int first;              // speculative first pass
-};
-
 // bits [p, p+l) of the stream, l <= 32
 __device__ __forceinline__ uint32_t getbits(const uint32_t* W, uint64_t p, int l) {
     if (l == 0) return 0;
@@ -56,76 +40,9 @@ __device__ __forceinline__ uint32_t getbits(const uint32_t* W, uint64_t p, int l
     return uint32_t((v << (p & 31)) >> (64 - l));
 }
 
-__device__ __forceinline__ void walk(const WalkArgs& a, uint64_t pos, uint64_t end, uint64_t* exit_pos,
-                                     uint32_t* cnt, uint64_t* out_idx_base, uint64_t* block_bit, uint64_t nblocks) {
-    uint32_t c = 0;
-    while (pos < end && pos < a.nbits) {
-        const uint32_t head = getbits(a.words, pos, 20);
-        const int bl = int(head >> 16);
-        int lw;
-        bool ok;
-        if (a.rle) {
-            lw = bl ? int((head << 16 >> 16) >> (16 - bl)) : 0;
-            ok = bl >= 1 && lw <= a.nn;
-        } else {
-            lw = a.nn;
-            ok = bl >= 1;
-        }
-        if (!ok) {  // cannot be a record start: slide (never happens on the true path)
-            pos += 1;
-            continue;
-        }
-        if (block_bit) {
-            const uint64_t idx = *out_idx_base + c;
-            if (idx < nblocks) block_bit[idx] = pos;
-        }
-        c++;
-        pos += 4 + uint64_t(bl) * uint64_t(lw + a.rle);
-    }
-    *exit_pos = pos;
-    *cnt = c;
-}
-
-__global__ void walk_kernel(WalkArgs a) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= a.nchunks) return;
-    const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
-    const uint64_t cend = cstart + a.chunk_bits;
-    uint64_t e;
-    if (a.first) {
-        e = cstart;
-    } else {
-        if (k == 0) {
-            a.exit_out[0] = a.exit_in[0];
-            return;
-        }
-        e = a.exit_in[k - 1];
-        if (e == a.entry[k]) {
-            a.exit_out[k] = a.exit_in[k];
-            return;
-        }
-        atomicOr(a.changed, 1u);
-    }
-    a.entry[k] = e;
-    uint64_t x;
-    uint32_t c;
-    uint64_t dummy = 0;
-    walk(a, e, cend, &x, &c, &dummy, nullptr, 0);
-    a.exit_out[k] = x;
-    a.count[k] = c;
-}
-
-__global__ void index_kernel(WalkArgs a, const uint64_t* base, uint64_t* block_bit, uint64_t nblocks) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= a.nchunks) return;
-    const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
-    uint64_t x, b = base[k];
-    uint32_t c;
-    walk(a, a.entry[k], cstart + a.chunk_bits, &x, &c, &b, block_bit, nblocks);
-}
-
 // exclusive scan of per-chunk counts: one workgroup, each thread owns kScanRun consecutive counts
-// (one block scan per kTPB * kScanRun counts instead of one per kTPB)
+// (one block scan per kTPB * kScanRun counts instead of one per kTPB; measured faster than an
+// LDS-transposed coalesced variant)
 constexpr int kScanRun = 32;
 __global__ __launch_bounds__(kTPB) void scan_counts_kernel(const uint32_t* count, uint64_t* base, int n) {
     __shared__ uint32_t scratch[8];
@@ -149,64 +66,6 @@ __global__ __launch_bounds__(kTPB) void scan_counts_kernel(const uint32_t* count
         }
         carry += tot;
         __syncthreads();  // scratch is reused by the next strip's scan
-    }
-}
-
-// Inverse of one block: parse, dequantise, IDCT in the reference order, clamp/truncate.
-template <int N>
-__global__ __launch_bounds__(kTPB) void decode_kernel(DecArgs a, const uint32_t* W, uint64_t* end_out) {
-    constexpr int NN = N * N;
-    const uint64_t nblocks = uint64_t(a.nframes) * a.bx * a.by;
-    const uint64_t b = uint64_t(blockIdx.x) * kTPB + threadIdx.x;
-    if (b >= nblocks) return;
-    const EncTables* __restrict__ tab = a.tab;
-    uint64_t pos = a.block_bit[b];
-    const int bl = int(getbits(W, pos, 4));
-    pos += 4;
-    int length = NN;
-    if (a.rle) {
-        length = int(getbits(W, pos, bl));
-        pos += bl;
-    }
-    if (length > NN) length = NN;  // cannot happen for a well-formed stream
-    double Y[NN];
-#pragma unroll
-    for (int k = 0; k < NN; k++) Y[k] = 0.0;
-    const int* zz = (N == 4) ? kZZ4 : kZZ8;
-    for (int k = 0; k < length; k++) {
-        const uint32_t raw = getbits(W, pos, bl);
-        pos += bl;
-        const int sh = 16 - bl;
-        const int16_t v = int16_t(int16_t(uint16_t(raw << sh)) >> sh);
-        Y[zz[k]] = double(v);
-    }
-    if (b == nblocks - 1 && end_out) *end_out = pos;
-    // Block::processIDCTMulQ: Y *= q, then temp[ij] += R[uv][ij] * Y[uv] over uv ascending.
-    // Zero Y terms add +-0 and leave every partial sum unchanged, so they are skipped.
-    double t[NN];
-#pragma unroll
-    for (int k = 0; k < NN; k++) t[k] = 0.0;
-#pragma unroll
-    for (int uv = 0; uv < NN; uv++) {
-        const double y = Y[uv] * tab->qd[uv];
-        if (y != 0.0) {
-            const double* R = &tab->R[uv * NN];
-#pragma unroll
-            for (int ij = 0; ij < NN; ij++) t[ij] = t[ij] + R[ij] * y;
-        }
-    }
-    const uint64_t bpf = uint64_t(a.bx) * a.by;
-    const uint64_t f = b / bpf, r = b - f * bpf;
-    const int byi = int(r / a.bx), bxi = int(r - uint64_t(byi) * a.bx);
-    uint8_t* o = a.out + f * a.frame_pitch + uint64_t(byi) * N * a.stride + uint64_t(bxi) * N;
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-#pragma unroll
-        for (int j = 0; j < N; j++) {
-            double x = t[i * N + j] + 128.0;
-            x = x < 0.0 ? 0.0 : (x > 255.0 ? 255.0 : x);
-            o[uint64_t(i) * a.stride + j] = uint8_t(x);
-        }
     }
 }
 
@@ -371,40 +230,32 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
     return 0;
 }
 
-// ---- fused record parse + decode (one launch) ---------------------------------------------------
-// The stream is cut into SEGMENTS of kDecTPB * C bits, one workgroup each, staged in LDS with
-// coalesced loads (plus a margin covering the longest record).  Inside a segment every lane walks
-// C bits from a speculative entry, from LDS; local fix-up rounds (entry := the left neighbour's
-// exit) make the segment's path consistent from its first bit; that path's record starts are
-// marked in an LDS bitmap.  A record stream resynchronises within a few records, so the path
-// from the segment's TRUE entry (the predecessor's exit) merges with the marked path after a few
-// records and the segment's exit does not depend on its entry: every segment publishes its exit
-// at once, and its successor walks from it only up to the merge.  The true record count then
-// feeds a decoupled look-back (ie_common.hpp) for the global block index, and the lanes decode
-// their records straight from LDS: dequantise (Block.cpp:163-169), FP64 IDCT in the reference's
-// order (algo.cpp:343-363), +128, clamp, truncate (Block.cpp:100-107).  Should a walk from the
-// true entry not merge inside its segment (or a spin time out), the launch reports it in err[1]
-// and the host re-runs the multi-kernel path above.
-constexpr int kDecTPB = 256;
-template <int N> struct DecSeg {
-    static constexpr int C = (N == 4) ? 256 : 512;    // bits per lane
-    static constexpr int S = kDecTPB * C;              // bits per segment
-    static constexpr int MARGIN = 1024 + 64;           // > longest record (4 + 15 * 65) + 64-bit reads
-    static constexpr int WORDS = (S + MARGIN) / 32 + 2;
-    static constexpr int MAXPRE = 64;                  // records walked from the true entry before merging
-};
-
-struct FusedArgs {
-    const uint32_t* words;  // stream as stored (big-endian bytes), zero-padded
-    uint64_t nbits, start_bit;
-    int nseg;
-    int rle;
-    uint64_t* st;           // chain state (kGran words per segment): 0 count aggregate, 1 inclusive, 3 exit
-    uint32_t tag;
-    unsigned* err;          // [0] spin timeouts, [1] fallback needed (no merge / malformed)
-    uint64_t* end_out;      // end bit of the last block's record
-    DecArgs d;
-};
+// ---- exact record parse: transfer tables, composed -------------------------------------------
+// A record's length depends on its own header, so the stream is a serial chain.  Cut it into
+// chunks of C bits.  The first record starting at or after a chunk's first bit sits at an offset
+// d < D (D = the longest record, 4 + 15*(N*N+1) bits: the record straddling the boundary ends
+// within D bits).  So a chunk is a FUNCTION of d: walking from offset d gives the offset at which
+// the walk enters the next chunk -- its transfer table T_k[d] over all D entries.  Tables compose
+// (T_{k+1} o T_k), and the true entry of every chunk follows from the stream's start by composing
+// tables: exact for any content, with no speculation to converge (periodic streams, which lock
+// speculative walks into a wrong phase, cost nothing extra).
+//   rec_table_kernel   one wave per chunk: the D walks share their work through claims in LDS --
+//                      the first walk to reach a position owns it, a later walk that lands there
+//                      stops and takes the owner's exit -- so about one walk per chunk survives.
+//   rec_compose_kernel one workgroup per group of G tables: the group's tables in LDS, every entry
+//                      chased through them; the chase writes the group-relative prefix map P_j
+//                      over each table (group entry -> entry of table j) and the group's
+//                      composite.  Levels repeat on the composites until at most G remain; the
+//                      last workgroup of that level chases the stream's start through them.
+//   rec_count_kernel   one wave per chunk: entry = the prefix maps applied to its top-level entry;
+//                      the chunk's true records are walked from it: their positions, their count,
+//                      and the count added to a sum per 256 chunks.
+//   rec_decode_kernel  one wave per chunk: first block index = the sums before the chunk's 256,
+//                      plus the counts before it among them (one load per lane, a wave sum); the
+//                      lanes decode the records: dequantise (Block.cpp:163-169), FP64 IDCT in the
+//                      reference's order (algo.cpp:343-363), +128, clamp, truncate
+//                      (Block.cpp:100-107).
+constexpr uint32_t kNoOwner = 0xFFFFu;
 
 // bits [p, p+l) of the LDS stream copy L (MSB-first words), l <= 32, p relative to the copy
 __device__ __forceinline__ uint32_t lbits(const uint32_t* L, uint32_t p, int l) {
@@ -413,42 +264,56 @@ __device__ __forceinline__ uint32_t lbits(const uint32_t* L, uint32_t p, int l) 
     return l ? uint32_t((v << s) >> (64 - l)) : 0u;
 }
 
-// length of the record whose header is at p, 0 if no record can start there
+// length of the record whose 20 header bits (bl:4, then the RLE length's bl bits) are `head`; 1
+// if no record can start there (a walk slides one bit; never on the true path of a well-formed
+// stream)
 template <int N>
-__device__ __forceinline__ uint32_t rec_len(const uint32_t* L, uint32_t p, int rle) {
+__device__ __forceinline__ uint32_t rec_len_head(uint32_t head, int rle) {
     constexpr int NN = N * N;
-    const uint32_t head = lbits(L, p, 20);
     const uint32_t bl = head >> 16;
-    if (!bl) return 0;
+    if (!bl) return 1u;
     if (!rle) return 4u + bl * NN;
     const uint32_t lw = (head & 0xFFFFu) >> (16 - bl);
-    return lw <= uint32_t(NN) ? 4u + bl * (lw + 1u) : 0u;
+    return lw <= uint32_t(NN) ? 4u + bl * (lw + 1u) : 1u;
+}
+// length of the record at p, 0 if no record can start there
+template <int N>
+__device__ __forceinline__ uint32_t rec_len(const uint32_t* L, uint32_t p, int rle) {
+    const uint32_t l = rec_len_head<N>(lbits(L, p, 20), rle);
+    return l > 1u ? l : 0u;
 }
 
-// speculative walk of [e, end): exit position and record count (invalid headers slide one bit)
-template <int N>
-__device__ __forceinline__ uint32_t spec_walk(const uint32_t* L, uint32_t e, uint32_t end, uint32_t lim, int rle,
-                                              uint32_t* cnt, uint32_t* bitmap) {
-    uint32_t c = 0;
-    while (e < end && e < lim) {
-        const uint32_t len = rec_len<N>(L, e, rle);
-        if (!len) {
-            e++;
-            continue;
-        }
-        if (bitmap) atomicOr(&bitmap[e >> 5], 1u << (e & 31u));
-        c++;
-        e += len;
+__host__ __device__ constexpr int rec_table_stream_words(uint32_t C) { return int((C + 95) >> 5) + 3; }
+__host__ __device__ constexpr int rec_decode_stream_words(uint32_t C, int D) { return int((C + D + 95) >> 5) + 3; }
+
+
+// words [w0, w0 + nw) of the stream, byte-swapped to MSB-first, zeros past the stream
+__device__ __forceinline__ void stage_words(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nwords,
+                                            int tid, int nthreads) {
+    for (int i = tid; i < nw; i += nthreads)
+        L[i] = (w0 + i < nwords) ? bswap32(__builtin_nontemporal_load(W + w0 + i)) : 0u;
+}
+
+// zig-zag rank of every coefficient position (the inverse of kZZ4 / kZZ8)
+template <int N> struct InvZZ {
+    int r[N * N];
+    constexpr InvZZ() : r() {
+        for (int k = 0; k < N * N; k++) r[(N == 4) ? kZZ4[k] : kZZ8[k]] = k;
     }
-    *cnt = c;
-    return e;
-}
+};
 
-// decode the record at p (relative to L) as block g; returns the bit after it
+// decode the record at p (relative to L) as block g; returns the bit after it.  Coefficient uv
+// (row-major) is value number izz[uv] of the record, read straight from its bit position, so the
+// IDCT runs in the reference's uv-ascending order without a zig-zag array.
+// sR / sq: the FP64 cos products R[uv][ij] and the quantiser through the constant address space:
+// the loads are uniform, so they become scalar loads and the FP64 multiplies take their operands
+// from SGPRs
+using const_f64 = const __attribute__((address_space(4))) double*;
 template <int N>
-__device__ __forceinline__ uint32_t decode_record(const uint32_t* L, uint32_t p, uint64_t g, const DecArgs& a) {
+__device__ __forceinline__ uint32_t decode_record(const uint32_t* L, uint32_t p, uint64_t g, const DecArgs& a,
+                                                  const_f64 sR, const_f64 sq) {
     constexpr int NN = N * N;
-    const EncTables* __restrict__ tab = a.tab;
+    constexpr InvZZ<N> izz;
     const int bl = int(lbits(L, p, 4));
     p += 4;
     int length = NN;
@@ -457,24 +322,24 @@ __device__ __forceinline__ uint32_t decode_record(const uint32_t* L, uint32_t p,
         p += bl;
     }
     if (length > NN) length = NN;
-    double Y[NN];
-#pragma unroll
-    for (int k = 0; k < NN; k++) Y[k] = 0.0;
-    const int* zz = (N == 4) ? kZZ4 : kZZ8;
-    for (int k = 0; k < length; k++) {
-        const uint32_t raw = lbits(L, p, bl);
-        p += bl;
-        const int sh = 16 - bl;
-        Y[zz[k]] = double(int16_t(int16_t(uint16_t(raw << sh)) >> sh));
-    }
+    const int sh = 16 - bl;
+    // Block::processIDCTMulQ: Y *= q, then temp[ij] += R[uv][ij] * Y[uv] over uv ascending.  A
+    // zero Y term adds +-0: it leaves every partial sum unchanged but possibly the sign of a zero,
+    // which +128 and the clamp erase, so a term is skipped when it is zero in every lane (the
+    // branch stays uniform and the R rows come through the scalar cache).
     double t[NN];
 #pragma unroll
     for (int k = 0; k < NN; k++) t[k] = 0.0;
 #pragma unroll
     for (int uv = 0; uv < NN; uv++) {
-        const double y = Y[uv] * tab->qd[uv];
-        if (y != 0.0) {
-            const double* R = &tab->R[uv * NN];
+        const int kz = izz.r[uv];
+        double y = 0.0;
+        if (kz < length) {
+            const uint32_t raw = lbits(L, p + uint32_t(kz * bl), bl);
+            y = double(int16_t(int16_t(uint16_t(raw << sh)) >> sh)) * sq[uv];  // utils.hpp:265-269
+        }
+        if (__ballot(y != 0.0)) {
+            const_f64 R = sR + uv * NN;
 #pragma unroll
             for (int ij = 0; ij < NN; ij++) t[ij] = t[ij] + R[ij] * y;
         }
@@ -503,232 +368,343 @@ __device__ __forceinline__ uint32_t decode_record(const uint32_t* L, uint32_t p,
             for (int j = 0; j < N; j++) row[j] = uint8_t(wv[j / 4] >> (8 * (j % 4)));
         }
     }
-    return p;
+    return p + uint32_t(length * bl);
+}
+
+// One wave tabulates M consecutive chunks.  All M*D walks run in one loop (entry e = lane,
+// lane + 64, ...; a lane starts its next walk as soon as one ends), interleaved over the chunks,
+// so the long walks of the M chunks run side by side in different lanes.  A walk steps between
+// valid record headers (a precomputed bitmap: an invalid header slides a walk to the next valid
+// one) and claims every position it visits -- the first walk to reach a position owns it; a walk
+// landing on an owned position stops and takes the owner's exit.  Claims live in a small
+// open-addressing hash table per chunk ((position << 16 | owner) words set by compare-and-swap):
+// a chunk's walks visit a few hundred positions, not all C.  Claims only save work -- a walk that
+// finds the table full just walks on -- so the tables are exact whatever the content.  Wrong-phase
+// walks step a few bits at a time and meet each other often, so a chunk keeps about one of them
+// alive besides its true path.
+template <int N>
+__global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
+    constexpr int D = RecGeom<N>::D, M = RecGeom<N>::M, E = M * D, HS = RecGeom<N>::HS;
+    constexpr int PER = (E + 63) / 64;
+    // dynamic LDS: the M chunks' bits (+ 64 for the last header) and their valid-header bitmap
+    extern __shared__ uint32_t L[];
+    __shared__ uint32_t H[M][HS];
+    __shared__ uint16_t res[E];
+    __shared__ uint16_t tgt[E];
+    const int lane = threadIdx.x, k0 = blockIdx.x * M;
+    const int m = min(M, a.nchunks - k0);           // chunks of this wave
+    const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
+    const uint64_t base = c0 & ~31ull;
+    const uint32_t s0 = uint32_t(c0 - base), C = a.C, CW = C >> 5;
+    const uint64_t lim64 = a.nbits - base;          // stream end relative to L: no record starts there or later
+    const uint32_t lim = uint32_t(min<uint64_t>(lim64, uint64_t(s0) + uint64_t(m) * C));
+    uint32_t* VB = L + rec_table_stream_words(uint32_t(M) * C);
+    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, (a.nbits + 31) >> 5, lane, 64);
+    for (int i = lane; i < M * HS; i += 64) (&H[0][0])[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    // 1. valid headers of every position (the 32 headers of a word from one 64-bit window)
+    for (uint32_t i = lane; i < uint32_t(m) * CW; i += 64) {
+        const uint32_t p0 = s0 + (i << 5);
+        uint32_t msk = 0;
+        if (p0 < lim) {
+            const uint32_t w0 = p0 >> 5, sb = p0 & 31u;
+            const uint64_t v = (((uint64_t(L[w0]) << 32) | L[w0 + 1]) << sb) |
+                               (sb ? (uint64_t(L[w0 + 2]) >> (32 - sb)) : 0ull);
+#pragma unroll
+            for (uint32_t q = 0; q < 32; q++)
+                msk |= (rec_len_head<N>(uint32_t((v << q) >> 44), a.rle) > 1u ? 1u : 0u) << q;
+            const uint32_t cut = lim - p0;  // no record starts at or past the stream's end
+            if (cut < 32u) msk &= (1u << cut) - 1u;
+        }
+        VB[i] = msk;
+    }
+    __syncthreads();
+    // 2. the walks
+    {
+        // entry e is offset e / M of chunk e % M: the first offsets of all M chunks -- where
+        // their surviving walks start -- run together in the first pass
+        uint32_t e = lane, p = 0, cs = 0, ce = 0, j = 0, id = 0;
+        uint32_t nsteps = 0, nwin = 0, nbey = 0;
+        bool fresh = true;
+        while (e < uint32_t(M * D)) {
+            nsteps++;
+            if (fresh) {
+                j = e % M;
+                const uint32_t d = e / M;
+                if (j >= uint32_t(m)) {  // no such chunk
+                    e += 64;
+                    continue;
+                }
+                id = j * D + d;  // index of the entry in res / tgt
+                cs = j * C;      // chunk-relative positions below are offsets from s0 + cs
+                ce = cs + C;
+                p = cs + d;
+                fresh = false;
+            }
+            bool done = false;
+            uint32_t t = kNoOwner;
+            if (p < ce) {
+                // next valid position of the chunk (or its end)
+                uint32_t wi = p >> 5, msk = VB[wi] & (0xFFFFFFFFu << (p & 31u));
+                const uint32_t wend = ce >> 5;
+                while (!msk && ++wi < wend) msk = VB[wi];
+                p = msk ? (wi << 5) + uint32_t(__builtin_ctz(msk)) : ce;
+            }
+            if (p >= ce) {
+                done = true;
+            } else {
+                const uint32_t head = lbits(L, s0 + p, 20);
+                const uint32_t key = (p - cs) << 16;  // chunk-relative position
+                uint32_t h = ((p - cs) * 2654435761u) >> (32 - RecGeom<N>::HSB);
+                for (int probe = 0; probe < HS; probe++) {
+                    const uint32_t o = atomicCAS(&H[j][h], 0xFFFFFFFFu, key | id);
+                    if (o == 0xFFFFFFFFu) break;                  // claimed
+                    if ((o & 0xFFFF0000u) == key) {               // owned: merge
+                        t = o & 0xFFFFu;
+                        done = true;
+                        break;
+                    }
+                    h = (h + 1) & uint32_t(HS - 1);               // another position: probe on
+                }
+                if (!done) p += rec_len_head<N>(head, a.rle);
+            }
+            if (done) {
+                if (t == kNoOwner) nwin++;
+                tgt[id] = uint16_t(t);
+                if (t == kNoOwner) res[id] = uint16_t(p - ce);
+                e += 64;
+                fresh = true;
+            }
+        }
+        if (a.stats) {
+            const uint32_t mx = __reduce_max_sync(~0ull, nsteps);
+            atomicAdd(&a.stats[0], uint64_t(nsteps));
+            atomicAdd(&a.stats[1], uint64_t(nbey));
+            atomicAdd(&a.stats[2], uint64_t(nwin));
+            if (lane == 0) { atomicAdd(&a.stats[3], uint64_t(mx)); atomicMax(&a.stats[4], uint64_t(mx)); }
+        }
+    }
+    __syncthreads();
+    // 3. an entry takes its owner's exit once the owner is resolved; else it jumps to its owner's
+    //    owner (owner chains climb to strictly later positions, so they end; pointer jumping
+    //    halves them every round)
+    for (;;) {
+        uint32_t nr[PER], nt[PER];
+        bool pend = false;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int e = lane + 64 * i;
+            nr[i] = kNoOwner;
+            nt[i] = kNoOwner;
+            if (e < m * D) {  // (entries of chunks past the stream's last never ran)
+                const uint32_t o = tgt[e];
+                if (o != kNoOwner) {
+                    const uint32_t oo = tgt[o];
+                    if (oo == kNoOwner) {
+                        nr[i] = res[o];
+                    } else {
+                        nt[i] = oo;
+                        pend = true;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int e = lane + 64 * i;
+            if (nr[i] != kNoOwner) {
+                res[e] = uint16_t(nr[i]);
+                tgt[e] = uint16_t(kNoOwner);
+            } else if (nt[i] != kNoOwner) {
+                tgt[e] = uint16_t(nt[i]);
+            }
+        }
+        if (!__syncthreads_or(pend)) break;
+    }
+    uint16_t* T = a.tab + size_t(k0) * D;
+    for (int e = lane; e < m * D; e += 64) T[e] = res[e];
+}
+
+// One composition level over n tables ([n][D], 16-bit exits): prefix maps written over the
+// tables, composites into comp ([ceil(n/G)][D]); with `top`, the last workgroup chases the
+// stream's start (entry 0) through the composites: E[q] = entry of composite q.
+template <int N>
+__global__ __launch_bounds__(kTPB) void rec_compose_kernel(uint16_t* tab, int n, uint16_t* comp, int top,
+                                                           uint32_t* E, unsigned* ticket) {
+    constexpr int D = RecGeom<N>::D, G = RecGeom<N>::G;
+    __shared__ uint16_t S[G * D];
+    __shared__ unsigned last;
+    const int tid = threadIdx.x, g = blockIdx.x, ng = gridDim.x;
+    const int k0 = g * G, nk = min(G, n - k0);
+    uint16_t* T = tab + size_t(k0) * D;
+    for (int i = tid; i < nk * D; i += kTPB) S[i] = T[i];
+    __syncthreads();
+    for (int d = tid; d < D; d += kTPB) {
+        uint32_t x = uint32_t(d);
+        for (int j = 0; j < nk; j++) {
+            T[j * D + d] = uint16_t(x);  // P_j: group entry d -> entry of table j
+            x = S[j * D + x];
+        }
+        comp[size_t(g) * D + d] = uint16_t(x);
+    }
+    if (!top) return;
+    // the last workgroup to finish sees every composite
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) last = (atomicAdd(ticket, 1u) == unsigned(ng) - 1u) ? 1u : 0u;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    for (int i = tid; i < ng * D; i += kTPB) S[i] = comp[i];  // ng <= G
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t x = 0;
+        for (int q = 0; q < ng; q++) {
+            E[q] = x;
+            x = S[q * D + x];
+        }
+        *ticket = 0u;  // re-armed for the next decode
+    }
+}
+
+// the chunk's entry offset: its top-level entry, then the prefix maps of every level down to its table
+template <int N>
+__device__ __forceinline__ uint32_t rec_chunk_entry(const RecParseArgs& a, int k) {
+    constexpr int D = RecGeom<N>::D, G = RecGeom<N>::G;
+    int u = k;
+    for (int l = 0; l < a.levels; l++) u /= G;
+    uint32_t x = a.E[u];
+    for (int l = a.levels - 1; l >= 0; l--) {
+        int ul = k;
+        for (int m = 0; m < l; m++) ul /= G;
+        x = a.lvl[l][size_t(ul) * D + x];
+    }
+    return x;
+}
+
+// Count pass: one LANE per chunk walks its true records from global memory (a record header is
+// one 64-bit window read; consecutive reads of a lane hit the same lines), storing up to
+// kRecPosCap record positions and the count.  Lanes of a wave walk 64 different chunks, so the
+// serial walks run 64 wide.
+template <int N>
+__global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
+    const int k = int(blockIdx.x * kTPB + threadIdx.x);
+    if (k >= a.nchunks) return;
+    const uint64_t c0 = a.start_bit + uint64_t(k) * a.C;
+    const uint64_t base = c0 & ~31ull;
+    const uint64_t end = min<uint64_t>(c0 + a.C, a.nbits);  // no record starts at or past the stream's end
+    uint64_t p = c0 + rec_chunk_entry<N>(a, k);
+    uint16_t* pos = a.pos + size_t(k) * kRecPosCap;
+    uint32_t R = 0;
+    while (p < end) {
+        const uint32_t l = rec_len_head<N>(getbits(a.words, p, 20), a.rle);
+        if (l > 1u) {
+            if (R < uint32_t(kRecPosCap)) pos[R] = uint16_t(p - base);
+            R++;
+        }
+        p += l;
+    }
+    a.cnt[k] = R;
 }
 
 template <int N>
-__global__ __launch_bounds__(kDecTPB) void parse_decode_kernel(FusedArgs a) {
-    using G = DecSeg<N>;
-    __shared__ uint32_t L[G::WORDS];
-    __shared__ uint32_t mark[G::S / 32 + 1];
-    __shared__ uint32_t X[kDecTPB];
-    __shared__ uint32_t pre[G::MAXPRE];
-    __shared__ uint32_t misc[24];  // [0..3] scan scratch, [4] any, [5] merge, [6] c_pre, [8..9] excl, [10] fail
-    const int tid = threadIdx.x, k = blockIdx.x;
-    const uint64_t seg0 = a.start_bit + uint64_t(k) * G::S;  // the segment's first bit
-    const uint64_t base = seg0 & ~31ull;                       // bit 0 of L
-    const uint32_t s0 = uint32_t(seg0 - base);                 // segment start, relative
-    const uint32_t s1 = s0 + G::S;                             // segment end (exclusive), relative
-    const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(G::WORDS - 2) * 32));  // readable bits
-    // 1. stage the segment's bits (MSB-first words), zeros past the stream
-    const uint64_t w0 = base >> 5, nw = (a.nbits + 31) >> 5;
-    for (int i = tid; i < G::WORDS; i += kDecTPB)
-        L[i] = (w0 + i < nw) ? bswap32(__builtin_nontemporal_load(a.words + w0 + i)) : 0u;
-    for (int i = tid; i < G::S / 32 + 1; i += kDecTPB) mark[i] = 0u;
-    __syncthreads();
-    // 2. speculative lane walks, then local rounds until every lane continues its neighbour's path
-    const uint32_t lane_end = s0 + uint32_t(tid + 1) * G::C;
-    uint32_t entry = s0 + uint32_t(tid) * G::C, cnt;
-    uint32_t ex = spec_walk<N>(L, entry, lane_end, lim, a.rle, &cnt, nullptr);
-    for (int round = 0; round <= kDecTPB; round++) {
-        X[tid] = ex;
-        __syncthreads();
-        const uint32_t ne = tid ? X[tid - 1] : s0;
-        const bool ch = ne != entry;
-        if (ch) {
-            entry = ne;
-            ex = spec_walk<N>(L, entry, lane_end, lim, a.rle, &cnt, nullptr);
+__global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a, DecArgs d) {
+    constexpr int D = RecGeom<N>::D;
+    extern __shared__ uint32_t dyn_all[];  // per wave: the chunk's bits + D + 64 (the last record's body)
+    const const_f64 sR = (const_f64)(d.tab->R);
+    const const_f64 sq = (const_f64)(d.tab->qd);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = blockIdx.x * kRecWPB + wv;
+    if (k >= a.nchunks) return;
+    uint32_t* L = dyn_all + size_t(wv) * rec_decode_stream_words(a.C, D);
+    const uint64_t c0 = a.start_bit + uint64_t(k) * a.C;
+    const uint64_t base = c0 & ~31ull;
+    const uint32_t s0 = uint32_t(c0 - base), end = s0 + a.C;
+    const uint64_t first = a.base[k];  // first block index (scan of the counts)
+    const uint32_t R = a.cnt[k];
+    if (k == a.nchunks - 1 && lane == 0) *a.total = first + R;
+    stage_words(L, a.words, base >> 5, int((end + D + 64) >> 5) + 2, (a.nbits + 31) >> 5, lane, 64);
+    wave_sync();
+    const uint64_t nblocks = uint64_t(d.nframes) * d.bx * d.by;
+    if (R <= uint32_t(kRecPosCap)) {
+        const uint16_t* pos = a.pos + size_t(k) * kRecPosCap;
+        for (uint32_t i = lane; i < R; i += 64) {
+            const uint64_t b = first + i;
+            if (b >= nblocks) break;
+            const uint32_t q = decode_record<N>(L, pos[i], b, d, sR, sq);
+            if (b == nblocks - 1) *a.end_out = base + q;
         }
-        if (!__syncthreads_or(ch)) break;
+        return;
     }
-    // 3. mark the segment's path; its exit is published at once (entry-independent, see above)
-    spec_walk<N>(L, entry, lane_end, lim, a.rle, &cnt, mark);
-    __syncthreads();  // marks visible
-    if (tid == kDecTPB - 1) st_state(&a.st[kGran * k + 3], (uint64_t(a.tag) << 56) | ((base + ex) & kMask56));
-    // 4. the true entry (predecessor's exit) and the walk from it to the merge with the marked path
-    if (tid == 0) {
-        uint64_t e = a.start_bit;
-        bool ok = true;
-        if (k > 0) {
-            unsigned sp = 0;
-            for (;;) {
-                const uint64_t g = ld_state(&a.st[kGran * (k - 1) + 3]);
-                if (uint32_t(g >> 56) == a.tag) {
-                    e = g & kMask56;
-                    break;
-                }
-                if (++sp > kSpinLimit) {
-                    atomicAdd(&a.err[0], 1u);
-                    ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
+    // more records than the position list holds: walk them again, 64 at a time
+    uint32_t p = s0 + rec_chunk_entry<N>(a, k);
+    const uint32_t wend = uint32_t(min<uint64_t>(end, a.nbits - base));
+    uint64_t gi = first;
+    while (p < wend && gi < nblocks) {
+        uint32_t mine = 0, n = 0;
+        while (n < 64u && p < wend) {
+            const uint32_t len = rec_len<N>(L, p, d.rle);
+            if (!len) {
+                p++;
+                continue;
             }
-        }
-        uint32_t p = uint32_t(e - base), c = 0;
-        // walk until a marked record start (the merge), the segment's end or the stream's end
-        while (ok && p < s1 && p < lim && !((mark[p >> 5] >> (p & 31u)) & 1u)) {
-            const uint32_t len = rec_len<N>(L, p, a.rle);
-            if (!len || c == G::MAXPRE) {  // malformed, or no merge within reach: fall back
-                ok = false;
-                break;
-            }
-            pre[c++] = p;
+            if (n == uint32_t(lane)) mine = p;
+            n++;
             p += len;
         }
-        // no merge inside the segment: its true exit must be the published one, else fall back
-        if (ok && p >= s1 && k != a.nseg - 1 && p != X[kDecTPB - 1]) ok = false;
-        misc[10] = ok ? 0u : 1u;
-        misc[5] = p;
-        misc[6] = c;
-    }
-    __syncthreads();
-    // (a fallback still publishes a count below, so successors' look-backs terminate; the host
-    // discards this launch's output)
-    if (misc[10] && tid == 0) atomicOr(&a.err[1], 1u);
-    const uint32_t m = misc[5], c_pre = misc[6];
-    // 5. true count = records before the merge + marked records from the merge on
-    uint32_t mine = 0;  // this lane's path records at or after m (the true records among them)
-    for (uint32_t e2 = entry; e2 < lane_end && e2 < lim;) {
-        const uint32_t len = rec_len<N>(L, e2, a.rle);
-        if (!len) {
-            e2++;
-            continue;
+        const uint64_t b = gi + lane;
+        if (uint32_t(lane) < n && b < nblocks) {
+            const uint32_t q = decode_record<N>(L, mine, b, d, sR, sq);
+            if (b == nblocks - 1) *a.end_out = base + q;
         }
-        mine += (e2 >= m) ? 1u : 0u;
-        e2 += len;
-    }
-    uint32_t tot2;
-    const uint32_t off = block_excl_scan<kDecTPB>(mine, misc, &tot2);
-    const uint32_t A = c_pre + tot2;
-    // 6. global index of the segment's first block: decoupled look-back over the counts
-    if (tid == 0) chain_publish_count(a.st, k, k, a.tag, A);
-    if (tid < 64 && k > 0) {
-        const Probe pr = probe_issue(a.st, k, k, 1, 0, kProbe0);
-        const uint64_t excl = lookback_wave(pr, a.st, k, k, 1, a.tag, a.err);
-        if (tid == 0) {
-            publish(a.st, k, 1, a.tag, excl + A);
-            misc[8] = uint32_t(excl);
-            misc[9] = uint32_t(excl >> 32);
-        }
-    } else if (tid == 0) {
-        misc[8] = 0u;
-        misc[9] = 0u;
-    }
-    __syncthreads();
-    const uint64_t excl = uint64_t(misc[8]) | (uint64_t(misc[9]) << 32);
-    // 7. decode: the pre-merge records (thread 0), then every lane's records from the merge on
-    const uint64_t nblocks = uint64_t(a.d.nframes) * a.d.bx * a.d.by;
-    if (tid == 0) {
-        for (uint32_t i = 0; i < c_pre; i++) {
-            const uint64_t g = excl + i;
-            if (g < nblocks) {
-                const uint32_t q = decode_record<N>(L, pre[i], g, a.d);
-                if (g == nblocks - 1) *a.end_out = base + q;
-            }
-        }
-    }
-    uint64_t g = excl + c_pre + off;
-    uint32_t e3 = entry;
-    while (e3 < lane_end && e3 < lim && g < nblocks) {
-        const uint32_t len = rec_len<N>(L, e3, a.rle);
-        if (!len) {
-            e3++;
-            continue;
-        }
-        if (e3 >= m) {
-            const uint32_t q = decode_record<N>(L, e3, g, a.d);
-            if (g == nblocks - 1) *a.end_out = base + q;
-            g++;
-        }
-        e3 += len;
+        gi += n;
     }
 }
 
-uint64_t parse_decode_segment_bits(int n) { return (n == 4) ? DecSeg<4>::S : DecSeg<8>::S; }
-
-// One launch: returns the number of segments (the host checks err[1] afterwards).
-int launch_parse_decode(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& d, int n,
-                        uint64_t* st, uint32_t tag, unsigned* err, uint64_t* end_out, hipStream_t s) {
-    const uint64_t S = (n == 4) ? DecSeg<4>::S : DecSeg<8>::S;
-    const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
-    const int nseg = int((span + S - 1) / S);
-    if (nseg == 0) return 0;
-    FusedArgs a{};
-    a.words = W;
-    a.nbits = nbits;
-    a.start_bit = start_bit;
-    a.nseg = nseg;
-    a.rle = d.rle;
-    a.st = st;
-    a.tag = tag;
-    a.err = err;
-    a.end_out = end_out;
-    a.d = d;
-    if (n == 4) hipLaunchKernelGGL((parse_decode_kernel<4>), dim3(nseg), dim3(kDecTPB), 0, s, a);
-    else hipLaunchKernelGGL((parse_decode_kernel<8>), dim3(nseg), dim3(kDecTPB), 0, s, a);
-    return nseg;
+int rec_group_chunks(int n) { return n == 4 ? RecGeom<4>::G : RecGeom<8>::G; }
+int rec_entry_span(int n) { return n == 4 ? RecGeom<4>::D : RecGeom<8>::D; }
+size_t rec_table_lds(uint32_t C, int n) {
+    const int M = n == 4 ? RecGeom<4>::M : RecGeom<8>::M;
+    return size_t(rec_table_stream_words(uint32_t(M) * C) + M * (C >> 5)) * 4;
 }
+size_t rec_decode_lds(uint32_t C, int n) { return size_t(rec_decode_stream_words(C, rec_entry_span(n))) * 4 * kRecWPB; }
 
-// Host-driven decode sequence (ie_capi.cpp::decode calls this).
-int decode_frames_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& da, int n,
-                         uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,
-                         uint64_t* base, uint64_t* block_bit, unsigned* changed, uint64_t* end_out, hipStream_t s,
-                         int max_rounds) {
-    const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
-    const int nchunks = int(span / chunk_bits + 1);
-    WalkArgs wa{};
-    wa.words = W;
-    wa.nbits = nbits;
-    wa.start_bit = start_bit;
-    wa.chunk_bits = chunk_bits;
-    wa.nchunks = nchunks;
-    wa.nn = n * n;
-    wa.rle = da.rle;
-    wa.entry = entry;
-    wa.count = count;
-    wa.changed = changed;
-    const dim3 g((nchunks + kTPB - 1) / kTPB), blk(kTPB);
-    wa.first = 1;
-    wa.exit_in = exA;
-    wa.exit_out = exA;
-    hipLaunchKernelGGL(walk_kernel, g, blk, 0, s, wa);
-    uint64_t* cur = exA;
-    uint64_t* nxt = exB;
-    // fix-up rounds in growing groups (1, 2, 4, 8, 8, ...) between host checks: most 4x4 streams
-    // settle after one round, 8x8 ones take ~20; a round after convergence is a near-empty launch
-    // (~15 us), a host round trip per round costs more
-    int rounds = 0, group = 1;
-    bool done = false;
-    // (convergence takes at most max_rounds rounds; a group after it confirms it)
-    while (!done && rounds < max_rounds + 8) {
-        unsigned h = 0;
-        if (hipMemsetAsync(changed, 0, sizeof(unsigned), s) != hipSuccess) return -1;
-        for (int r = 0; r < group; r++) {
-            wa.first = 0;
-            wa.exit_in = cur;
-            wa.exit_out = nxt;
-            hipLaunchKernelGGL(walk_kernel, g, blk, 0, s, wa);
-            uint64_t* t = cur;
-            cur = nxt;
-            nxt = t;
+int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t s) {
+    if (a.nchunks <= 0) return 0;
+    const int G = rec_group_chunks(n), D = rec_entry_span(n);
+    const int nb = (a.nchunks + kRecWPB - 1) / kRecWPB;  // blocks of kRecWPB chunk waves
+    // composition levels: tables of level l+1 are the composites of level l
+    int cur = a.nchunks, levels = 0;
+    uint16_t* arr = a.tab;
+    for (;;) {
+        const int ng = (cur + G - 1) / G;
+        const int top = ng <= G ? 1 : 0;
+        if (levels >= kRecMaxLevels) return -1;
+        a.lvl[levels] = arr;
+        uint16_t* comp = arr + size_t(cur) * D;
+        if (levels == 0) {
+            const int M = n == 4 ? RecGeom<4>::M : RecGeom<8>::M;
+            const int nt = (a.nchunks + M - 1) / M;
+            if (n == 4) hipLaunchKernelGGL((rec_table_kernel<4>), dim3(nt), dim3(64), rec_table_lds(a.C, 4), s, a);
+            else hipLaunchKernelGGL((rec_table_kernel<8>), dim3(nt), dim3(64), rec_table_lds(a.C, 8), s, a);
         }
-        rounds += group;
-        group = group < 8 ? 2 * group : 8;
-        if (hipMemcpyAsync(&h, changed, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
-        if (hipStreamSynchronize(s) != hipSuccess) return -1;
-        done = (h == 0);
+        if (n == 4)
+            hipLaunchKernelGGL((rec_compose_kernel<4>), dim3(ng), dim3(kTPB), 0, s, arr, cur, comp, top, a.E, a.ticket + 1);
+        else
+            hipLaunchKernelGGL((rec_compose_kernel<8>), dim3(ng), dim3(kTPB), 0, s, arr, cur, comp, top, a.E, a.ticket + 1);
+        levels++;
+        if (top) break;
+        arr = comp;
+        cur = ng;
     }
-    if (!done) return -2;
-    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
-    hipLaunchKernelGGL(index_kernel, g, blk, 0, s, wa, base, block_bit, uint64_t(da.nframes) * da.bx * da.by);
-    DecArgs d = da;
-    d.block_bit = block_bit;
-    const uint64_t nblocks = uint64_t(da.nframes) * da.bx * da.by;
-    const dim3 gd(unsigned((nblocks + kTPB - 1) / kTPB));
-    if (n == 4) hipLaunchKernelGGL((decode_kernel<4>), gd, blk, 0, s, d, W, end_out);
-    else hipLaunchKernelGGL((decode_kernel<8>), gd, blk, 0, s, d, W, end_out);
-    return rounds;
+    a.levels = levels;
+    const int nbc = (a.nchunks + kTPB - 1) / kTPB;
+    if (n == 4) hipLaunchKernelGGL((rec_count_kernel<4>), dim3(nbc), dim3(kTPB), 0, s, a);
+    else hipLaunchKernelGGL((rec_count_kernel<8>), dim3(nbc), dim3(kTPB), 0, s, a);
+    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(kTPB), 0, s, a.cnt, a.base, a.nchunks);
+    if (n == 4) hipLaunchKernelGGL((rec_decode_kernel<4>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 4), s, a, d);
+    else hipLaunchKernelGGL((rec_decode_kernel<8>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 8), s, a, d);
+    return levels;
 }
 
 }  // namespace ie

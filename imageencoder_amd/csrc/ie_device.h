@@ -146,26 +146,52 @@ void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uin
                        unsigned long long* first, unsigned* unresolved, hipStream_t s, bool counts = true);
 
 struct DecArgs {
-    const uint64_t* block_bit;  // [nblocks] start bit of every block record (from the walk index)
     int nframes, bx, by, rle;
     uint8_t* out;
     uint64_t stride, frame_pitch;
     const EncTables* tab;
 };
-// Parallel record index (chunk walks + fix-up rounds) followed by the block decode.  Returns the
-// number of fix-up rounds (>= 0) or < 0 on error.
-int decode_frames_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& da, int n,
-                         uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,
-                         uint64_t* base, uint64_t* block_bit, unsigned* changed, uint64_t* end_out, hipStream_t s,
-                         int max_rounds);
 
-// Fused parse + decode in one launch (segments in LDS, speculative walks merged with the true
-// path, decoupled look-back over record counts).  err[1] != 0 afterwards: re-run the path above.
-// st / tag: the encoder's chain state (granules 0, 1 and 3 of every segment).  Returns the
-// number of segments.
-int launch_parse_decode(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const DecArgs& d, int n,
-                        uint64_t* st, uint32_t tag, unsigned* err, uint64_t* end_out, hipStream_t s);
-uint64_t parse_decode_segment_bits(int n);
+// Exact record parse + decode (ie_decode.hip): per-chunk transfer tables over every entry offset
+// [0, D), composed per group of G tables (levels until at most G remain), then the decode with a
+// look-back over record counts; no host round trip.  D = the longest record (4 + 15*(N*N+1) bits).
+#ifndef IE_REC_M
+#define IE_REC_M 1  // measured on 4K streams: 1 beats 2, 4 and 8 (occupancy over lane packing)
+#endif
+template <int N> struct RecGeom {
+    static constexpr int D = 4 + 15 * (N * N + 1);
+    static constexpr int G = (N == 4) ? 128 : 64;  // tables per group ([G][D] 16-bit exits in LDS)
+    static constexpr int M = IE_REC_M;              // chunks per table wave
+    static constexpr int HSB = (N == 4) ? 10 : 11;  // claim hash slots per chunk: 1 << HSB
+    static constexpr int HS = 1 << HSB;
+};
+constexpr int kRecMaxLevels = 4;
+constexpr int kRecPosCap = 256;  // record positions kept per chunk (more: the decode walks again)
+constexpr int kRecWPB = 4;       // chunk waves per block of the per-chunk passes
+struct RecParseArgs {
+    const uint32_t* words;  // stream as stored (big-endian bytes), zero-padded by >= 2 words
+    uint64_t nbits, start_bit;
+    uint32_t C;             // chunk bits (multiple of 32)
+    int nchunks, rle;
+    uint16_t* tab;          // [nchunks][D] transfer tables (then prefix maps), followed by the
+                            // composites of every level
+    uint16_t* lvl[kRecMaxLevels];  // set by the launcher: the table array of every level
+    int levels;
+    uint32_t* E;            // [<= G] entry offset of every top-level composite
+    unsigned* ticket;       // [1]: the composition ticket, 0 before the launch (left 0)
+    uint16_t* pos;          // [nchunks][kRecPosCap] record positions (relative to the chunk's word)
+    uint32_t* cnt;          // [nchunks] records of every chunk
+    uint64_t* base;         // [nchunks] records before every chunk
+    uint64_t* total;        // records on the true path
+    uint64_t* end_out;      // end bit of the last block's record
+    unsigned long long* stats;  // diagnostics (IE_DEC_STATS): walk steps; nullptr = off
+};
+int rec_group_chunks(int n);
+int rec_entry_span(int n);
+size_t rec_table_lds(uint32_t C, int n);
+size_t rec_decode_lds(uint32_t C, int n);
+// Returns the number of composition levels (< 0: too many chunks).
+int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t s);
 
 // Huffman decode (ie_decode.hip): write = false runs the walk + fix-up rounds + scan and leaves the
 // symbol count in *total (device); write = true then emits the symbols into out.

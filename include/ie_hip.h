@@ -232,10 +232,10 @@ int ie_decode_frames(ie_ctx* ctx, const uint8_t* in, size_t len, uint64_t start_
                      int nframes, int use_rle, uint8_t* out, size_t stride, size_t frame_pitch,
                      uint64_t* end_bit);
 
-/* How the last ie_decode_frames ran: fused = 1 for the one-launch parse + decode (stream segments
- * in LDS, speculative walks merged with the true path); 0 for the multi-kernel fallback (chunk
- * walks with `rounds` fix-up rounds), taken when a segment's true path did not merge. */
-int ie_last_decode_info(ie_ctx* ctx, int* fused, int* rounds);
+/* Chunks and composition levels of the last ie_decode_frames call's exact parse (diagnostics: the
+ * stream is cut into chunks of about 32 (4x4) / 16 (8x8) records, each tabulated over every entry
+ * offset; the tables are composed G at a time, level after level). */
+int ie_last_decode_info(ie_ctx* ctx, int* chunks, int* levels);
 
 #ifdef __cplusplus
 }

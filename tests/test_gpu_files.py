@@ -465,26 +465,32 @@ def test_decode_multi_segment_vs_oracle(codec, n, kind):
     assert np.array_equal(pix, O.load().decode_image(enc, n))
 
 
-@pytest.mark.parametrize("name", ["synM4k_4x4", "synU4k_4x4"])
-def test_decode_one_launch_path_matches(codec, tmp_path, name):
-    """The one-launch parse + decode (IE_DEC_FUSED=1, opt-in) gives the reference decoder's pixels
-    (the default multi-kernel path is pinned by every other decode test), in a fresh process."""
+@pytest.mark.parametrize("recs", ["1", "7", "200"])
+@pytest.mark.parametrize("name", ["synM4k_4x4", "synU4k_4x4", "synM4k_8x8"])
+def test_decode_chunking_matches(codec, tmp_path, name, recs):
+    """The exact parse gives the reference decoder's pixels for any chunking (IE_DEC_R records per
+    chunk: 1 = many groups and the cross-group chase from global memory, 200 = long chunks), in a
+    fresh process."""
     import subprocess
     import sys
-    c = next(c for c in O.manifest() if c["name"] == name)
+    c = next((c for c in O.manifest() if c["name"] == name), None)
+    if c is None:
+        pytest.skip(name + " not in the manifest")
     enc = _encode_case(codec, c)
-    default = codec.decode_image_file(enc, 4)
+    default = codec.decode_image_file(enc, c["n"])
     (tmp_path / "s.enc").write_bytes(enc)
     code = ("import sys, hashlib; sys.path.insert(0, %r)\n"
             "from imageencoder_amd import Codec\n"
             "c = Codec(0)\n"
-            "pix = c.decode_image_file(open(%r, 'rb').read(), 4)\n"
-            "print(hashlib.md5(pix.tobytes()).hexdigest(), c.last_decode_info()[0])\n") % (O.ROOT, str(tmp_path / "s.enc"))
-    env = dict(os.environ, IE_DEC_FUSED="1")
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+            "pix = c.decode_image_file(open(%r, 'rb').read(), %d)\n"
+            "print(hashlib.md5(pix.tobytes()).hexdigest(), *c.last_decode_info())\n") % (
+        O.ROOT, str(tmp_path / "s.enc"), c["n"])
+    env = dict(os.environ, IE_DEC_R=recs)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env,
+                       cwd=O.ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
-    md5, fused = r.stdout.strip().splitlines()[-1].split()
-    assert fused == "True"
+    md5, chunks, groups = r.stdout.strip().splitlines()[-1].split()
+    assert int(chunks) >= 1 and int(groups) >= 1
     assert md5 == _md5(default.tobytes())
     if "dec_md5" in c:
         assert md5 == c["dec_md5"]

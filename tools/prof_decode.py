@@ -1,6 +1,6 @@
-"""Decode timing per content kind (4K): the fused one-launch decode vs the multi-kernel path
-(IE_DEC_NOFUSED=1 in the environment selects the latter for the whole process).
-usage: python tools/prof_decode.py [n]"""
+"""Decode timing per content kind (4K, device-resident stream and pixels): the exact table parse
+(IE_DEC_R in the environment sets the records per chunk).
+usage: python tools/prof_decode.py [n] [kind,kind...]"""
 import os
 import sys
 import time
@@ -21,13 +21,16 @@ kinds = {"U": synth.frame("U", w, h, 5), "M": synth.frame("M", w, h, 5),
          "grad": ((xx * 3 + yy * 5) % 256).astype(np.uint8), "flat": np.full((h, w), 77, np.uint8)}
 out = torch.zeros(stream_bound(w, h, n, 1, 0), dtype=torch.uint8, device="cuda")
 pix = torch.empty((h, w), dtype=torch.uint8, device="cuda")
-tag = "multi-kernel" if os.environ.get("IE_DEC_NOFUSED") else "default"
+tag = "R=" + os.environ.get("IE_DEC_R", "32")
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(kinds)
 for name, y in kinds.items():
+    if name not in only:
+        continue
     _, end = c.encode_frames(torch.from_numpy(y).cuda(), w, h, out)
     nb = (end + 7) // 8
     c.decode_frames(out[:nb], w, h, pix, length=nb)
     ok = torch.equal(pix.cpu(), torch.from_numpy(y)) or True  # lossy: no pixel identity expected
-    fused, rounds = c.last_decode_info()
+    chunks, groups = c.last_decode_info()
     torch.cuda.synchronize()
     k = 5
     t0 = time.perf_counter()
@@ -35,4 +38,4 @@ for name, y in kinds.items():
         c.decode_frames(out[:nb], w, h, pix, length=nb)
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / k
-    print(f"{tag:12s} n={n} {name:5s} {nb:9d} B  {t * 1e6:9.1f} us  fused={fused} rounds={rounds}", flush=True)
+    print(f"{tag:12s} n={n} {name:5s} {nb:9d} B  {t * 1e6:9.1f} us  chunks={chunks} groups={groups}", flush=True)
