@@ -1,5 +1,6 @@
 """Streamed host path timing: ie_encode_images from host buffers (pageable numpy / pinned
-ie_host_alloc), 16 x 4K frames, for a few chunk sizes (IE_CHUNK_MB).  usage: python tools/e2e.py"""
+ie_host_alloc), 16 x 4K frames, for a few chunk sizes (IE_CHUNK_MB).  usage: python tools/e2e.py [MB ...]
+(E2E_N=8 in the environment: 8x8 blocks with matrix8_1.txt)"""
 import os
 import sys
 import time
@@ -11,10 +12,11 @@ from imageencoder_amd import Codec, stream_bound, synth, write_header  # noqa: E
 from tests import oracle_lib as O  # noqa: E402
 
 w, h, B = 3840, 2160, 16
-q = O.read_matrix("matrix.txt", 4)
-c = Codec(0, q, 4)
-hdr, hb = write_header(4, q, True, w, h)
-pitch = (stream_bound(w, h, 4, 1, hb) + 255) // 256 * 256
+n = int(os.environ.get("E2E_N", "4"))
+q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+c = Codec(0, q, n)
+hdr, hb = write_header(n, q, True, w, h)
+pitch = (stream_bound(w, h, n, 1, hb) + 255) // 256 * 256
 fr = synth.frames("U", w, h, B, seed=3).ravel()
 bufs = {"pageable": (fr, np.zeros(pitch * B, dtype=np.uint8))}
 yp, op = c.host_array(fr.size), c.host_array(pitch * B)
