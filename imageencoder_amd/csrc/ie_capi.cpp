@@ -1987,14 +1987,14 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     const uint64_t nblocks = uint64_t(nframes) * (w / n) * (h / n);
     // chunking: about R records per chunk (IE_DEC_R, default 32: measured on 4K streams against
     // 16, 64 and 128) so that every chunk's walks are short; C a multiple of 32, at least
-    // 256 bits, at most 2^13 (a table wave's LDS -- M chunks' bits, valid-header bitmap, 16-bit
-    // claims -- within 80 KB)
+    // 256 bits, at most 2^15 (16-bit record positions; a table wave's LDS -- the chunk's bits and
+    // valid-header bitmap -- stays small)
     const int G = ie::rec_group_chunks(n), D = ie::rec_entry_span(n);
     static const char* rs = getenv("IE_DEC_R");
     const uint64_t recs = rs ? std::max<uint64_t>(1, strtoull(rs, nullptr, 10)) : 32;
     const uint64_t want = std::max<uint64_t>((nblocks + recs - 1) / recs, 1);
     uint64_t C = (span + want - 1) / want;
-    C = std::min<uint64_t>(std::max<uint64_t>((C + 31) / 32 * 32, 256), uint64_t(1) << 13);
+    C = std::min<uint64_t>(std::max<uint64_t>((C + 31) / 32 * 32, 256), uint64_t(1) << 15);
     const uint64_t nch = std::max<uint64_t>((span + C - 1) / C, 1);
     // levels: ceil(n / G) composites per level until at most G remain (G^4 chunks at most)
     size_t tab_rows = 0;
@@ -2011,9 +2011,11 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
         return fail(c, IE_EINVAL, "stream too long for one decode call");
     const int nchunks = int(nch);
     if ((r = ensure(c, c->d_rtab, c->cap_rtab, tab_rows * D))) return r;
-    // d_walk: [nchunks] record bases, [G / 2] top-level entries, [nchunks / 2] chunk counts
-    const size_t e_at = size_t(nchunks), cnt_at = e_at + size_t(G) / 2 + 1;
-    if ((r = ensure(c, c->d_walk, c->cap_walk, cnt_at + size_t(nchunks) / 2 + 1))) return r;
+    // d_walk (8-byte words): [nchunks / 2] in-workgroup record bases, [G / 2] top-level entries,
+    // [nchunks / 2] chunk counts, [nchunks / 512] workgroup totals
+    const size_t e_at = size_t(nchunks) / 2 + 1, cnt_at = e_at + size_t(G) / 2 + 1;
+    const size_t wg_at = cnt_at + size_t(nchunks) / 2 + 1;
+    if ((r = ensure(c, c->d_walk, c->cap_walk, wg_at + size_t(nchunks) / 512 + 2))) return r;
     if ((r = ensure(c, c->d_rpos, c->cap_rpos, size_t(nchunks) * ie::kRecPosCap))) return r;
     const size_t pix_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
     const bool out_dev = is_device_ptr(out);
@@ -2039,7 +2041,8 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     pa.nchunks = nchunks;
     pa.rle = da.rle;
     pa.tab = c->d_rtab;
-    pa.base = c->d_walk;
+    pa.lbase = reinterpret_cast<uint32_t*>(c->d_walk);
+    pa.wgsum = reinterpret_cast<uint32_t*>(c->d_walk + wg_at);
     pa.E = reinterpret_cast<uint32_t*>(c->d_walk + e_at);
     pa.cnt = reinterpret_cast<uint32_t*>(c->d_walk + cnt_at);
     pa.pos = c->d_rpos;

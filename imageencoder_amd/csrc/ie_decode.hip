@@ -589,23 +589,32 @@ __device__ __forceinline__ uint32_t rec_chunk_entry(const RecParseArgs& a, int k
 // serial walks run 64 wide.
 template <int N>
 __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
+    __shared__ uint32_t scratch[8];
     const int k = int(blockIdx.x * kTPB + threadIdx.x);
-    if (k >= a.nchunks) return;
-    const uint64_t c0 = a.start_bit + uint64_t(k) * a.C;
-    const uint64_t base = c0 & ~31ull;
-    const uint64_t end = min<uint64_t>(c0 + a.C, a.nbits);  // no record starts at or past the stream's end
-    uint64_t p = c0 + rec_chunk_entry<N>(a, k);
-    uint16_t* pos = a.pos + size_t(k) * kRecPosCap;
     uint32_t R = 0;
-    while (p < end) {
-        const uint32_t l = rec_len_head<N>(getbits(a.words, p, 20), a.rle);
-        if (l > 1u) {
-            if (R < uint32_t(kRecPosCap)) pos[R] = uint16_t(p - base);
-            R++;
+    if (k < a.nchunks) {
+        const uint64_t c0 = a.start_bit + uint64_t(k) * a.C;
+        const uint64_t base = c0 & ~31ull;
+        const uint64_t end = min<uint64_t>(c0 + a.C, a.nbits);  // no record starts at or past the stream's end
+        uint64_t p = c0 + rec_chunk_entry<N>(a, k);
+        uint16_t* pos = a.pos + size_t(k) * kRecPosCap;
+        while (p < end) {
+            const uint32_t l = rec_len_head<N>(getbits(a.words, p, 20), a.rle);
+            if (l > 1u) {
+                if (R < uint32_t(kRecPosCap)) pos[R] = uint16_t(p - base);
+                R++;
+            }
+            p += l;
         }
-        p += l;
     }
-    a.cnt[k] = R;
+    // records before the chunk among its workgroup's kTPB chunks, and the workgroup's total
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(R, scratch, &tot);
+    if (k < a.nchunks) {
+        a.cnt[k] = R;
+        a.lbase[k] = ex;
+    }
+    if (threadIdx.x == 0) a.wgsum[blockIdx.x] = tot;
 }
 
 template <int N>
@@ -620,7 +629,11 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
     const uint64_t c0 = a.start_bit + uint64_t(k) * a.C;
     const uint64_t base = c0 & ~31ull;
     const uint32_t s0 = uint32_t(c0 - base), end = s0 + a.C;
-    const uint64_t first = a.base[k];  // first block index (scan of the counts)
+    // first block index: the totals of the count pass's workgroups before this chunk's, plus the
+    // records before it in its own (no separate scan launch)
+    uint64_t part = 0;
+    for (int g = lane; g < k / kTPB; g += 64) part += a.wgsum[g];
+    const uint64_t first = wave_sum64(part) + a.lbase[k];
     const uint32_t R = a.cnt[k];
     if (k == a.nchunks - 1 && lane == 0) *a.total = first + R;
     stage_words(L, a.words, base >> 5, int((end + D + 64) >> 5) + 2, (a.nbits + 31) >> 5, lane, 64);
@@ -701,7 +714,6 @@ int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t
     const int nbc = (a.nchunks + kTPB - 1) / kTPB;
     if (n == 4) hipLaunchKernelGGL((rec_count_kernel<4>), dim3(nbc), dim3(kTPB), 0, s, a);
     else hipLaunchKernelGGL((rec_count_kernel<8>), dim3(nbc), dim3(kTPB), 0, s, a);
-    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(kTPB), 0, s, a.cnt, a.base, a.nchunks);
     if (n == 4) hipLaunchKernelGGL((rec_decode_kernel<4>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 4), s, a, d);
     else hipLaunchKernelGGL((rec_decode_kernel<8>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 8), s, a, d);
     return levels;

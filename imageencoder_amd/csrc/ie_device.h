@@ -181,7 +181,8 @@ struct RecParseArgs {
     unsigned* ticket;       // [1]: the composition ticket, 0 before the launch (left 0)
     uint16_t* pos;          // [nchunks][kRecPosCap] record positions (relative to the chunk's word)
     uint32_t* cnt;          // [nchunks] records of every chunk
-    uint64_t* base;         // [nchunks] records before every chunk
+    uint32_t* lbase;        // [nchunks] records before every chunk within its count-pass workgroup
+    uint32_t* wgsum;        // [count-pass workgroups] their record totals
     uint64_t* total;        // records on the true path
     uint64_t* end_out;      // end bit of the last block's record
     unsigned long long* stats;  // diagnostics (IE_DEC_STATS): walk steps; nullptr = off
