@@ -1913,16 +1913,20 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
     const uint64_t chunk_bits = std::max<uint64_t>(256, huf_chunk);
     const size_t nchunks = size_t((nbits - start_bit + chunk_bits - 1) / chunk_bits);
     if (!nchunks) return IE_OK;
-    if ((r = ensure(c, c->d_walk, c->cap_walk, 4 * nchunks))) return r;
+    // d_walk: [cap] entries, [cap] symbol bases, then 128 words of top-level entries (256 x u32)
+    if ((r = ensure(c, c->d_walk, c->cap_walk, 2 * nchunks + 130))) return r;
     if ((r = ensure(c, c->d_count, c->cap_count, nchunks))) return r;
+    if ((r = ensure(c, c->d_rtab, c->cap_rtab, ie::huffman_table_rows(nbits, start_bit, chunk_bits) + 2))) return r;
     uint64_t* wk = c->d_walk;
-    const size_t cap = c->cap_walk / 4;
+    const size_t cap = (c->cap_walk - 130) / 2;
     unsigned* flags = reinterpret_cast<unsigned*>(c->d_misc + 1);
-    HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 4 * sizeof(uint64_t), c->stream));
+    uint32_t* E = reinterpret_cast<uint32_t*>(wk + 2 * cap);
+    unsigned* ticket = reinterpret_cast<unsigned*>(c->d_misc + 5);
+    HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 6 * sizeof(uint64_t), c->stream));
     const uint32_t* W = reinterpret_cast<const uint32_t*>(c->d_dec);
-    const int rounds = ie::huffman_decode_device(W, nbits, start_bit, c->d_hlut, chunk_bits, wk, wk + cap,
-                                                 wk + 2 * cap, c->d_count, wk + 3 * cap, flags, c->d_misc + 2,
-                                                 nullptr, false, c->stream, int(nchunks) + 2);
+    const int rounds = ie::huffman_decode_device(W, nbits, start_bit, c->d_hlut, chunk_bits, wk, c->d_rtab, E, ticket,
+                                                 c->d_count, wk + cap, flags, c->d_misc + 2, nullptr, false,
+                                                 c->stream);
     if (rounds < 0) return fail(c, IE_EHIP, "Huffman decode walk failed");
     HIPCHK(c, hipGetLastError());
     uint64_t total = 0;
@@ -1936,8 +1940,8 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
         if ((r = ensure(c, c->d_hout, c->cap_hout, size_t(total) + 1))) return r;
         dout = c->d_hout;
     }
-    ie::huffman_decode_device(W, nbits, start_bit, c->d_hlut, chunk_bits, wk, wk + cap, wk + 2 * cap, c->d_count,
-                              wk + 3 * cap, flags, c->d_misc + 2, dout, true, c->stream, 0);
+    ie::huffman_decode_device(W, nbits, start_bit, c->d_hlut, chunk_bits, wk, c->d_rtab, E, ticket, c->d_count,
+                              wk + cap, flags, c->d_misc + 2, dout, true, c->stream);
     HIPCHK(c, hipGetLastError());
     unsigned f[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(f, flags, sizeof(f), hipMemcpyDeviceToHost, c->stream));

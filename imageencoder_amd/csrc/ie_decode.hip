@@ -70,16 +70,17 @@ __global__ __launch_bounds__(kTPB) void scan_counts_kernel(const uint32_t* count
 }
 
 // ---- Huffman decode (Huffman.cpp:354-402; the per-bit tree walk of :190-204) -------------------
-// Same chunked speculation as the record walk: one lane per chunk of bits decodes symbols with a
-// prefix table until it leaves the chunk; fix-up rounds re-walk chunks whose entry differs from the
-// predecessor's exit (prefix codes resynchronise within a few symbols); a scan of the per-chunk
-// symbol counts places every chunk's output; a last walk writes the symbols.  The reference walks
-// to the end of the buffer, padding bits of the last byte included (a code may run past it with
-// zero bits), and so does this walk.
+// One lane per chunk of bits decodes symbols with a prefix table until it leaves the chunk; its
+// entry comes from composed transfer tables (the exact parse at the end of this file); a scan of
+// the per-chunk symbol counts places every chunk's output; a last walk writes the symbols.  The
+// reference walks to the end of the buffer, padding bits of the last byte included (a code may run
+// past it with zero bits), and so does this walk.
 //   lut   [2^15]: sym | len << 8 for every 15-bit prefix, len 0 = no code (codes are <= 15 bits:
 //         the dictionary stores lengths in 4 bits, Huffman.cpp:41-42)
 //   LDS   the 2^kHufL1 first-level entries (codes of <= kHufL1 bits resolve there)
 constexpr int kHufL1 = 11;
+constexpr int kHufD = 15;   // entry offsets of a chunk: codes are at most 15 bits
+constexpr int kHufG = 256;  // tables per composition group
 struct HufArgs {
     const uint32_t* words;
     uint64_t nbits, start_bit, chunk_bits;
@@ -90,9 +91,12 @@ struct HufArgs {
     uint64_t* exit_out;
     uint32_t* count;
     unsigned* changed;  // [0] a round changed an entry, [1] invalid code on the exact walk
-    int first;
+    int first;              // 1: speculative entry (chunk start); 2: entry from the composed tables
     const uint64_t* base;
     uint8_t* out;
+    uint16_t* lvl[kRecMaxLevels];  // mode 2: the composition's levels
+    int levels;
+    const uint32_t* E;
 };
 
 __device__ __forceinline__ void huf_l1(const uint16_t* lut, uint16_t* l1) {
@@ -135,7 +139,18 @@ __global__ __launch_bounds__(kTPB) void huf_walk_kernel(HufArgs a) {
     if (k >= a.nchunks) return;
     const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
     uint64_t e;
-    if (a.first) {
+    if (a.first == 2) {
+        // the chunk's true entry: its top-level entry through every level's prefix map
+        int u = k;
+        for (int l = 0; l < a.levels; l++) u /= kHufG;
+        uint32_t x = a.E[u];
+        for (int l = a.levels - 1; l >= 0; l--) {
+            int ul = k;
+            for (int m = 0; m < l; m++) ul /= kHufG;
+            x = a.lvl[l][size_t(ul) * kHufD + x];
+        }
+        e = cstart + x;
+    } else if (a.first) {
         e = cstart;
     } else {
         if (k == 0) {
@@ -151,7 +166,8 @@ __global__ __launch_bounds__(kTPB) void huf_walk_kernel(HufArgs a) {
     }
     a.entry[k] = e;
     uint32_t c;
-    a.exit_out[k] = huf_walk(a, l1, e, cstart + a.chunk_bits, &c, nullptr, false);
+    const uint64_t x = huf_walk(a, l1, e, cstart + a.chunk_bits, &c, nullptr, false);
+    if (a.exit_out) a.exit_out[k] = x;
     a.count[k] = c;
 }
 
@@ -165,69 +181,9 @@ __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
     huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, a.out + a.base[k], true);
 }
 
-// Returns the number of fix-up rounds (>= 0), -1 on a HIP error, -2 if the rounds did not settle.
 // total receives the symbol count (device, 1 word) = base[last] + count[last].
 __global__ void huf_total_kernel(const uint64_t* base, const uint32_t* count, int n, uint64_t* total) {
     if (threadIdx.x == 0 && blockIdx.x == 0) *total = base[n - 1] + count[n - 1];
-}
-
-int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
-                          uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,
-                          uint64_t* base, unsigned* changed, uint64_t* total, uint8_t* out, bool write,
-                          hipStream_t s, int max_rounds) {
-    const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
-    const int nchunks = int((span + chunk_bits - 1) / chunk_bits);
-    if (nchunks == 0) return 0;
-    HufArgs a{};
-    a.words = W;
-    a.nbits = nbits;
-    a.start_bit = start_bit;
-    a.chunk_bits = chunk_bits;
-    a.nchunks = nchunks;
-    a.lut = lut;
-    a.entry = entry;
-    a.count = count;
-    a.changed = changed;
-    a.base = base;
-    a.out = out;
-    const dim3 g((nchunks + kTPB - 1) / kTPB), blk(kTPB);
-    if (!write) {
-        a.first = 1;
-        a.exit_in = exA;
-        a.exit_out = exA;
-        hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
-        uint64_t* cur = exA;
-        uint64_t* nxt = exB;
-        // fix-up rounds in growing groups (1, 2, 4, 8, 8, ...) between host checks of the
-        // "changed" flag (a round after convergence is a near-empty launch; a host round trip per
-        // round costs more)
-        int rounds = 0, group = 1;
-        bool done = false;
-        while (!done && rounds < max_rounds + 8) {
-            unsigned h = 0;
-            if (hipMemsetAsync(changed, 0, sizeof(unsigned), s) != hipSuccess) return -1;
-            for (int r = 0; r < group; r++) {
-                a.first = 0;
-                a.exit_in = cur;
-                a.exit_out = nxt;
-                hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
-                uint64_t* t = cur;
-                cur = nxt;
-                nxt = t;
-            }
-            rounds += group;
-            group = group < 8 ? 2 * group : 8;
-            if (hipMemcpyAsync(&h, changed, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
-            if (hipStreamSynchronize(s) != hipSuccess) return -1;
-            done = (h == 0);
-        }
-        if (!done) return -2;
-        hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
-        hipLaunchKernelGGL(huf_total_kernel, dim3(1), dim3(1), 0, s, base, count, nchunks, total);
-        return rounds;
-    }
-    hipLaunchKernelGGL(huf_emit_kernel, g, blk, 0, s, a);
-    return 0;
 }
 
 // ---- exact record parse: transfer tables, composed -------------------------------------------
@@ -528,11 +484,11 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
 
 // One composition level over n tables ([n][D], 16-bit exits): prefix maps written over the
 // tables, composites into comp ([ceil(n/G)][D]); with `top`, the last workgroup chases the
-// stream's start (entry 0) through the composites: E[q] = entry of composite q.
-template <int N>
-__global__ __launch_bounds__(kTPB) void rec_compose_kernel(uint16_t* tab, int n, uint16_t* comp, int top,
-                                                           uint32_t* E, unsigned* ticket) {
-    constexpr int D = RecGeom<N>::D, G = RecGeom<N>::G;
+// stream's start (entry 0) through the composites: E[q] = entry of composite q.  Shared by the
+// record parse (D = the longest record) and the Huffman decode (D = the longest code).
+template <int D, int G>
+__global__ __launch_bounds__(kTPB) void compose_kernel(uint16_t* tab, int n, uint16_t* comp, int top, uint32_t* E,
+                                                       unsigned* ticket) {
     __shared__ uint16_t S[G * D];
     __shared__ unsigned last;
     const int tid = threadIdx.x, g = blockIdx.x, ng = gridDim.x;
@@ -568,19 +524,55 @@ __global__ __launch_bounds__(kTPB) void rec_compose_kernel(uint16_t* tab, int n,
     }
 }
 
-// the chunk's entry offset: its top-level entry, then the prefix maps of every level down to its table
-template <int N>
-__device__ __forceinline__ uint32_t rec_chunk_entry(const RecParseArgs& a, int k) {
-    constexpr int D = RecGeom<N>::D, G = RecGeom<N>::G;
+// The composition levels over n tables: level l+1's tables are level l's composites, until at
+// most G remain (the top chase).  lvl[l] receives level l's table array; returns the number of
+// levels, or -1 past kRecMaxLevels.
+template <int D, int G>
+int launch_compose(uint16_t* tab, int n, uint32_t* E, unsigned* ticket, uint16_t** lvl, hipStream_t s) {
+    int cur = n, levels = 0;
+    uint16_t* arr = tab;
+    for (;;) {
+        const int ng = (cur + G - 1) / G;
+        const int top = ng <= G ? 1 : 0;
+        if (levels >= kRecMaxLevels) return -1;
+        lvl[levels] = arr;
+        uint16_t* comp = arr + size_t(cur) * D;
+        hipLaunchKernelGGL((compose_kernel<D, G>), dim3(ng), dim3(kTPB), 0, s, arr, cur, comp, top, E, ticket);
+        levels++;
+        if (top) return levels;
+        arr = comp;
+        cur = ng;
+    }
+}
+
+// Table rows a composition over n tables needs (the tables and every level's composites).
+template <int D, int G>
+size_t compose_rows(int n) {
+    size_t rows = 0;
+    for (int cur = n;; cur = (cur + G - 1) / G) {
+        rows += size_t(cur);
+        if ((cur + G - 1) / G <= G) return rows + size_t((cur + G - 1) / G);
+    }
+}
+
+// the entry offset of table k: its top-level entry, then the prefix maps of every level down
+template <int D, int G>
+__device__ __forceinline__ uint32_t table_entry(const uint32_t* E, uint16_t* const* lvl, int levels, int k) {
     int u = k;
-    for (int l = 0; l < a.levels; l++) u /= G;
-    uint32_t x = a.E[u];
-    for (int l = a.levels - 1; l >= 0; l--) {
+    for (int l = 0; l < levels; l++) u /= G;
+    uint32_t x = E[u];
+    for (int l = levels - 1; l >= 0; l--) {
         int ul = k;
         for (int m = 0; m < l; m++) ul /= G;
-        x = a.lvl[l][size_t(ul) * D + x];
+        x = lvl[l][size_t(ul) * D + x];
     }
     return x;
+}
+
+// the chunk's entry offset (record parse)
+template <int N>
+__device__ __forceinline__ uint32_t rec_chunk_entry(const RecParseArgs& a, int k) {
+    return table_entry<RecGeom<N>::D, RecGeom<N>::G>(a.E, a.lvl, a.levels, k);
 }
 
 // Count pass: one LANE per chunk walks its true records from global memory (a record header is
@@ -684,32 +676,13 @@ size_t rec_decode_lds(uint32_t C, int n) { return size_t(rec_decode_stream_words
 
 int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t s) {
     if (a.nchunks <= 0) return 0;
-    const int G = rec_group_chunks(n), D = rec_entry_span(n);
     const int nb = (a.nchunks + kRecWPB - 1) / kRecWPB;  // blocks of kRecWPB chunk waves
-    // composition levels: tables of level l+1 are the composites of level l
-    int cur = a.nchunks, levels = 0;
-    uint16_t* arr = a.tab;
-    for (;;) {
-        const int ng = (cur + G - 1) / G;
-        const int top = ng <= G ? 1 : 0;
-        if (levels >= kRecMaxLevels) return -1;
-        a.lvl[levels] = arr;
-        uint16_t* comp = arr + size_t(cur) * D;
-        if (levels == 0) {
-            const int M = n == 4 ? RecGeom<4>::M : RecGeom<8>::M;
-            const int nt = (a.nchunks + M - 1) / M;
-            if (n == 4) hipLaunchKernelGGL((rec_table_kernel<4>), dim3(nt), dim3(64), rec_table_lds(a.C, 4), s, a);
-            else hipLaunchKernelGGL((rec_table_kernel<8>), dim3(nt), dim3(64), rec_table_lds(a.C, 8), s, a);
-        }
-        if (n == 4)
-            hipLaunchKernelGGL((rec_compose_kernel<4>), dim3(ng), dim3(kTPB), 0, s, arr, cur, comp, top, a.E, a.ticket + 1);
-        else
-            hipLaunchKernelGGL((rec_compose_kernel<8>), dim3(ng), dim3(kTPB), 0, s, arr, cur, comp, top, a.E, a.ticket + 1);
-        levels++;
-        if (top) break;
-        arr = comp;
-        cur = ng;
-    }
+    const int nt = (a.nchunks + RecGeom<4>::M - 1) / RecGeom<4>::M;  // table waves (M chunks each)
+    if (n == 4) hipLaunchKernelGGL((rec_table_kernel<4>), dim3(nt), dim3(64), rec_table_lds(a.C, 4), s, a);
+    else hipLaunchKernelGGL((rec_table_kernel<8>), dim3(nt), dim3(64), rec_table_lds(a.C, 8), s, a);
+    const int levels = (n == 4) ? launch_compose<RecGeom<4>::D, RecGeom<4>::G>(a.tab, a.nchunks, a.E, a.ticket + 1, a.lvl, s)
+                                : launch_compose<RecGeom<8>::D, RecGeom<8>::G>(a.tab, a.nchunks, a.E, a.ticket + 1, a.lvl, s);
+    if (levels < 0) return -1;
     a.levels = levels;
     const int nbc = (a.nchunks + kTPB - 1) / kTPB;
     if (n == 4) hipLaunchKernelGGL((rec_count_kernel<4>), dim3(nbc), dim3(kTPB), 0, s, a);
@@ -717,6 +690,89 @@ int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t
     if (n == 4) hipLaunchKernelGGL((rec_decode_kernel<4>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 4), s, a, d);
     else hipLaunchKernelGGL((rec_decode_kernel<8>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 8), s, a, d);
     return levels;
+}
+
+// ---- exact Huffman parse: the same transfer tables --------------------------------------------
+// A code is at most 15 bits long, so the first code that starts at or after a chunk's first bit
+// sits at an offset d < 15: a chunk of the Huffman stream is a function of d exactly like a chunk
+// of the record stream, with 15 entries instead of D.  huf_table_kernel walks all 15 entries of
+// 16 chunks per workgroup (one lane each, the chunks' bits staged in LDS; a position where no code
+// starts slides one bit -- never on the true path of a valid stream); compose_kernel composes the
+// tables; huf_walk_kernel (mode 2) then walks each chunk once from its true entry for the symbol
+// count, and huf_emit_kernel writes the symbols.  Exact for any content: a periodic stream (e.g. a
+// flat image's records, Huffman-coded) no longer leaves speculative walks locked in a wrong phase.
+__global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* tab) {
+    __shared__ uint16_t l1[1 << kHufL1];
+    extern __shared__ uint32_t L[];  // the block's 16 chunks' bits (+ 64 for the last code)
+    huf_l1(a.lut, l1);               // (ends with a barrier)
+    const int tid = threadIdx.x, kc = tid >> 4, d = tid & 15;
+    const int k0 = blockIdx.x * 16, k = k0 + kc;
+    const uint32_t C = uint32_t(a.chunk_bits);
+    const int m = min(16, a.nchunks - k0);
+    const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
+    const uint64_t base = c0 & ~31ull;
+    const uint32_t s0 = uint32_t(c0 - base);
+    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, (a.nbits + 31) >> 5, tid, kTPB);
+    __syncthreads();
+    if (d >= kHufD || kc >= m) return;
+    const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(s0) + uint64_t(m) * C));
+    const uint32_t ce = s0 + uint32_t(kc + 1) * C;
+    uint32_t p = s0 + uint32_t(kc) * C + uint32_t(d);
+    while (p < ce) {
+        if (p >= lim) {  // past the stream: the walk ends (the last chunk's exit is never used)
+            p = ce;
+            break;
+        }
+        const uint32_t p15 = lbits(L, p, 15);
+        uint32_t e = l1[p15 >> (15 - kHufL1)];
+        if (!e) e = a.lut[p15];
+        const uint32_t len = e >> 8;
+        p += len ? len : 1u;
+    }
+    tab[size_t(k) * kHufD + d] = uint16_t(p - ce);
+}
+
+int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
+                          uint64_t chunk_bits, uint64_t* entry, uint16_t* tab, uint32_t* E, unsigned* ticket,
+                          uint32_t* count, uint64_t* base, unsigned* changed, uint64_t* total, uint8_t* out,
+                          bool write, hipStream_t s) {
+    const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
+    const int nchunks = int((span + chunk_bits - 1) / chunk_bits);
+    if (nchunks == 0) return 0;
+    HufArgs a{};
+    a.words = W;
+    a.nbits = nbits;
+    a.start_bit = start_bit;
+    a.chunk_bits = chunk_bits;
+    a.nchunks = nchunks;
+    a.lut = lut;
+    a.entry = entry;
+    a.count = count;
+    a.changed = changed;
+    a.base = base;
+    a.out = out;
+    const dim3 g((nchunks + kTPB - 1) / kTPB), blk(kTPB);
+    if (write) {
+        hipLaunchKernelGGL(huf_emit_kernel, g, blk, 0, s, a);
+        return 0;
+    }
+    const size_t lds = size_t(((16 * chunk_bits + 95) >> 5) + 3) * 4;
+    hipLaunchKernelGGL(huf_table_kernel, dim3((nchunks + 15) / 16), blk, lds, s, a, tab);
+    const int levels = launch_compose<kHufD, kHufG>(tab, nchunks, E, ticket, a.lvl, s);
+    if (levels < 0) return -1;
+    a.levels = levels;
+    a.E = E;
+    a.first = 2;  // entries from the composed tables
+    hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
+    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
+    hipLaunchKernelGGL(huf_total_kernel, dim3(1), dim3(1), 0, s, base, count, nchunks, total);
+    return levels;
+}
+
+size_t huffman_table_rows(uint64_t nbits, uint64_t start_bit, uint64_t chunk_bits) {
+    const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
+    const int nchunks = int((span + chunk_bits - 1) / chunk_bits);
+    return nchunks ? compose_rows<kHufD, kHufG>(nchunks) * kHufD : 0;
 }
 
 }  // namespace ie

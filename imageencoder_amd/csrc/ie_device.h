@@ -194,11 +194,15 @@ size_t rec_decode_lds(uint32_t C, int n);
 // Returns the number of composition levels (< 0: too many chunks).
 int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t s);
 
-// Huffman decode (ie_decode.hip): write = false runs the walk + fix-up rounds + scan and leaves the
-// symbol count in *total (device); write = true then emits the symbols into out.
+// Huffman decode (ie_decode.hip): write = false runs the exact parse (per-chunk transfer tables
+// over the 15 entry offsets, composed) + the counting walk + scan and leaves the symbol count in
+// *total (device); write = true then emits the symbols into out.  tab: huffman_table_rows()
+// 16-bit words; E: at least 256 words; ticket: 0 (left 0).  Returns the composition levels (< 0
+// on error).
 int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
-                          uint64_t chunk_bits, uint64_t* entry, uint64_t* exA, uint64_t* exB, uint32_t* count,
-                          uint64_t* base, unsigned* changed, uint64_t* total, uint8_t* out, bool write,
-                          hipStream_t s, int max_rounds);
+                          uint64_t chunk_bits, uint64_t* entry, uint16_t* tab, uint32_t* E, unsigned* ticket,
+                          uint32_t* count, uint64_t* base, unsigned* changed, uint64_t* total, uint8_t* out,
+                          bool write, hipStream_t s);
+size_t huffman_table_rows(uint64_t nbits, uint64_t start_bit, uint64_t chunk_bits);
 
 }  // namespace ie
