@@ -231,8 +231,10 @@ static bool parse_header(const uint8_t* src, size_t len, size_t start, int n, bo
 
 // Decode a file image into frames of pixels.  out_frame_pitch bytes per decoded frame.
 // Video frames come out as Y followed by w*h/2 bytes of UV fill.
+// cap: the caller's pixel capacity -- a smaller one returns IE_ECAP right after the header (sh
+// filled in), before the payload is decoded
 static int decode_file(ie_ctx* c, const uint8_t* enc, size_t len, int n, bool video, StreamHeader& sh,
-                       std::vector<uint8_t>& pix, std::string& err) {
+                       std::vector<uint8_t>& pix, std::string& err, size_t cap = SIZE_MAX) {
     if (!c) return (err = "no GPU context", IE_EHIP);
     std::vector<uint8_t> dec;
     bool pass = false;
@@ -248,6 +250,7 @@ static int decode_file(ie_ctx* c, const uint8_t* enc, size_t len, int n, bool vi
     if ((r = ie_set_quant(c, sh.q.data(), n))) return (err = ie_last_error(c), r);
     const size_t fbytes = size_t(sh.w) * sh.h;
     const size_t pitch = video ? fbytes + fbytes / 2 : fbytes;
+    if (pitch * size_t(sh.frames) > cap) return IE_ECAP;
     pix.assign(pitch * size_t(sh.frames), video ? 0x80 : 0);  // UV fill (Frame.cpp:121-124)
     if (!fbytes || !sh.frames) return IE_OK;
     if ((r = ie_decode_frames(c, src, srclen, sh.payload_bit, sh.w, sh.h, sh.frames, sh.rle, pix.data(), size_t(sh.w),
@@ -463,11 +466,10 @@ int64_t ieh_decode_image(ie_ctx* c, const uint8_t* enc, size_t len, int n, uint8
     dc::StreamHeader sh;
     std::vector<uint8_t> pix;
     std::string err;
-    const int r = dc::decode_file(c, enc, len, n, false, sh, pix, err);
+    const int r = dc::decode_file(c, enc, len, n, false, sh, pix, err, cap);
     if (w) *w = sh.w;
     if (h) *h = sh.h;
     if (r) return r;
-    if (pix.size() > cap) return IE_ECAP;
     std::memcpy(out, pix.data(), pix.size());
     return int64_t(pix.size());
 }
@@ -478,12 +480,11 @@ int64_t ieh_decode_video(ie_ctx* c, const uint8_t* enc, size_t len, int n, uint8
     dc::StreamHeader sh;
     std::vector<uint8_t> pix;
     std::string err;
-    const int r = dc::decode_file(c, enc, len, n, true, sh, pix, err);
+    const int r = dc::decode_file(c, enc, len, n, true, sh, pix, err, cap);
     if (w) *w = sh.w;
     if (h) *h = sh.h;
     if (frames) *frames = sh.frames;
     if (r) return r;
-    if (pix.size() > cap) return IE_ECAP;
     std::memcpy(out, pix.data(), pix.size());
     return int64_t(pix.size());
 }

@@ -87,11 +87,8 @@ struct HufArgs {
     int nchunks;
     const uint16_t* lut;
     uint64_t* entry;
-    const uint64_t* exit_in;
-    uint64_t* exit_out;
     uint32_t* count;
-    unsigned* changed;  // [0] a round changed an entry, [1] invalid code on the exact walk
-    int first;              // 1: speculative entry (chunk start); 2: entry from the composed tables
+    unsigned* changed;  // [1] invalid code on the emitting walk
     const uint64_t* base;
     uint8_t* out;
     uint16_t* lvl[kRecMaxLevels];  // mode 2: the composition's levels
@@ -132,42 +129,26 @@ __device__ __forceinline__ uint64_t huf_walk(const HufArgs& a, const uint16_t* l
     return pos;
 }
 
+// The counting walk: each chunk from its true entry (its top-level entry through every level's
+// prefix map of the composed transfer tables), symbols counted; the entry is kept for the emit.
 __global__ __launch_bounds__(kTPB) void huf_walk_kernel(HufArgs a) {
     __shared__ uint16_t l1[1 << kHufL1];
     huf_l1(a.lut, l1);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.nchunks) return;
     const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
-    uint64_t e;
-    if (a.first == 2) {
-        // the chunk's true entry: its top-level entry through every level's prefix map
-        int u = k;
-        for (int l = 0; l < a.levels; l++) u /= kHufG;
-        uint32_t x = a.E[u];
-        for (int l = a.levels - 1; l >= 0; l--) {
-            int ul = k;
-            for (int m = 0; m < l; m++) ul /= kHufG;
-            x = a.lvl[l][size_t(ul) * kHufD + x];
-        }
-        e = cstart + x;
-    } else if (a.first) {
-        e = cstart;
-    } else {
-        if (k == 0) {
-            a.exit_out[0] = a.exit_in[0];
-            return;
-        }
-        e = a.exit_in[k - 1];
-        if (e == a.entry[k]) {
-            a.exit_out[k] = a.exit_in[k];
-            return;
-        }
-        atomicOr(a.changed, 1u);
+    int u = k;
+    for (int l = 0; l < a.levels; l++) u /= kHufG;
+    uint32_t x = a.E[u];
+    for (int l = a.levels - 1; l >= 0; l--) {
+        int ul = k;
+        for (int m = 0; m < l; m++) ul /= kHufG;
+        x = a.lvl[l][size_t(ul) * kHufD + x];
     }
+    const uint64_t e = cstart + x;
     a.entry[k] = e;
     uint32_t c;
-    const uint64_t x = huf_walk(a, l1, e, cstart + a.chunk_bits, &c, nullptr, false);
-    if (a.exit_out) a.exit_out[k] = x;
+    huf_walk(a, l1, e, cstart + a.chunk_bits, &c, nullptr, false);
     a.count[k] = c;
 }
 
@@ -762,7 +743,6 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
     if (levels < 0) return -1;
     a.levels = levels;
     a.E = E;
-    a.first = 2;  // entries from the composed tables
     hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
     hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
     hipLaunchKernelGGL(huf_total_kernel, dim3(1), dim3(1), 0, s, base, count, nchunks, total);

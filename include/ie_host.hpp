@@ -331,10 +331,13 @@ int64_t ieh_encode_image(ie_ctx* ctx, const uint8_t* y, int w, int h, const uint
 // gop=1 video file from a YUV420 buffer (frame_count = len / (1.5 w h)).
 int64_t ieh_encode_video(ie_ctx* ctx, const uint8_t* yuv, size_t len, int w, int h, const uint16_t* q, int n,
                          int rle, int huffman, int merange, int mode, uint8_t* out, size_t cap);
-// Decode an image file (host buffer) with block size n: pixels into out (w*h bytes).
+// Decode an image file (host buffer) with block size n: pixels into out (w*h bytes).  A cap
+// below w*h returns IE_ECAP with *w / *h set, right after the header (the payload is not decoded):
+// call with cap = 0 to size the buffer.
 int64_t ieh_decode_image(ie_ctx* ctx, const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap, int* w,
                          int* h);
-// Decode a gop=1 video file: frames of Y + w*h/2 bytes of 0x80 (Frame.cpp:121-124).
+// Decode a gop=1 video file: frames of Y + w*h/2 bytes of 0x80 (Frame.cpp:121-124).  A cap
+// below the frames' size returns IE_ECAP after the header, as ieh_decode_image.
 int64_t ieh_decode_video(ie_ctx* ctx, const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap, int* w,
                          int* h, int* frames);
 // Huffman post-pass entirely between device buffers (in, out device memory; out needs

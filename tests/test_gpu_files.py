@@ -445,12 +445,14 @@ def test_counted_encode_histogram(codec, w, h, f, start_bit, kind):
 
 
 # ------------------------------------------------- multi-segment decode; one-launch path (opt-in)
+@pytest.mark.parametrize("huffman", [False, True])
 @pytest.mark.parametrize("n", [4, 8])
 @pytest.mark.parametrize("kind", ["flat", "U", "M", "grad"])
-def test_decode_multi_segment_vs_oracle(codec, n, kind):
+def test_decode_multi_segment_vs_oracle(codec, n, kind, huffman):
     """Streams spanning many parse segments (4x4: 65536 bits, 8x8: 131072 bits each), with
     records from 5 bits (flat blocks) to the longest, and periodic record streams (flat image,
-    regular gradient): the decode == the oracle's."""
+    regular gradient), with and without the Huffman pass (a periodic record stream makes a periodic
+    code stream too): the decode == the oracle's."""
     w, h = 648, 488
     if kind == "flat":
         y = np.full((h, w), 77, dtype=np.uint8)
@@ -460,7 +462,7 @@ def test_decode_multi_segment_vs_oracle(codec, n, kind):
     else:
         y = synth.frame(kind, w, h, seed=99 + n)
     q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
-    enc = codec.encode_image_file(y, w, h, q, n, rle=True, huffman=False)
+    enc = codec.encode_image_file(y, w, h, q, n, rle=True, huffman=huffman)
     pix = codec.decode_image_file(enc, n)
     assert np.array_equal(pix, O.load().decode_image(enc, n))
 
