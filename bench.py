@@ -410,7 +410,7 @@ def main():
             chunks, groups = codec.last_decode_info()
             extra["decode_one_image"] = {"us": round(td * 1e6, 1), "Mpx_s": round(w * h / td / 1e6, 1),
                                          "path": f"exact parse: {chunks} chunk transfer tables composed in "
-                                                 f"{groups} level(s), then count / scan / decode launches; "
+                                                 f"{groups} level(s), then count and decode launches; "
                                                  "one host sync at the end (device-resident stream and pixels)"}
         workload = (f"{wl}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
                     f"{' +Huffman' if cfg['huffman'] else ''}, batch of {B} independent images per step, "
