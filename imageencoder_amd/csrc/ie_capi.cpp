@@ -2054,11 +2054,13 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     pa.total = c->d_misc + 2;
     pa.end_out = c->d_misc;
     HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 3 * sizeof(uint64_t), c->stream));
+#if IE_PROFILE  // walk statistics of the table pass (profiling builds only)
     static const bool dstats = getenv("IE_DEC_STATS") != nullptr;
     if (dstats) {
         pa.stats = reinterpret_cast<unsigned long long*>(c->d_misc + 3);  // [3..7]
         HIPCHK(c, hipMemsetAsync(c->d_misc + 3, 0, 5 * sizeof(uint64_t), c->stream));
     }
+#endif
     if (ie::launch_rec_parse_decode(pa, da, n, c->stream) < 0) return fail(c, IE_EINVAL, "stream too long for one decode call");
     HIPCHK(c, hipGetLastError());
     c->last_chunks = nchunks;
@@ -2067,6 +2069,7 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     HIPCHK(c, hipMemcpyAsync(hm, c->d_misc, sizeof(hm), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const uint64_t end = hm[0];
+#if IE_PROFILE
     if (dstats) {
         uint64_t st[5];
         HIPCHK(c, hipMemcpy(st, c->d_misc + 3, sizeof(st), hipMemcpyDeviceToHost));
@@ -2075,6 +2078,7 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
                 double(st[2]) / nchunks, double(st[3]) / nchunks, (unsigned long long)st[4]);
         HIPCHK(c, hipMemsetAsync(c->d_misc + 3, 0, sizeof(uint64_t), c->stream));
     }
+#endif
     if (hm[2] < nblocks || end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
     return finish_decode(c, out, dpix, out_dev, nframes, w, h, stride, frame_pitch, end, end_bit);
 }

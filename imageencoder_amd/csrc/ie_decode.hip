@@ -413,6 +413,10 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
                 fresh = true;
             }
         }
+        (void)nsteps;
+        (void)nwin;
+        (void)nbey;
+#if IE_PROFILE  // walk statistics (IE_DEC_STATS in a profiling build)
         if (a.stats) {
             const uint32_t mx = __reduce_max_sync(~0ull, nsteps);
             atomicAdd(&a.stats[0], uint64_t(nsteps));
@@ -420,6 +424,7 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
             atomicAdd(&a.stats[2], uint64_t(nwin));
             if (lane == 0) { atomicAdd(&a.stats[3], uint64_t(mx)); atomicMax(&a.stats[4], uint64_t(mx)); }
         }
+#endif
     }
     __syncthreads();
     // 3. an entry takes its owner's exit once the owner is resolved; else it jumps to its owner's
