@@ -15,6 +15,12 @@ w, h, B = 3840, 2160, 16
 n = int(os.environ.get("E2E_N", "4"))
 q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
 c = Codec(0, q, n)
+if os.environ.get("E2E_TORCH_STREAM"):  # the bench's setting: kernels on a torch stream
+    import torch
+    _big = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    _st = torch.cuda.Stream()
+    torch.cuda.set_stream(_st)
+    c.set_stream(_st.cuda_stream)
 hdr, hb = write_header(n, q, True, w, h)
 pitch = (stream_bound(w, h, n, 1, hb) + 255) // 256 * 256
 fr = synth.frames("U", w, h, B, seed=3).ravel()
