@@ -2016,10 +2016,11 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     const int nchunks = int(nch);
     if ((r = ensure(c, c->d_rtab, c->cap_rtab, tab_rows * D))) return r;
     // d_walk (8-byte words): [nchunks / 2] in-workgroup record bases, [G / 2] top-level entries,
-    // [nchunks / 2] chunk counts, [nchunks / 512] workgroup totals
+    // [nchunks / 2] chunk counts, [nchunks / 2] count-pass workgroup totals (a workgroup covers at
+    // least 4 chunks)
     const size_t e_at = size_t(nchunks) / 2 + 1, cnt_at = e_at + size_t(G) / 2 + 1;
     const size_t wg_at = cnt_at + size_t(nchunks) / 2 + 1;
-    if ((r = ensure(c, c->d_walk, c->cap_walk, wg_at + size_t(nchunks) / 512 + 2))) return r;
+    if ((r = ensure(c, c->d_walk, c->cap_walk, wg_at + size_t(nchunks) / 2 + 2))) return r;
     if ((r = ensure(c, c->d_rpos, c->cap_rpos, size_t(nchunks) * ie::kRecPosCap))) return r;
     const size_t pix_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
     const bool out_dev = is_device_ptr(out);
@@ -2045,6 +2046,7 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
     pa.nchunks = nchunks;
     pa.rle = da.rle;
     pa.tab = c->d_rtab;
+    pa.seg = ie::rec_count_seg(uint32_t(C));
     pa.lbase = reinterpret_cast<uint32_t*>(c->d_walk);
     pa.wgsum = reinterpret_cast<uint32_t*>(c->d_walk + wg_at);
     pa.E = reinterpret_cast<uint32_t*>(c->d_walk + e_at);

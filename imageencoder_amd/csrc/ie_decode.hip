@@ -222,6 +222,13 @@ __device__ __forceinline__ uint32_t rec_len(const uint32_t* L, uint32_t p, int r
 
 __host__ __device__ constexpr int rec_table_stream_words(uint32_t C) { return int((C + 95) >> 5) + 3; }
 __host__ __device__ constexpr int rec_decode_stream_words(uint32_t C, int D) { return int((C + D + 95) >> 5) + 3; }
+// a count wave's LDS words: seg chunks' bits + 64 + alignment slack, a multiple of 4 (16-byte rows)
+__host__ __device__ constexpr int rec_count_wave_words(uint32_t C, int seg) {
+    return (int((uint64_t(seg) * C + 95) >> 5) + 3 + 3 + 3) & ~3;
+}
+int rec_count_seg(uint32_t C) {  // chunks per count wave: <= 16, a wave's bits within 10 KB
+    return int(std::max<uint64_t>(1, std::min<uint64_t>(16, (uint64_t(10 * 1024) * 8 - 256) / C)));
+}
 
 
 // words [w0, w0 + nw) of the stream, byte-swapped to MSB-first, zeros past the stream
@@ -561,38 +568,95 @@ __device__ __forceinline__ uint32_t rec_chunk_entry(const RecParseArgs& a, int k
     return table_entry<RecGeom<N>::D, RecGeom<N>::G>(a.E, a.lvl, a.levels, k);
 }
 
-// Count pass: one LANE per chunk walks its true records from global memory (a record header is
-// one 64-bit window read; consecutive reads of a lane hit the same lines), storing up to
-// kRecPosCap record positions and the count.  Lanes of a wave walk 64 different chunks, so the
-// serial walks run 64 wide.
+// L[i] = bswap(W[w0 + i]) for i < nw (zeros past nwords) by one wave with 16-byte loads, four
+// per lane in flight; L must be 16-byte aligned.  The copy starts at the aligned word w0 & ~3:
+// returns the offset of word w0 in L (0..3).
+__device__ __forceinline__ int stage_words16(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nwords,
+                                             int lane) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const uint64_t wa = w0 & ~3ull;
+    const int off = int(w0 - wa);
+    const int nq = (nw + off + 3) >> 2;  // 16-byte groups
+    const uint64_t nfull = nwords >> 2;  // groups wholly inside the stream
+    for (int q0 = 0; q0 < nq; q0 += 64 * 4) {
+        u4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + u * 64 + lane;
+            const uint64_t g = (wa >> 2) + uint64_t(q);
+            if (q < nq && g < nfull) {
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(W) + g);
+            } else {
+                u4 z = {0u, 0u, 0u, 0u};
+                if (q < nq)
+                    for (int e = 0; e < 4; e++)
+                        if (4 * g + e < nwords) z[e] = W[4 * g + e];
+                v[u] = z;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + u * 64 + lane;
+            if (q < nq) {
+                u4 b = {bswap32(v[u].x), bswap32(v[u].y), bswap32(v[u].z), bswap32(v[u].w)};
+                reinterpret_cast<u4*>(L)[q] = b;
+            }
+        }
+    }
+    return off;
+}
+
+// Count pass: each wave stages `seg` consecutive chunks' bits in LDS and one lane per chunk walks
+// its true records from its entry (the prefix maps applied to its top-level entry), storing up to
+// kRecPosCap record positions (relative to the chunk's first word) and the count; the workgroup
+// then scans its 4 * seg chunks' counts (records before each chunk among them, and their total).
 template <int N>
 __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t Lall[];
     __shared__ uint32_t scratch[8];
-    const int k = int(blockIdx.x * kTPB + threadIdx.x);
-    uint32_t R = 0;
-    if (k < a.nchunks) {
-        const uint64_t c0 = a.start_bit + uint64_t(k) * a.C;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int seg = a.seg;
+    const int k0 = (blockIdx.x * 4 + wv) * seg;  // this wave's first chunk
+    const int m = max(0, min(seg, a.nchunks - k0));
+    uint32_t* L = Lall + size_t(wv) * rec_count_wave_words(a.C, seg);
+    uint32_t s0 = 0;
+    if (m > 0) {
+        const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
         const uint64_t base = c0 & ~31ull;
-        const uint64_t end = min<uint64_t>(c0 + a.C, a.nbits);  // no record starts at or past the stream's end
-        uint64_t p = c0 + rec_chunk_entry<N>(a, k);
+        const int off = stage_words16(L, a.words, base >> 5, int(((c0 - base) + uint64_t(m) * a.C + 64) >> 5) + 2,
+                                      (a.nbits + 31) >> 5, lane);
+        s0 = uint32_t(c0 - base) + 32u * uint32_t(off);  // the wave's first bit, relative to L
+    }
+    const int k = k0 + lane;
+    const bool mine = lane < m;
+    const uint32_t x = mine ? rec_chunk_entry<N>(a, k) : 0u;
+    wave_sync();
+    uint32_t R = 0;
+    if (mine) {
+        const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;  // = bit s0 of L
+        const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - c0 + s0, uint64_t(s0) + uint64_t(m) * a.C));
+        const uint32_t cs = s0 + uint32_t(lane) * a.C;
+        const uint32_t cb = cs & ~31u;  // the chunk's first word
+        const uint32_t ce = min(cs + a.C, lim);  // no record starts at or past the stream's end
         uint16_t* pos = a.pos + size_t(k) * kRecPosCap;
-        while (p < end) {
-            const uint32_t l = rec_len_head<N>(getbits(a.words, p, 20), a.rle);
+        uint32_t p = cs + x;
+        while (p < ce) {
+            const uint32_t l = rec_len_head<N>(lbits(L, p, 20), a.rle);
             if (l > 1u) {
-                if (R < uint32_t(kRecPosCap)) pos[R] = uint16_t(p - base);
+                if (R < uint32_t(kRecPosCap)) pos[R] = uint16_t(p - cb);
                 R++;
             }
             p += l;
         }
     }
-    // records before the chunk among its workgroup's kTPB chunks, and the workgroup's total
+    // records before each chunk within the workgroup (thread order = chunk order; idle lanes add 0)
     uint32_t tot;
     const uint32_t ex = block_excl_scan(R, scratch, &tot);
-    if (k < a.nchunks) {
+    if (mine) {
         a.cnt[k] = R;
         a.lbase[k] = ex;
     }
-    if (threadIdx.x == 0) a.wgsum[blockIdx.x] = tot;
+    if (tid == 0) a.wgsum[blockIdx.x] = tot;
 }
 
 template <int N>
@@ -610,7 +674,7 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
     // first block index: the totals of the count pass's workgroups before this chunk's, plus the
     // records before it in its own (no separate scan launch)
     uint64_t part = 0;
-    for (int g = lane; g < k / kTPB; g += 64) part += a.wgsum[g];
+    for (int g = lane; g < k / (4 * a.seg); g += 64) part += a.wgsum[g];
     const uint64_t first = wave_sum64(part) + a.lbase[k];
     const uint32_t R = a.cnt[k];
     if (k == a.nchunks - 1 && lane == 0) *a.total = first + R;
@@ -670,9 +734,10 @@ int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t
                                 : launch_compose<RecGeom<8>::D, RecGeom<8>::G>(a.tab, a.nchunks, a.E, a.ticket + 1, a.lvl, s);
     if (levels < 0) return -1;
     a.levels = levels;
-    const int nbc = (a.nchunks + kTPB - 1) / kTPB;
-    if (n == 4) hipLaunchKernelGGL((rec_count_kernel<4>), dim3(nbc), dim3(kTPB), 0, s, a);
-    else hipLaunchKernelGGL((rec_count_kernel<8>), dim3(nbc), dim3(kTPB), 0, s, a);
+    const int nbc = (a.nchunks + 4 * a.seg - 1) / (4 * a.seg);
+    const size_t lc = size_t(rec_count_wave_words(a.C, a.seg)) * 4 * 4;
+    if (n == 4) hipLaunchKernelGGL((rec_count_kernel<4>), dim3(nbc), dim3(kTPB), lc, s, a);
+    else hipLaunchKernelGGL((rec_count_kernel<8>), dim3(nbc), dim3(kTPB), lc, s, a);
     if (n == 4) hipLaunchKernelGGL((rec_decode_kernel<4>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 4), s, a, d);
     else hipLaunchKernelGGL((rec_decode_kernel<8>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 8), s, a, d);
     return levels;

@@ -183,6 +183,7 @@ struct RecParseArgs {
     uint32_t* cnt;          // [nchunks] records of every chunk
     uint32_t* lbase;        // [nchunks] records before every chunk within its count-pass workgroup
     uint32_t* wgsum;        // [count-pass workgroups] their record totals
+    int seg;                // chunks per count-pass wave (rec_count_seg): a workgroup covers 4 * seg
     uint64_t* total;        // records on the true path
     uint64_t* end_out;      // end bit of the last block's record
     unsigned long long* stats;  // diagnostics (IE_DEC_STATS): walk steps; nullptr = off
@@ -191,6 +192,7 @@ int rec_group_chunks(int n);
 int rec_entry_span(int n);
 size_t rec_table_lds(uint32_t C, int n);
 size_t rec_decode_lds(uint32_t C, int n);
+int rec_count_seg(uint32_t C);
 // Returns the number of composition levels (< 0: too many chunks).
 int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t s);
 

@@ -496,3 +496,19 @@ def test_decode_chunking_matches(codec, tmp_path, name, recs):
     assert md5 == _md5(default.tobytes())
     if "dec_md5" in c:
         assert md5 == c["dec_md5"]
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_decode_truncated_stream_fails(codec, n):
+    """A payload cut short holds fewer records than the header's frame needs: the decode fails with
+    IE_EFORMAT ("stream ends before the last block") instead of returning pixels."""
+    from imageencoder_amd import IEError
+    w, h = 256, 128
+    y = synth.frame("U", w, h, seed=5)
+    q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+    enc = codec.encode_image_file(y, w, h, q, n, rle=True, huffman=False)
+    assert np.array_equal(codec.decode_image_file(enc, n), O.load().decode_image(enc, n))
+    with pytest.raises(IEError):
+        codec.decode_image_file(enc[: len(enc) * 9 // 10], n)
+    # the context stays usable
+    assert np.array_equal(codec.decode_image_file(enc, n), O.load().decode_image(enc, n))
