@@ -476,44 +476,53 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
 }
 
 // One composition level over n tables ([n][D], 16-bit exits): prefix maps written over the
-// tables, composites into comp ([ceil(n/G)][D]); with `top`, the last workgroup chases the
-// stream's start (entry 0) through the composites: E[q] = entry of composite q.  Shared by the
-// record parse (D = the longest record) and the Huffman decode (D = the longest code).
+// tables, composites into comp ([ceil(n/G)][D]).  Shared by the record parse (D = the longest
+// record) and the Huffman decode (D = the longest code).
 template <int D, int G>
-__global__ __launch_bounds__(kTPB) void compose_kernel(uint16_t* tab, int n, uint16_t* comp, int top, uint32_t* E,
-                                                       unsigned* ticket) {
+__global__ __launch_bounds__(kTPB) void compose_kernel(uint16_t* tab, int n, uint16_t* comp) {
     __shared__ uint16_t S[G * D];
-    __shared__ unsigned last;
-    const int tid = threadIdx.x, g = blockIdx.x, ng = gridDim.x;
+    const int tid = threadIdx.x, g = blockIdx.x;
     const int k0 = g * G, nk = min(G, n - k0);
     uint16_t* T = tab + size_t(k0) * D;
     for (int i = tid; i < nk * D; i += kTPB) S[i] = T[i];
     __syncthreads();
-    for (int d = tid; d < D; d += kTPB) {
-        uint32_t x = uint32_t(d);
-        for (int j = 0; j < nk; j++) {
-            T[j * D + d] = uint16_t(x);  // P_j: group entry d -> entry of table j
-            x = S[j * D + x];
+    // every entry chased through the group's tables; a thread's entries (tid, tid + kTPB, ...) are
+    // chased side by side, so their dependent LDS reads overlap
+    constexpr int CH = (D + kTPB - 1) / kTPB;
+    uint32_t x[CH];
+#pragma unroll
+    for (int c = 0; c < CH; c++) x[c] = uint32_t(tid + c * kTPB);
+    for (int j = 0; j < nk; j++) {
+#pragma unroll
+        for (int c = 0; c < CH; c++) {
+            const int d = tid + c * kTPB;
+            if (d < D) {
+                T[j * D + d] = uint16_t(x[c]);  // P_j: group entry d -> entry of table j
+                x[c] = S[j * D + x[c]];
+            }
         }
-        comp[size_t(g) * D + d] = uint16_t(x);
     }
-    if (!top) return;
-    // the last workgroup to finish sees every composite
-    __threadfence();
+#pragma unroll
+    for (int c = 0; c < CH; c++) {
+        const int d = tid + c * kTPB;
+        if (d < D) comp[size_t(g) * D + d] = uint16_t(x[c]);
+    }
+}
+
+// The top chase: the stream's start (entry 0) through the ng <= G top-level composites, E[q] = the
+// entry of composite q (one workgroup; a launch of its own, so the composites are visible without
+// a device-wide fence in every composing workgroup).
+template <int D, int G>
+__global__ __launch_bounds__(kTPB) void compose_top_kernel(const uint16_t* comp, int ng, uint32_t* E) {
+    __shared__ uint16_t S[G * D];
+    for (int i = threadIdx.x; i < ng * D; i += kTPB) S[i] = comp[i];
     __syncthreads();
-    if (tid == 0) last = (atomicAdd(ticket, 1u) == unsigned(ng) - 1u) ? 1u : 0u;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    for (int i = tid; i < ng * D; i += kTPB) S[i] = comp[i];  // ng <= G
-    __syncthreads();
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
         uint32_t x = 0;
         for (int q = 0; q < ng; q++) {
             E[q] = x;
             x = S[q * D + x];
         }
-        *ticket = 0u;  // re-armed for the next decode
     }
 }
 
@@ -530,9 +539,13 @@ int launch_compose(uint16_t* tab, int n, uint32_t* E, unsigned* ticket, uint16_t
         if (levels >= kRecMaxLevels) return -1;
         lvl[levels] = arr;
         uint16_t* comp = arr + size_t(cur) * D;
-        hipLaunchKernelGGL((compose_kernel<D, G>), dim3(ng), dim3(kTPB), 0, s, arr, cur, comp, top, E, ticket);
+        hipLaunchKernelGGL((compose_kernel<D, G>), dim3(ng), dim3(kTPB), 0, s, arr, cur, comp);
         levels++;
-        if (top) return levels;
+        if (top) {
+            hipLaunchKernelGGL((compose_top_kernel<D, G>), dim3(1), dim3(kTPB), 0, s, comp, ng, E);
+            (void)ticket;
+            return levels;
+        }
         arr = comp;
         cur = ng;
     }
