@@ -56,8 +56,16 @@ def frame(kind: str, w: int, h: int, seed: int = DEFAULT_SEED) -> np.ndarray:
 
 
 def frames(kind: str, w: int, h: int, count: int, seed: int = DEFAULT_SEED) -> np.ndarray:
-    """``count`` distinct frames (seed + frame index), shape (count, h, w)."""
+    """``count`` distinct frames (seed + frame index), shape (count, h, w).  Kind "P" (panning):
+    windows of one larger "mixed" picture moving by (3, 2) px per frame plus +-2 noise -- content
+    a motion search can follow (the P-frame tests)."""
     out = np.empty((count, h, w), dtype=np.uint8)
+    if kind in ("P", "panning"):
+        base = mixed(w + 3 * count + 8, h + 2 * count + 8, seed).astype(np.int64)
+        for f in range(count):
+            noise = (splitmix64(seed + 1 + f, 0, w * h) % np.uint64(5)).astype(np.int64).reshape(h, w) - 2
+            out[f] = np.clip(base[2 * f: 2 * f + h, 3 * f: 3 * f + w] + noise, 0, 255).astype(np.uint8)
+        return out
     for f in range(count):
         out[f] = frame(kind, w, h, seed + f)
     return out

@@ -193,6 +193,154 @@ int64_t encode_frames(const uint8_t* y, int w, int h, size_t stride, size_t fram
     return int64_t(wr.pos);
 }
 
+// ------------------------------------------------------------ P-frames (gop > 1)
+// The 9-point pattern of algo.cpp:90-100 (index 0 = the centre).
+const int kMerSx[9] = {0, 1, 1, 0, -1, -1, -1, 0, 1};
+const int kMerSy[9] = {0, 0, 1, 1, 1, 0, -1, -1, -1};
+constexpr int kMB = 16;  // dc::MacroBlockSize (Block.hpp:14)
+
+inline int clamp_i16(int v, int lo, int hi) { return int(std::clamp(int16_t(v), int16_t(lo), int16_t(hi))); }
+
+// sum |cur - ref| over the 16x16 macroblock (Block.cpp:241-254)
+uint64_t mb_sad(const uint8_t* cur, size_t cs, const uint8_t* ref, size_t rs) {
+    uint64_t d = 0;
+    for (int y = 0; y < kMB; y++)
+        for (int x = 0; x < kMB; x++) d += uint64_t(std::abs(int(cur[y * cs + x]) - int(ref[y * rs + x])));
+    return d;
+}
+
+// One P-frame (Frame.cpp:160-243): motion search per macroblock (Block.cpp:267-339 over the
+// pattern tree of algo.cpp:119-139, walked without materialising it: child p of the node at
+// (x, y) with radius r sits at (x + sx[p] r, y + sy[p] r), radius r / 2; r == 0 is a leaf),
+// the prediction error per 4x4 microblock through processDCTDivQ / createRLESequence /
+// processIDCTMulQ (ImageBase.cpp:266-306), the reference block copied into the frame
+// (copyBlockMatrixTo) and expandDifferences (Block.cpp:110-119) over every microblock.
+// cur is read, rec receives the frame as the reference leaves it in its buffer (the next frame's
+// reference).  Writes the mvecs, then the microblock records.
+void pframe(const Tables& T, const double* qd, const uint8_t* cur, size_t cs, const uint8_t* ref, size_t rs,
+            uint8_t* rec, int w, int h, int rle, int merange, BitWriter& wr) {
+    const int n = T.n, nn = n * n;
+    const int mbx = w / kMB, mby = h / kMB;  // ImageBase.cpp:213-214 (floor)
+    const int bx = w / n;
+    const int mv_bits = bits_needed_ref(int16_t(merange));  // VideoBase.cpp:42
+    // microblocks are built BEFORE any macroblock copy: expanded = the frame's own pixels
+    std::vector<double> E(size_t(w) * h);
+    for (size_t i = 0; i < size_t(w) * h; i++) E[i] = double(cur[(i / w) * cs + i % w]);
+    std::vector<uint8_t> M(size_t(w) * h);  // the frame buffer (matrix) as the macroblock loop leaves it
+    for (int y = 0; y < h; y++) std::memcpy(&M[size_t(y) * w], cur + size_t(y) * cs, size_t(w));
+    std::vector<int16_t> coef(size_t(bx) * (h / n) * nn, 0);
+    std::vector<char> has_rle(size_t(bx) * (h / n), 0);
+    // micro_per_macro_row (ImageBase.cpp:271): integer division, 0 for 8x8 blocks
+    const int mpr = (kMB * kMB / nn) / n;
+    for (int mb = 0; mb < mbx * mby; mb++) {
+        const int mx = (mb % mbx) * kMB, my = (mb / mbx) * kMB;
+        const uint8_t* cb = cur + size_t(my) * cs + mx;
+        // search: the first best block is the one at ABSOLUTE (0, 0) (Block.cpp:272-274)
+        int cx = 0, cy = 0, r = merange / 2;
+        int bbx = clamp_i16(0, 0, w - kMB), bby = clamp_i16(0, 0, h - kMB);
+        uint64_t best = UINT64_MAX;
+        while (r != 0) {
+            int np = -1, nbx = 0, nby = 0;
+            uint64_t nd = best;
+            for (int p = 0; p < 9; p++) {
+                const int px = clamp_i16(int16_t(cx + kMerSx[p] * r + mx), 0, w - kMB);
+                const int py = clamp_i16(int16_t(cy + kMerSy[p] * r + my), 0, h - kMB);
+                if (p > 0 && px == mx && py == my) continue;  // Block.cpp:297-301
+                const uint64_t d = mb_sad(cb, cs, ref + size_t(py) * rs + px, rs);
+                if (d <= nd) { np = p; nd = d; nbx = px; nby = py; }
+            }
+            if (np < 0) break;
+            cx += kMerSx[np] * r;
+            cy += kMerSy[np] * r;
+            r /= 2;
+            best = nd;
+            bbx = nbx;
+            bby = nby;
+        }
+        // prediction error (expandDifferenceWith, Block.cpp:256-265) per microblock
+        for (int y = 0; y < mpr; y++)
+            for (int x = 0; x < mpr; x++) {
+                double xs[64];
+                for (int i = 0; i < n; i++)
+                    for (int j = 0; j < n; j++) {
+                        const int yy = y * n + i, xx = x * n + j;
+                        const double diff = double(cb[size_t(yy) * cs + xx]) - double(ref[size_t(bby + yy) * rs + bbx + xx]);
+                        xs[i * n + j] = diff + double(-128);
+                    }
+                const size_t b = size_t(my / n + y) * bx + size_t(mx / n + x);
+                int16_t* o = &coef[b * nn];
+                for (int uv = 0; uv < nn; uv++) {
+                    const double* Puv = &T.P[size_t(uv) * nn];
+                    double acc = 0.0;
+                    for (int k = 0; k < nn; k++) acc = acc + Puv[k] * xs[k];
+                    o[uv] = int16_t(std::round((acc * T.S[uv]) / qd[uv]));
+                }
+                has_rle[b] = 1;
+                // processIDCTMulQ (Block.cpp:162-177): the decoded error + 128 replaces expanded
+                double yq[64], t[64];
+                for (int k = 0; k < nn; k++) { yq[k] = double(o[k]) * qd[k]; t[k] = 0.0; }
+                for (int uv = 0; uv < nn; uv++) {
+                    const double* Ruv = &T.R[size_t(uv) * nn];
+                    for (int ij = 0; ij < nn; ij++) t[ij] = t[ij] + Ruv[ij] * yq[uv];
+                }
+                for (int i = 0; i < n; i++)
+                    for (int j = 0; j < n; j++)
+                        E[size_t(my + y * n + i) * w + mx + x * n + j] = t[i * n + j] + double(128);
+            }
+        // the reference block at the motion vector replaces the macroblock (Frame.cpp:220-225)
+        const int ccx = clamp_i16(int16_t(mx + cx), 0, w - kMB), ccy = clamp_i16(int16_t(my + cy), 0, h - kMB);
+        for (int y = 0; y < kMB; y++)
+            std::memcpy(&M[size_t(my + y) * w + mx], ref + size_t(ccy + y) * rs + ccx, kMB);
+        wr.put(mv_bits, uint32_t(int32_t(int16_t(cx))));  // streamMVec (Block.cpp:415-423)
+        wr.put(mv_bits, uint32_t(int32_t(int16_t(cy))));
+    }
+    // expandDifferences over every microblock (Frame.cpp:234-242); only those a macroblock
+    // covered have an RLE sequence to stream (Block.cpp:373-375)
+    for (size_t i = 0; i < size_t(w) * h; i++)
+        rec[i] = uint8_t(std::clamp(double(M[i]) + E[i], 0.0, 255.0));
+    for (size_t b = 0; b < has_rle.size(); b++)
+        if (has_rle[b]) emit_block(T, &coef[b * nn], rle, wr);
+}
+
+// The frame loop of VideoEncoder.cpp:83-91 with gop (VideoBase.cpp:96-122, VideoBase.hpp:32):
+// frame f is an I-frame when f % gop == 0; a P-frame's reference is the previous frame's buffer
+// as that frame's processing left it (an I-frame leaves its pixels untouched).
+int64_t encode_gop(const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes, int n,
+                   const uint16_t* q, int rle, int gop, int merange, uint8_t* out, size_t cap, uint64_t start_bit,
+                   uint64_t* frame_bits) {
+    if ((n != 4 && n != 8) || w <= 0 || h <= 0 || w % n || h % n) return -1;
+    gop = std::max(1, gop);
+    // P-frames with W % 16 != 0 and two or more macroblock rows: the reference reads its
+    // macroblocks from misplaced, overlapping rows (ImageBase.cpp:223-227) in a racy OpenMP loop
+    if (gop > 1 && nframes > 1 && w % kMB && h / kMB >= 2) return -1;
+    Tables T(n);
+    double qd[64];
+    for (int k = 0; k < n * n; k++) qd[k] = double(q[k]);
+    BitWriter wr(out, cap, start_bit);
+    std::vector<uint8_t> rec[2] = {std::vector<uint8_t>(size_t(w) * h), std::vector<uint8_t>(size_t(w) * h)};
+    const uint8_t* ref = nullptr;
+    size_t rs = 0;
+    for (int f = 0; f < nframes; f++) {
+        const uint8_t* fy = y + size_t(f) * frame_pitch;
+        const uint64_t s = wr.pos;
+        if (f % gop == 0) {
+            const int64_t e = encode_frames(fy, w, h, stride, 0, 1, n, q, rle, out, cap, wr.pos, nullptr);
+            if (e < 0) return e;
+            wr.pos = uint64_t(e);  // encode_frames wrote through its own writer
+            ref = fy;
+            rs = stride;
+        } else {
+            std::vector<uint8_t>& rb = rec[f & 1];
+            pframe(T, qd, fy, stride, ref, rs, rb.data(), w, h, rle, merange, wr);
+            ref = rb.data();
+            rs = size_t(w);
+        }
+        if (frame_bits) frame_bits[f] = wr.pos - s;
+    }
+    if (wr.overflow) return -2;
+    return int64_t(wr.pos);
+}
+
 // ------------------------------------------------------------ Huffman (Huffman.hpp / .cpp)
 struct Node {
     const uint8_t data;
@@ -432,16 +580,28 @@ int64_t ieo_encode_image(const uint8_t* y, int w, int h, int n, const uint16_t* 
 
 int64_t ieo_encode_video(const uint8_t* yuv, size_t yuv_len, int w, int h, int n, const uint16_t* q, int rle,
                          int huffman, int merange, uint8_t* out, size_t cap) {
+    return ieo_encode_video_gop(yuv, yuv_len, w, h, n, q, rle, huffman, 1, merange, out, cap);
+}
+
+int64_t ieo_encode_video_gop(const uint8_t* yuv, size_t yuv_len, int w, int h, int n, const uint16_t* q, int rle,
+                             int huffman, int gop, int merange, uint8_t* out, size_t cap) {
     if ((n != 4 && n != 8) || w % n || h % n) return -1;
     const size_t pitch = size_t(w) * h + size_t(w) * h / 2;  // Y + UV (VideoBase.cpp:8-9,39-40)
     const int frames = int(yuv_len / pitch);
-    const size_t bound = 128 + 16 * 64 + (size_t(w) * h * 17 / 8 + size_t(w) * h / (n * n)) * size_t(frames);
+    const size_t bound = 128 + 16 * 64 + (size_t(w) * h * 17 / 8 + size_t(w) * h / (n * n) + size_t(w) * h / 32) * size_t(frames);
     std::vector<uint8_t> buf(bound, 0);
-    const int64_t hb = ieo_write_header(buf.data(), bound, n, q, rle, w, h, huffman, 1, frames, 1, merange);
+    const int64_t hb = ieo_write_header(buf.data(), bound, n, q, rle, w, h, huffman, 1, frames, std::max(1, gop), merange);
     if (hb < 0) return hb;
-    const int64_t end = encode_frames(yuv, w, h, size_t(w), pitch, frames, n, q, rle, buf.data(), bound, uint64_t(hb), nullptr);
+    const int64_t end = encode_gop(yuv, w, h, size_t(w), pitch, frames, n, q, rle, gop, merange, buf.data(), bound,
+                                   uint64_t(hb), nullptr);
     if (end < 0) return end;
     return finish(buf, uint64_t(end), huffman, out, cap);
+}
+
+int64_t ieo_encode_gop(const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes, int n,
+                       const uint16_t* q, int rle, int gop, int merange, uint8_t* out, size_t cap, uint64_t start_bit,
+                       uint64_t* frame_bits) {
+    return encode_gop(y, w, h, stride, frame_pitch, nframes, n, q, rle, gop, merange, out, cap, start_bit, frame_bits);
 }
 
 // Huffman<uint8_t>::decode alone (Huffman.cpp:354-402): the decoded bytes (passthrough = 0) or,

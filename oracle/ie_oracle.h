@@ -54,6 +54,17 @@ int64_t ieo_encode_image(const uint8_t* y, int w, int h, int n, const uint16_t* 
 int64_t ieo_encode_video(const uint8_t* yuv, size_t yuv_len, int w, int h, int n, const uint16_t* q,
                          int rle, int huffman, int merange, uint8_t* out, size_t cap);
 
+/* Complete video file with I/P-frames: frame f is an I-frame when f % gop == 0, every other frame
+ * a P-frame -- macroblock motion search + coded prediction error (VideoEncoder.cpp:22-107,
+ * VideoBase.cpp:96-122, Frame.cpp:129-247, Block.cpp:241-339, ImageBase.cpp:208-306). */
+int64_t ieo_encode_video_gop(const uint8_t* yuv, size_t yuv_len, int w, int h, int n, const uint16_t* q,
+                             int rle, int huffman, int gop, int merange, uint8_t* out, size_t cap);
+
+/* The payload alone (ieo_encode_blocks with gop / merange): frames at y + f*frame_pitch. */
+int64_t ieo_encode_gop(const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes, int n,
+                       const uint16_t* q, int rle, int gop, int merange, uint8_t* out, size_t cap,
+                       uint64_t start_bit, uint64_t* frame_bits);
+
 /* Huffman post-pass over whole bytes (Huffman.cpp:233-344).  Returns output bytes. */
 int64_t ieo_huffman_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap);
 /* Huffman<uint8_t>::decode (Huffman.cpp:354-402): decoded bytes, or 0 with *passthrough = 1 when

@@ -41,6 +41,12 @@ class Oracle:
         L.ieo_encode_video.argtypes = [_u8p, C.c_size_t, C.c_int, C.c_int, C.c_int, _u16p, C.c_int, C.c_int,
                                        C.c_int, _u8p, C.c_size_t]
         L.ieo_encode_video.restype = C.c_int64
+        L.ieo_encode_video_gop.argtypes = [_u8p, C.c_size_t, C.c_int, C.c_int, C.c_int, _u16p, C.c_int, C.c_int,
+                                           C.c_int, C.c_int, _u8p, C.c_size_t]
+        L.ieo_encode_video_gop.restype = C.c_int64
+        L.ieo_encode_gop.argtypes = [_u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, _u16p,
+                                     C.c_int, C.c_int, C.c_int, _u8p, C.c_size_t, C.c_uint64, _u64p]
+        L.ieo_encode_gop.restype = C.c_int64
         L.ieo_huffman_encode.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t]
         L.ieo_huffman_encode.restype = C.c_int64
         L.ieo_huffman_decode.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t, C.POINTER(C.c_int)]
@@ -120,6 +126,30 @@ class Oracle:
         assert r >= 0, r
         return out[:r].tobytes()
 
+    def encode_video_gop(self, yuv: bytes, w: int, h: int, n: int, q, rle=True, huffman=False, gop=1,
+                         merange=16) -> bytes:
+        buf = np.frombuffer(yuv, dtype=np.uint8)
+        q = np.ascontiguousarray(q, dtype=np.uint16)
+        cap = len(yuv) * 3 + 4096
+        out = np.zeros(cap, dtype=np.uint8)
+        r = self.lib.ieo_encode_video_gop(self._p(buf), buf.size, w, h, n, self._p(q, _u16p), int(rle),
+                                          int(huffman), gop, merange, self._p(out), cap)
+        assert r >= 0, r
+        return out[:r].tobytes()
+
+    def encode_gop(self, y: np.ndarray, n: int, q, gop: int, merange: int, rle=True, start_bit=0):
+        """y: (frames, h, w).  The I/P payload from start_bit: (buffer, end_bit, frame_bits)."""
+        y = np.ascontiguousarray(y, dtype=np.uint8)
+        f, h, w = y.shape
+        q = np.ascontiguousarray(q, dtype=np.uint16)
+        cap = (start_bit + 7) // 8 + f * (w * h * 17 // 8 + w * h // (n * n) + w * h // 32) + 64
+        out = np.zeros(cap, dtype=np.uint8)
+        fb = np.zeros(f, dtype=np.uint64)
+        end = self.lib.ieo_encode_gop(self._p(y), w, h, w, w * h, f, n, self._p(q, _u16p), int(rle), gop, merange,
+                                      self._p(out), out.size, start_bit, fb.ctypes.data_as(_u64p))
+        assert end >= 0, end
+        return out, int(end), fb
+
     def huffman_encode(self, data: bytes) -> bytes:
         a = np.frombuffer(data, dtype=np.uint8)
         cap = len(data) * 2 + 4096
@@ -193,3 +223,8 @@ def case_expected(c) -> bytes | None:
     if "file" in c:
         return open(os.path.join(GOLDEN, c["file"]), "rb").read()
     return None
+
+
+def manifest_gop():
+    """P-frame video cases (tests/golden/make_golden_gop.py)."""
+    return json.load(open(os.path.join(GOLDEN, "manifest_gop.json")))
