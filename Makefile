@@ -10,7 +10,7 @@ OBJDIR   := build
 # the FP32 fast path uses explicit fmaf and is unaffected.
 HIPFLAGS := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -ffp-contract=off \
             -Wall -Wno-unused-function
-KERNELS  := ie_encode ie_huffman ie_decode
+KERNELS  := ie_encode ie_huffman ie_decode ie_pframe
 OBJS     := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(KERNELS) ie_capi))
 
 .PHONY: all lib oracle ref host clean asmcheck

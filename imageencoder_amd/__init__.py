@@ -63,6 +63,10 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.ie_stream_bound.restype = C.c_size_t
     L.ie_encode_frames.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                    u8p, C.c_size_t, C.c_uint64, u64p, u64p]
+    L.ie_gop_stream_bound.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
+    L.ie_gop_stream_bound.restype = C.c_size_t
+    L.ie_encode_gop.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                C.c_int, C.c_int, u8p, C.c_size_t, C.c_uint64, u64p, u64p]
     L.ie_encode_images.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                    u8p, C.c_size_t, C.c_uint64, u64p]
     L.ie_encode_images_counted.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
@@ -124,6 +128,8 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
                                    C.c_size_t]
     H.ieh_encode_video.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, vp, C.c_size_t]
+    H.ieh_encode_video_gop.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_int, C.c_int, vp, C.c_size_t]
     H.ieh_decode_image.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip]
     H.ieh_decode_video.argtypes = [vp, vp, C.c_size_t, C.c_int, vp, C.c_size_t, ip, ip, ip]
     H.ieh_huffman_encode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t]
@@ -145,7 +151,7 @@ def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
     H.ieh_huffman_encode_device_batch.restype = C.c_int
     H.ieh_release.argtypes = [vp]
     H.ieh_release.restype = None
-    for f in ("ieh_encode_image", "ieh_encode_video", "ieh_decode_image", "ieh_decode_video", "ieh_huffman_encode",
+    for f in ("ieh_encode_image", "ieh_encode_video", "ieh_encode_video_gop", "ieh_decode_image", "ieh_decode_video", "ieh_huffman_encode",
               "ieh_huffman_decode"):
         getattr(H, f).restype = C.c_int64
     _host = H
@@ -327,6 +333,24 @@ class Codec:
             return None
         return fb, int(end.value)
 
+    def gop_stream_bound(self, w: int, h: int, nframes: int, merange: int, start_bit: int = 0) -> int:
+        return int(self.L.ie_gop_stream_bound(w, h, self.n, nframes, merange, start_bit))
+
+    def encode_gop(self, y, w: int, h: int, out, gop: int, merange: int, start_bit: int = 0,
+                   stride: int | None = None, frame_pitch: int | None = None, nframes: int = 1, rle: bool = True,
+                   mode: int = MODE_FAST):
+        """The payload of a video with I- and P-frames (frame f is an I-frame when f % gop == 0;
+        VideoEncoder.cpp:83-91, Frame.cpp:129-247) appended to ``out`` from ``start_bit``; ``out``
+        holds :meth:`gop_stream_bound` bytes.  Returns ``(frame_bits, end_bit)``."""
+        stride = w if stride is None else stride
+        frame_pitch = stride * h if frame_pitch is None else frame_pitch
+        fb = np.zeros(nframes, dtype=np.uint64)
+        end = C.c_uint64(0)
+        self._chk(self.L.ie_encode_gop(self.h, _ptr(y), w, h, stride, frame_pitch, nframes, gop, merange, int(rle),
+                                       mode, _ptr(out), _nbytes(out), start_bit,
+                                       fb.ctypes.data_as(C.POINTER(C.c_uint64)), C.pointer(end)))
+        return fb, int(end.value)
+
     def encode_images(self, y, w: int, h: int, out, out_pitch: int, nframes: int, start_bit: int = 0,
                       stride: int | None = None, frame_pitch: int | None = None, rle: bool = True,
                       mode: int = MODE_FAST, want_sizes: bool = True, count_bytes: bool = False):
@@ -438,14 +462,16 @@ class Codec:
         return out[:r].tobytes()
 
     def encode_video_file(self, yuv, w: int, h: int, q, n: int, rle: bool = True, huffman: bool = True,
-                          merange: int = 0, mode: int = MODE_FAST) -> bytes:
+                          merange: int = 0, mode: int = MODE_FAST, gop: int = 1) -> bytes:
+        """A video file as VideoEncoder writes it; gop > 1 adds P-frames (motion search + coded
+        prediction error, Frame.cpp:160-243)."""
         H = load_host_library()
         q = np.ascontiguousarray(np.asarray(q, dtype=np.uint16).ravel())
         frames = _nbytes(yuv) // (w * h + w * h // 2)
-        cap = stream_bound(w, h, n, max(frames, 1), 2048) + 64
+        cap = stream_bound(w, h, n, max(frames, 1), 2048) + (w // 16) * (h // 16) * 4 * max(frames, 1) + 64
         out = np.zeros(cap, dtype=np.uint8)
-        r = self._host_chk(H.ieh_encode_video(self.h, _ptr(yuv), _nbytes(yuv), w, h, q.ctypes.data, n, int(rle),
-                                              int(huffman), merange, mode, out.ctypes.data, cap))
+        r = self._host_chk(H.ieh_encode_video_gop(self.h, _ptr(yuv), _nbytes(yuv), w, h, q.ctypes.data, n, int(rle),
+                                                  int(huffman), gop, merange, mode, out.ctypes.data, cap))
         return out[:r].tobytes()
 
     def decode_image_file(self, data: bytes, n: int):

@@ -101,15 +101,22 @@ int encode_file(ie_ctx* c, const uint8_t* y, const FileParams& p, std::vector<ui
     const uint64_t H = hdr.get_position();
 
     Scratch& s = scratch(c);
-    const size_t cap = ie_stream_bound(p.w, p.h, p.n, p.frames, H);
+    const bool pframes = p.video && p.gop > 1;  // I/P-frame video (VideoEncoder.cpp:83-91 with gop)
+    const size_t cap = pframes ? ie_gop_stream_bound(p.w, p.h, p.n, p.frames, p.merange, H)
+                               : ie_stream_bound(p.w, p.h, p.n, p.frames, H);
     if (!cap) return (err = "invalid dimensions", IE_EINVAL);
     if ((r = s.enc.reserve(cap))) return (err = ie_last_error(c), r);
     const size_t hb = size_t((H + 7) / 8);
-    if ((r = ie_memset(c, s.enc.p, 0, hb + 4))) return (err = ie_last_error(c), r);
+    // the P-frame records are ORed into the stream: it must be zero from the header on
+    if ((r = ie_memset(c, s.enc.p, 0, pframes ? cap : hb + 4))) return (err = ie_last_error(c), r);
     if ((r = ie_memcpy(c, s.enc.p, hdr.get_buffer(), hb))) return (err = ie_last_error(c), r);
     uint64_t end = 0;
-    if ((r = ie_encode_frames(c, y, p.w, p.h, size_t(p.w), p.frame_pitch, p.frames, p.rle ? 1 : 0, p.mode, s.enc.p,
-                              s.enc.cap, H, nullptr, &end)))
+    if (pframes) {
+        if ((r = ie_encode_gop(c, y, p.w, p.h, size_t(p.w), p.frame_pitch, p.frames, p.gop, p.merange, p.rle ? 1 : 0,
+                               p.mode, s.enc.p, s.enc.cap, H, nullptr, &end)))
+            return (err = ie_last_error(c), r);
+    } else if ((r = ie_encode_frames(c, y, p.w, p.h, size_t(p.w), p.frame_pitch, p.frames, p.rle ? 1 : 0, p.mode,
+                                     s.enc.p, s.enc.cap, H, nullptr, &end)))
         return (err = ie_last_error(c), r);
     const size_t bytes = size_t((end + 7) / 8);
     if (!p.huffman) {
@@ -350,7 +357,6 @@ bool VideoEncoder::process() {
     util::Logger::WriteLn("[VideoEncoder] Processing video...");
     const int n = quant_m.n;
     if (width % n || height % n) return (err_ = "width and height must be multiples of the block size", false);
-    if (gop != 1) return (err_ = "P-frames (gop > 1) need motion estimation, which this encoder does not provide", false);
     const size_t pitch = size_t(width) * height + size_t(width) * height / 2;  // Y + UV (VideoBase.cpp:8-9)
     const size_t frames = pitch ? raw_size / pitch : 0;
     if (frames == 0 || frames > 32767) return (err_ = "frame count must be in 1..32767", false);
@@ -367,6 +373,13 @@ bool VideoEncoder::process() {
     p.gop = gop;
     p.merange = merange;
     p.frame_pitch = pitch;
+    if (gop != 1) {
+        // P-frames chain through the previous frame's reconstruction: the whole video goes to the
+        // device first (as VideoBase.cpp:6-19 reads it), then one ie_encode_gop
+        std::vector<uint8_t> all;
+        if (!read_file(source_file, all)) return (err_ = "Could not read file '" + source_file + "'", false);
+        return encode_file(Device::get(), all.data(), p, result_, err_) == IE_OK;
+    }
     return encode_video_streamed(Device::get(), source_file, p, result_, err_) == IE_OK;
 }
 
@@ -437,6 +450,11 @@ int64_t ieh_encode_image(ie_ctx* c, const uint8_t* y, int w, int h, const uint16
 
 int64_t ieh_encode_video(ie_ctx* c, const uint8_t* yuv, size_t len, int w, int h, const uint16_t* q, int n, int rle,
                          int huffman, int merange, int mode, uint8_t* out, size_t cap) {
+    return ieh_encode_video_gop(c, yuv, len, w, h, q, n, rle, huffman, 1, merange, mode, out, cap);
+}
+
+int64_t ieh_encode_video_gop(ie_ctx* c, const uint8_t* yuv, size_t len, int w, int h, const uint16_t* q, int n,
+                             int rle, int huffman, int gop, int merange, int mode, uint8_t* out, size_t cap) {
     if (!c || !yuv || !q || !out || w <= 0 || h <= 0) return IE_EINVAL;
     dc::FileParams p;
     p.w = w;
@@ -449,7 +467,7 @@ int64_t ieh_encode_video(ie_ctx* c, const uint8_t* yuv, size_t len, int w, int h
     p.video = true;
     p.frame_pitch = size_t(w) * h + size_t(w) * h / 2;
     p.frames = int(len / p.frame_pitch);
-    p.gop = 1;
+    p.gop = gop < 1 ? 1 : gop;
     p.merange = merange;
     if (p.frames <= 0 || p.frames > 32767) return IE_EINVAL;
     std::vector<uint8_t> v;

@@ -106,6 +106,18 @@ struct ie_ctx {
     int last_groups = 0;               // and their groups
     unsigned long long* d_first = nullptr;  // [256]
     ie_pipe* pipe = nullptr;           // streamed host path of image batches (created on first use)
+    // P-frame videos (ie_encode_gop): reconstructed frames (two, alternating), the prediction
+    // error's coefficients and record lengths, the scan's tile sums, the frames' bit positions
+    uint8_t* d_gop_rec = nullptr;
+    size_t cap_gop_rec = 0;
+    int16_t* d_gop_coef = nullptr;
+    size_t cap_gop_coef = 0;
+    uint32_t* d_gop_bits = nullptr;
+    size_t cap_gop_bits = 0;
+    uint64_t* d_gop_tile = nullptr;
+    size_t cap_gop_tile = 0;
+    uint64_t* d_gop_pos = nullptr;
+    size_t cap_gop_pos = 0;
 };
 
 namespace {
@@ -1447,6 +1459,11 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_hout);
     (void)hipFree(c->d_pix);
     (void)hipFree(c->d_coef);
+    (void)hipFree(c->d_gop_rec);
+    (void)hipFree(c->d_gop_coef);
+    (void)hipFree(c->d_gop_bits);
+    (void)hipFree(c->d_gop_tile);
+    (void)hipFree(c->d_gop_pos);
     pipe_free(c->pipe);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -1501,6 +1518,140 @@ int ie_encode_frames(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, s
     if (!c || !y || !out) return IE_EINVAL;
     return encode(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_cap, 0, start_bit, 0,
                   frame_bits, end_bit);
+}
+
+// bits_needed of an int16 (utils.hpp:226-243): Frame::MVEC_BIT_SIZE = bits_needed(merange) (VideoBase.cpp:42)
+static int mvec_bits(int merange) {
+    int b = 1;
+    const int16_t v = int16_t(merange);
+    while (int16_t(int16_t((v & ((1 << b) - 1)) << (16 - b)) >> (16 - b)) != v) b++;
+    return b;
+}
+
+size_t ie_gop_stream_bound(int w, int h, int n, int nframes, int merange, uint64_t start_bit) {
+    if ((n != 4 && n != 8) || w <= 0 || h <= 0 || nframes <= 0 || merange < 0 || merange > 32767) return 0;
+    const uint64_t per_frame = uint64_t(w / n) * (h / n) * bound_bits_per_block(n) +
+                               uint64_t(w / 16) * (h / 16) * 2u * uint64_t(mvec_bits(merange));
+    return size_t((start_bit + per_frame * uint64_t(nframes) + 31) / 32) * 4 + 8;
+}
+
+// The frame loop of VideoEncoder.cpp:83-91 with I- and P-frames (VideoBase.cpp:96-122): I-frames
+// through the block encoder, P-frames through ie_pframe.hip; every frame starts at the previous
+// frame's end bit read on the device, and a P-frame's reference is the previous frame's buffer as
+// the reference leaves it (an I-frame's own pixels, a P-frame's reconstruction).
+int ie_encode_gop(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes, int gop,
+                  int merange, int use_rle, int mode, uint8_t* out, size_t out_cap, uint64_t start_bit,
+                  uint64_t* frame_bits, uint64_t* end_bit) {
+    if (!c || !y || !out) return IE_EINVAL;
+    int r = check_dims(c, w, h, nframes);
+    if (r) return r;
+    gop = std::max(1, gop);
+    if (merange < 0 || merange > 32767) return fail(c, IE_EINVAL, "merange must be in [0, 32767] (15-bit header field)");
+    if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
+    if (nframes > 1 && frame_pitch < stride * size_t(h - 1) + size_t(w))
+        return fail(c, IE_EINVAL, "frame_pitch smaller than a frame");
+    const bool has_p = gop > 1 && nframes > 1;
+    if (has_p && w % 16 && h / 16 >= 2)
+        return fail(c, IE_EINVAL, "P-frames need W % 16 == 0 when H >= 32: the reference builds its macroblocks "
+                                  "from misplaced, overlapping rows there (ImageBase.cpp:223-227)");
+    const size_t need = ie_gop_stream_bound(w, h, c->n, nframes, merange, start_bit);
+    if (out_cap < need) return fail(c, IE_ECAP, "output capacity below ie_gop_stream_bound");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool in_dev = is_device_ptr(y), out_dev = is_device_ptr(out);
+
+    const uint8_t* dy = y;
+    if (!in_dev) {
+        const size_t in_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
+        if ((r = ensure(c, c->d_in, c->cap_in, in_bytes))) return r;
+        HIPCHK(c, hipMemcpyAsync(c->d_in, y, in_bytes, hipMemcpyHostToDevice, c->stream));
+        dy = c->d_in;
+    }
+    uint32_t* dout;
+    if (out_dev) {
+        if (reinterpret_cast<uintptr_t>(out) % 4) return fail(c, IE_EINVAL, "device output must be 4-byte aligned");
+        dout = reinterpret_cast<uint32_t*>(out);
+    } else {
+        // zeroed staging (the P-frame records are ORed in) holding the caller's leading bytes
+        if ((r = ensure(c, c->d_out, c->cap_out, need))) return r;
+        HIPCHK(c, hipMemsetAsync(c->d_out, 0, need, c->stream));
+        const size_t hb = size_t((start_bit + 7) / 8);
+        if (hb) HIPCHK(c, hipMemcpyAsync(c->d_out, out, hb, hipMemcpyHostToDevice, c->stream));
+        dout = reinterpret_cast<uint32_t*>(c->d_out);
+    }
+    const int n = c->n, bx = w / n, nb = bx * (h / n);
+    if (has_p) {
+        if ((r = ensure(c, c->d_gop_rec, c->cap_gop_rec, 2 * size_t(w) * h))) return r;
+        if ((r = ensure(c, c->d_gop_coef, c->cap_gop_coef, size_t(nb) * 16))) return r;
+        if ((r = ensure(c, c->d_gop_bits, c->cap_gop_bits, size_t(nb)))) return r;
+        if ((r = ensure(c, c->d_gop_tile, c->cap_gop_tile, size_t(ie::pframe_tiles(nb)) + 1))) return r;
+    }
+    if ((r = ensure(c, c->d_gop_pos, c->cap_gop_pos, size_t(nframes) + 1))) return r;
+    HIPCHK(c, hipMemcpy(c->d_gop_pos, &start_bit, sizeof(uint64_t), hipMemcpyHostToDevice));
+
+    const uint8_t* ref = nullptr;
+    size_t rs = 0;
+    for (int f = 0; f < nframes; f++) {
+        const uint8_t* cf = dy + size_t(f) * frame_pitch;
+        if (f % gop == 0) {
+            Launch L;
+            L.dy = cf;
+            L.w = w;
+            L.h = h;
+            L.stride = stride;
+            L.nframes = 1;
+            L.use_rle = use_rle;
+            L.mode = mode;
+            L.dout = dout;
+            L.start_bit = start_bit;
+            L.start_dev = c->d_gop_pos + f;
+            L.chain_end = c->d_gop_pos + f + 1;
+            if ((r = launch_chain(c, L))) return r;
+            ref = cf;
+            rs = stride;
+        } else {
+            ie::PfArgs a{};
+            a.cur = cf;
+            a.cs = stride;
+            a.ref = ref;
+            a.rs = rs;
+            a.rec = c->d_gop_rec + size_t(f & 1) * size_t(w) * h;
+            a.w = w;
+            a.h = h;
+            a.mbx = w / 16;
+            a.mby = h / 16;
+            a.bx = bx;
+            a.rle = use_rle ? 1 : 0;
+            a.merange = merange;
+            a.mv_bits = mvec_bits(merange);
+            a.tab = c->d_tab;
+            a.coef = c->d_gop_coef;
+            a.bits = c->d_gop_bits;
+            a.out = dout;
+            a.start = c->d_gop_pos + f;
+            a.end = c->d_gop_pos + f + 1;
+            ie::launch_pframe(a, n, c->d_gop_tile, c->stream);
+            HIPCHK(c, hipGetLastError());
+            ref = a.rec;
+            rs = size_t(w);
+        }
+    }
+    std::vector<uint64_t> pos(size_t(nframes) + 1);
+    HIPCHK(c, hipMemcpyAsync(pos.data(), c->d_gop_pos, pos.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    unsigned timeouts = 0;
+    if ((r = read_errors(c, &timeouts, nullptr))) return r;
+    if (timeouts) {
+        c->use_ticket = true;  // an I-frame's tiles did not run in order: redo in ticket mode
+        return ie_encode_gop(c, y, w, h, stride, frame_pitch, nframes, gop, merange, use_rle, mode, out, out_cap,
+                             start_bit, frame_bits, end_bit);
+    }
+    if (!out_dev) {
+        const size_t b0 = size_t(start_bit / 8), b1 = size_t((pos[nframes] + 7) / 8);
+        HIPCHK(c, hipMemcpy(out + b0, c->d_out + b0, b1 - b0, hipMemcpyDeviceToHost));
+    }
+    if (frame_bits)
+        for (int f = 0; f < nframes; f++) frame_bits[f] = pos[f + 1] - pos[f];
+    if (end_bit) *end_bit = pos[nframes];
+    return IE_OK;
 }
 
 int ie_encode_images(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,

@@ -207,4 +207,23 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
                           bool write, hipStream_t s);
 size_t huffman_table_rows(uint64_t nbits, uint64_t start_bit, uint64_t chunk_bits);
 
+// P-frame of a gop > 1 video (ie_pframe.hip): one launch sequence per frame, chained on the device.
+struct PfArgs {
+    const uint8_t* cur;      // the frame, rows cs apart
+    uint64_t cs;
+    const uint8_t* ref;      // the previous frame's buffer as the reference leaves it, rows rs apart
+    uint64_t rs;
+    uint8_t* rec;            // [h][w]: this frame's buffer after the P-frame pass (the next reference)
+    int w, h, mbx, mby, bx;  // macroblocks per row / column (floor), microblocks per row
+    int rle, merange, mv_bits;
+    const EncTables* tab;
+    int16_t* coef;           // [bx*by][16] quantised prediction error (natural order), 4x4 only
+    uint32_t* bits;          // [bx*by] record bits, 0 = no record
+    uint32_t* out;           // stream words (zero from the frame's first bit on)
+    const uint64_t* start;   // device: the frame's first bit
+    uint64_t* end;           // device: its end bit
+};
+void launch_pframe(const PfArgs& a, int n, uint64_t* tile_scratch, hipStream_t s);
+int pframe_tiles(int nb);    // tile_scratch entries
+
 }  // namespace ie

@@ -89,6 +89,21 @@ int ie_encode_frames(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride,
                      int nframes, int use_rle, int mode, uint8_t* out, size_t out_cap,
                      uint64_t start_bit, uint64_t* frame_bits, uint64_t* end_bit);
 
+/* Videos with P-frames (gop > 1; VideoEncoder.cpp:22-107, VideoBase.cpp:96-122, Frame.cpp:129-247):
+ * frame f is an I-frame when f % gop == 0 (its payload = ie_encode_frames'), every other frame a
+ * P-frame against the previous frame as the reference leaves it: per 16x16 macroblock a SAD pattern
+ * search within merange (Block.cpp:267-339, algo.cpp:90-139), its motion vector (bits_needed(merange)
+ * bits per component, Block.cpp:415-423), then the records of the 4x4 microblocks' coded prediction
+ * error (ImageBase.cpp:266-306) -- 8x8 blocks carry the vectors only (the reference's
+ * micro_per_macro_row is 0 there, ImageBase.cpp:271).  Replaces the frame loop of
+ * VideoEncoder.cpp:83-91 for any gop; gop = 1 equals ie_encode_frames.  Arguments as
+ * ie_encode_frames; out holds ie_gop_stream_bound() bytes.  IE_EINVAL for P-frames with W % 16 != 0
+ * and H >= 32 (the reference reads misplaced, overlapping macroblocks there, ImageBase.cpp:223-227). */
+size_t ie_gop_stream_bound(int w, int h, int n, int nframes, int merange, uint64_t start_bit);
+int ie_encode_gop(ie_ctx* ctx, const uint8_t* y, int w, int h, size_t stride, size_t frame_pitch, int nframes,
+                  int gop, int merange, int use_rle, int mode, uint8_t* out, size_t out_cap, uint64_t start_bit,
+                  uint64_t* frame_bits, uint64_t* end_bit);
+
 /* Encode nframes INDEPENDENT images in one launch (an image-server batch): image f's records
  * go to out + f*out_pitch from bit start_bit (each image carries its own header region).
  * end_bits optional [nframes].  out_pitch must be a multiple of 4 bytes. */

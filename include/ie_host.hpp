@@ -10,7 +10,8 @@
 //   dc::VideoProcessor            VideoBase.hpp:17-48       base of the video encoder / decoder
 //   algo::Huffman                 Huffman.hpp:109-142       byte Huffman post-pass (tree on the host)
 //   dc::ImageEncoder/ImageDecoder ImageEncoder.hpp, ImageDecoder.hpp
-//   dc::VideoEncoder/VideoDecoder VideoEncoder.hpp, VideoDecoder.hpp (gop = 1: I-frames only)
+//   dc::VideoEncoder/VideoDecoder VideoEncoder.hpp, VideoDecoder.hpp (the encoder takes any gop;
+//                                 the decoder reads gop = 1 streams)
 // Every block-level operation (DCT, quantisation, RLE, bit packing, the inverse) runs on the
 // GPU; there is no CPU fallback.
 #pragma once
@@ -331,6 +332,10 @@ int64_t ieh_encode_image(ie_ctx* ctx, const uint8_t* y, int w, int h, const uint
 // gop=1 video file from a YUV420 buffer (frame_count = len / (1.5 w h)).
 int64_t ieh_encode_video(ie_ctx* ctx, const uint8_t* yuv, size_t len, int w, int h, const uint16_t* q, int n,
                          int rle, int huffman, int merange, int mode, uint8_t* out, size_t cap);
+// Video file with I/P-frames: frame f is an I-frame when f % gop == 0 (VideoEncoder.cpp:22-107; the
+// P-frames' motion search + coded error through ie_encode_gop).  gop = 1: ieh_encode_video.
+int64_t ieh_encode_video_gop(ie_ctx* ctx, const uint8_t* yuv, size_t len, int w, int h, const uint16_t* q, int n,
+                             int rle, int huffman, int gop, int merange, int mode, uint8_t* out, size_t cap);
 // Decode an image file (host buffer) with block size n: pixels into out (w*h bytes).  A cap
 // below w*h returns IE_ECAP with *w / *h set, right after the header (the payload is not decoded):
 // call with cap = 0 to size the buffer.

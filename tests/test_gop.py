@@ -64,3 +64,80 @@ def test_oracle_rejects_misplaced_macroblocks():
     y = np.zeros((2, 40, 72), dtype=np.uint8)
     with pytest.raises(AssertionError):
         o.encode_gop(y, 4, q, 2, 8)
+
+
+# ------------------------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def codec():
+    from imageencoder_amd import Codec
+    return Codec(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_gpu_gop_file_matches_reference(codec, c):
+    """Whole video files (header + I/P payload) through libie_host.so -> ie_encode_gop."""
+    from imageencoder_amd import MODE_FAST
+    q = O.read_matrix(c["matrix"], 4)
+    y = np.frombuffer(O.case_input(c), dtype=np.uint8)
+    got = codec.encode_video_file(y, c["w"], c["h"], q, 4, rle=bool(c["rle"]), huffman=c["huffman"],
+                                  merange=c["merange"], mode=MODE_FAST, gop=c["gop"])
+    assert len(got) == c["size"], (len(got), c["size"])
+    assert hashlib.md5(got).hexdigest() == c["md5"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["gopP64x48x5_g3_m8", "gopM64x48x5_g2_m0", "gopP64x40x4_g4_m8"])
+def test_gpu_gop_exact_mode_and_huffman(codec, name):
+    """EXACT mode gives the same file; the Huffman pass over a P-frame payload equals the
+    oracle's (the reference's Huffman build aborts on P-frame videos, see make_golden_gop.py)."""
+    from imageencoder_amd import MODE_EXACT
+    c = next(c for c in CASES if c["name"] == name)
+    q = O.read_matrix(c["matrix"], 4)
+    raw = O.case_input(c)
+    y = np.frombuffer(raw, dtype=np.uint8)
+    got = codec.encode_video_file(y, c["w"], c["h"], q, 4, rle=bool(c["rle"]), huffman=False,
+                                  merange=c["merange"], mode=MODE_EXACT, gop=c["gop"])
+    assert hashlib.md5(got).hexdigest() == c["md5"]
+    gh = codec.encode_video_file(y, c["w"], c["h"], q, 4, rle=bool(c["rle"]), huffman=True,
+                                 merange=c["merange"], gop=c["gop"])
+    assert gh == O.load().encode_video_gop(raw, c["w"], c["h"], 4, q, rle=c["rle"], huffman=True, gop=c["gop"],
+                                           merange=c["merange"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,gen,w,h,frames,gop,merange,start", [
+    (8, "P", 64, 48, 5, 3, 8, 0),       # 8x8: motion vectors only (parity pinned by the oracle)
+    (8, "M", 72, 24, 4, 4, 16, 7),
+    (4, "P", 128, 96, 7, 4, 32, 13),    # odd start bit, device-resident frames and stream
+    (4, "U", 48, 32, 6, 2, 6, 31),
+    (4, "P", 256, 144, 9, 9, 64, 1),
+])
+def test_gpu_gop_payload_vs_oracle(codec, n, gen, w, h, frames, gop, merange, start):
+    import torch
+    from imageencoder_amd import synth
+    q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+    y = synth.frames(gen, w, h, frames, synth.DEFAULT_SEED + 31 * w + h)
+    exp, exp_end, exp_fb = O.load().encode_gop(y, n, q, gop, merange, start_bit=start)
+    codec.set_quant(q, n)
+    cap = codec.gop_stream_bound(w, h, frames, merange, start)
+    dy = torch.from_numpy(y).cuda()
+    out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    fb, end = codec.encode_gop(dy, w, h, out, gop, merange, start_bit=start, nframes=frames)
+    assert end == exp_end
+    assert list(fb) == list(exp_fb)
+    nb = (end + 7) // 8
+    assert out.cpu().numpy()[:nb].tobytes() == exp[:nb].tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_gop_rejects_misplaced_macroblocks(codec):
+    from imageencoder_amd import IEError
+    q = O.read_matrix("matrix.txt", 4)
+    codec.set_quant(q, 4)
+    y = np.zeros((2, 40, 72), dtype=np.uint8)
+    out = np.zeros(codec.gop_stream_bound(72, 40, 2, 8), dtype=np.uint8)
+    with pytest.raises(IEError):
+        codec.encode_gop(y, 72, 40, out, 2, 8, nframes=2)
+    # gop = 1 (no P-frame) stays valid at that size
+    codec.encode_gop(y, 72, 40, out, 1, 8, nframes=2)
