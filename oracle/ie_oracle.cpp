@@ -680,4 +680,84 @@ int64_t ieo_decode_image(const uint8_t* enc, size_t len, int n, uint8_t* out, si
     return int64_t(w) * h;
 }
 
+
+// Video decode with I/P-frames (VideoDecoder.cpp:28-58, Frame.cpp:47-127): an I-frame is parsed and
+// inverse-transformed as an image; a P-frame reads one motion vector per macroblock
+// (Block.cpp:481-496: bits_needed(merange)-bit signed fields), copies the previous DECODED frame's
+// block at the (clamped) vector into place, then reads a record for EVERY microblock and, with
+// motion compensation on, adds the decoded error (IDCT + 128) to the copied pixels
+// (Block.cpp:110-119).  P-frames need W and H multiples of 16 (otherwise the reference's macroblocks
+// are misplaced and its uncovered microblocks read records the encoder never wrote): -1.
+// out receives frames of Y + W*H/2 bytes of 0x80 (Frame.cpp:121-124).  Returns the byte count.
+int64_t ieo_decode_video_gop(const uint8_t* enc, size_t len, int n, int motioncomp, uint8_t* out, size_t cap,
+                             int* w_out, int* h_out, int* frames_out) {
+    if (n != 4 && n != 8) return -1;
+    std::vector<uint8_t> dec;
+    uint64_t pos = 0;
+    bool pass = false;
+    if (!huffman_decode(enc, len, dec, pos, pass)) return -3;
+    const uint8_t* src = pass ? enc : dec.data();
+    BitReader rd(src, pass ? len : dec.size());
+    rd.pos = pos;
+    Tables T(n);
+    const int nn = n * n;
+    const int qb = int(rd.get(5));
+    double qd[64];
+    for (int k = 0; k < nn; k++) qd[k] = double(rd.get(qb));
+    const int rle = int(rd.get(1));
+    const int w = int(rd.get(15)), h = int(rd.get(15));
+    const int frames = int(rd.get(15)), gop = std::max(1, int(rd.get(15))), merange = int(rd.get(15));
+    if (w_out) *w_out = w;
+    if (h_out) *h_out = h;
+    if (frames_out) *frames_out = frames;
+    if (w % n || h % n) return -1;
+    if (gop > 1 && frames > 1 && (w % kMB || h % kMB)) return -1;
+    const size_t fsz = size_t(w) * h, pitch = fsz + fsz / 2;
+    if (pitch * size_t(frames) > cap) return -2;
+    const int mv = bits_needed_ref(int16_t(merange));
+    const int bx = w / n, by = h / n, mbx = w / kMB, mby = h / kMB;
+    const size_t nb = size_t(bx) * by;
+    std::vector<double> Y(nb * nn);
+    for (int f = 0; f < frames; f++) {
+        uint8_t* o = out + size_t(f) * pitch;
+        const bool iframe = (f % gop) == 0;
+        std::memset(o, 0, fsz);
+        if (!iframe) {
+            const uint8_t* ref = out + size_t(f - 1) * pitch;
+            for (int mb = 0; mb < mbx * mby; mb++) {
+                const int mx = (mb % mbx) * kMB, my = (mb / mbx) * kMB;
+                const int vx = shift_signed16(rd.get(mv), mv), vy = shift_signed16(rd.get(mv), mv);
+                const int cx = clamp_i16(int16_t(mx + vx), 0, w - kMB), cy = clamp_i16(int16_t(my + vy), 0, h - kMB);
+                for (int y = 0; y < kMB; y++) std::memcpy(o + size_t(my + y) * w + mx, ref + size_t(cy + y) * w + cx, kMB);
+            }
+        }
+        std::fill(Y.begin(), Y.end(), 0.0);
+        for (size_t b = 0; b < nb; b++) {
+            const int bl = int(rd.get(4));
+            const int length = rle ? int(rd.get(bl)) : nn;
+            if (length > nn) return -4;
+            for (int k = 0; k < length; k++) Y[b * nn + T.zz[k]] = double(shift_signed16(rd.get(bl), bl));
+        }
+        if (iframe || motioncomp) {
+            for (size_t b = 0; b < nb; b++) {
+                double yq[64], t[64];
+                for (int k = 0; k < nn; k++) { yq[k] = Y[b * nn + k] * qd[k]; t[k] = 0.0; }
+                for (int uv = 0; uv < nn; uv++) {
+                    const double* Ruv = &T.R[size_t(uv) * nn];
+                    for (int ij = 0; ij < nn; ij++) t[ij] = t[ij] + Ruv[ij] * yq[uv];
+                }
+                uint8_t* ob = o + size_t(b / bx) * n * w + size_t(b % bx) * n;
+                for (int i = 0; i < n; i++)
+                    for (int j = 0; j < n; j++) {
+                        const double e = t[i * n + j] + double(128);
+                        uint8_t& px = ob[size_t(i) * w + j];
+                        px = uint8_t(std::clamp(iframe ? e : double(px) + e, 0.0, 255.0));
+                    }
+            }
+        }
+        std::memset(o + fsz, 0x80, fsz / 2);
+    }
+    return int64_t(pitch * size_t(frames));
+}
+
 }  // extern "C"

@@ -80,6 +80,11 @@ void ieo_byte_histogram(const uint8_t* in, size_t n, uint32_t* hist, uint64_t* f
 int64_t ieo_decode_image(const uint8_t* enc, size_t len, int n, uint8_t* out, size_t cap,
                          int* w_out, int* h_out);
 
+/* Video decode with I/P-frames (VideoDecoder.cpp:28-58, Frame.cpp:47-127, Block.cpp:441-496):
+ * frames of Y + W*H/2 bytes of 0x80.  motioncomp 0: P-frames are the copied blocks only. */
+int64_t ieo_decode_video_gop(const uint8_t* enc, size_t len, int n, int motioncomp, uint8_t* out, size_t cap,
+                             int* w_out, int* h_out, int* frames_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,6 +39,17 @@ def ref_video(binary: str, raw: bytes, w: int, h: int, rle: int, matrix: str, go
         return open(os.path.join(d, "out.enc"), "rb").read()
 
 
+def ref_video_decode(enc: bytes, mc: int) -> bytes:
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "e.enc"), "wb").write(enc)
+        keys = dict(rawfile="in.raw", encfile="e.enc", decfile="o.dec", width=0, height=0, rle=1,
+                    quantfile="m.txt", logfile="", motioncompensation=mc)
+        open(os.path.join(d, "c.conf"), "w").write("".join(f"{k}={v}\n" for k, v in keys.items()))
+        G.run([os.path.join(G.REF, "decoder"), "c.conf"], d)
+        return open(os.path.join(d, "o.dec"), "rb").read()
+
+
 def cases():
     S = synth.DEFAULT_SEED
     out = []
@@ -86,6 +97,12 @@ def main():
             fn = c["name"] + ".enc"
             open(os.path.join(HERE, fn), "wb").write(enc)
             entry["file"] = fn
+        # the reference's video decoder (VideoDecoder.cpp / Frame::loadFromStream), motion
+        # compensation on and off, where its P-frames are well-formed (W, H multiples of 16)
+        if c["w"] % 16 == 0 and c["h"] % 16 == 0:
+            for mc in (1, 0):
+                dec = ref_video_decode(enc, mc)
+                entry[f"dec{mc}_size"], entry[f"dec{mc}_md5"] = len(dec), G.md5(dec)
         manifest.append(entry)
         print(f"{c['name']:28s} {len(enc):9d} B  {entry['md5'][:12]}", flush=True)
     json.dump(manifest, open(os.path.join(HERE, "manifest_gop.json"), "w"), indent=1)

@@ -47,6 +47,9 @@ class Oracle:
         L.ieo_encode_gop.argtypes = [_u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, _u16p,
                                      C.c_int, C.c_int, C.c_int, _u8p, C.c_size_t, C.c_uint64, _u64p]
         L.ieo_encode_gop.restype = C.c_int64
+        L.ieo_decode_video_gop.argtypes = [_u8p, C.c_size_t, C.c_int, C.c_int, _u8p, C.c_size_t, C.POINTER(C.c_int),
+                                           C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.ieo_decode_video_gop.restype = C.c_int64
         L.ieo_huffman_encode.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t]
         L.ieo_huffman_encode.restype = C.c_int64
         L.ieo_huffman_decode.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t, C.POINTER(C.c_int)]
@@ -149,6 +152,17 @@ class Oracle:
                                       self._p(out), out.size, start_bit, fb.ctypes.data_as(_u64p))
         assert end >= 0, end
         return out, int(end), fb
+
+    def decode_video_gop(self, enc: bytes, n: int, motioncomp: bool = True) -> bytes:
+        """A video file (any gop) decoded as the reference's VideoDecoder writes it."""
+        src = np.frombuffer(enc, dtype=np.uint8).copy()
+        w, h, f = C.c_int(0), C.c_int(0), C.c_int(0)
+        cap = 64 << 20
+        out = np.zeros(cap, dtype=np.uint8)
+        r = self.lib.ieo_decode_video_gop(self._p(src), src.size, n, int(motioncomp), self._p(out), cap,
+                                          C.byref(w), C.byref(h), C.byref(f))
+        assert r >= 0, r
+        return out[:r].tobytes()
 
     def huffman_encode(self, data: bytes) -> bytes:
         a = np.frombuffer(data, dtype=np.uint8)

@@ -41,6 +41,18 @@ def test_oracle_matches_reference_gop(c):
         assert enc == exp
 
 
+DEC = [c for c in CASES if "dec1_md5" in c]
+
+
+@pytest.mark.parametrize("c", DEC, ids=[c["name"] for c in DEC])
+@pytest.mark.parametrize("mc", [1, 0])
+def test_oracle_video_decode_matches_reference(c, mc):
+    """The reference's VideoDecoder (Frame::loadFromStream, motion compensation on / off)."""
+    dec = O.load().decode_video_gop(O.case_expected(c), 4, bool(mc))
+    assert len(dec) == c[f"dec{mc}_size"]
+    assert hashlib.md5(dec).hexdigest() == c[f"dec{mc}_md5"]
+
+
 def test_oracle_gop_payload_matches_file():
     """The payload entry (ieo_encode_gop) continues the header exactly as the file writer does."""
     o = O.load()
