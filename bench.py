@@ -74,6 +74,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-iters", type=int, default=2)
     p.add_argument("--no-decode", action="store_true", help="skip the one-image decode timing (inverse path)")
+    p.add_argument("--no-gop", action="store_true", help="skip the P-frame video timing (gop > 1)")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) timing")
     p.add_argument("--no-check", action="store_true", help="skip the output self-check")
     p.add_argument("--batch", type=int, default=None, help="frames per launch (default: the workload's)")
@@ -412,6 +413,30 @@ def main():
                                          "path": f"exact parse: {chunks} chunk transfer tables composed in "
                                                  f"{groups} level(s), then count and decode launches; "
                                                  "one host sync at the end (device-resident stream and pixels)"}
+        if n == 4 and not cfg["huffman"] and not args.no_gop:
+            # P-frames: 8 resident frames as one video, gop = 1 against gop = 8
+            # (one I-frame + 7 P-frames: macroblock search + coded error + reconstruction), merange 16
+            F, mer = 8, 16
+            vf = frames[:F]
+            vcap = codec.gop_stream_bound(w, h, F, mer, 0)
+            vout = torch.zeros(vcap, dtype=torch.uint8, device=dev)
+            tv = {}
+            for gop in (1, F):
+                codec.encode_gop(vf, w, h, vout, gop, mer, nframes=F, mode=mode)
+                torch.cuda.synchronize(dev)
+                kv = 5
+                t0 = time.perf_counter()
+                for _ in range(kv):
+                    vout.zero_()
+                    codec.encode_gop(vf, w, h, vout, gop, mer, nframes=F, mode=mode)
+                torch.cuda.synchronize(dev)
+                tv[gop] = (time.perf_counter() - t0) / kv
+            tp = max(tv[F] - tv[1] / F, 0.0) / (F - 1)
+            extra["video_gop"] = {"frames": F, "gop": F, "merange": mer, "ms_gop1": round(tv[1] * 1e3, 3),
+                                  "ms_gop": round(tv[F] * 1e3, 3), "us_per_pframe": round(tp * 1e6, 1),
+                                  "pframe_Mpx_s": round(w * h / tp / 1e6, 1) if tp else None,
+                                  "note": "ie_encode_gop, device-resident frames and stream, one host sync per "
+                                          "call (stream zeroing included)"}
         workload = (f"{wl}: {w}x{h} {n}x{n} {cfg['matrix']} RLE"
                     f"{' +Huffman' if cfg['huffman'] else ''}, batch of {B} independent images per step, "
                     f"{R} distinct resident frames per GPU ({R * w * h / 2**20:.0f} MiB)")

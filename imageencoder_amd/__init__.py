@@ -63,6 +63,8 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.ie_stream_bound.restype = C.c_size_t
     L.ie_encode_frames.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                    u8p, C.c_size_t, C.c_uint64, u64p, u64p]
+    L.ie_decode_gop.argtypes = [vp, u8p, C.c_size_t, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                C.c_int, u8p, C.c_size_t, C.c_size_t, u64p]
     L.ie_gop_stream_bound.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
     L.ie_gop_stream_bound.restype = C.c_size_t
     L.ie_encode_gop.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
@@ -350,6 +352,18 @@ class Codec:
                                        mode, _ptr(out), _nbytes(out), start_bit,
                                        fb.ctypes.data_as(C.POINTER(C.c_uint64)), C.pointer(end)))
         return fb, int(end.value)
+
+    def decode_gop(self, stream, w: int, h: int, out, gop: int, merange: int, nframes: int, start_bit: int = 0,
+                   length: int | None = None, stride: int | None = None, frame_pitch: int | None = None,
+                   rle: bool = True, motioncomp: bool = True) -> int:
+        """Decode an I/P-frame payload (VideoDecoder / Frame::loadFromStream) into ``out``; the end bit."""
+        stride = w if stride is None else stride
+        frame_pitch = stride * h if frame_pitch is None else frame_pitch
+        end = C.c_uint64(0)
+        self._chk(self.L.ie_decode_gop(self.h, _ptr(stream), _nbytes(stream) if length is None else length, start_bit,
+                                       w, h, nframes, gop, merange, int(rle), int(motioncomp), _ptr(out), stride,
+                                       frame_pitch, C.pointer(end)))
+        return int(end.value)
 
     def encode_images(self, y, w: int, h: int, out, out_pitch: int, nframes: int, start_bit: int = 0,
                       stride: int | None = None, frame_pitch: int | None = None, rle: bool = True,

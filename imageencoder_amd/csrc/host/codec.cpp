@@ -241,7 +241,7 @@ static bool parse_header(const uint8_t* src, size_t len, size_t start, int n, bo
 // cap: the caller's pixel capacity -- a smaller one returns IE_ECAP right after the header (sh
 // filled in), before the payload is decoded
 static int decode_file(ie_ctx* c, const uint8_t* enc, size_t len, int n, bool video, StreamHeader& sh,
-                       std::vector<uint8_t>& pix, std::string& err, size_t cap = SIZE_MAX) {
+                       std::vector<uint8_t>& pix, std::string& err, size_t cap = SIZE_MAX, bool motioncomp = true) {
     if (!c) return (err = "no GPU context", IE_EHIP);
     std::vector<uint8_t> dec;
     bool pass = false;
@@ -251,8 +251,6 @@ static int decode_file(ie_ctx* c, const uint8_t* enc, size_t len, int n, bool vi
     const uint8_t* src = pass ? enc : dec.data();
     const size_t srclen = pass ? len : dec.size();
     if (!parse_header(src, srclen, start, n, video, sh)) return (err = "stream shorter than its header", IE_EFORMAT);
-    if (video && sh.gop != 1)
-        return (err = "P-frames (gop > 1) are not supported: only gop = 1 streams decode", IE_EINVAL);
     int r;
     if ((r = ie_set_quant(c, sh.q.data(), n))) return (err = ie_last_error(c), r);
     const size_t fbytes = size_t(sh.w) * sh.h;
@@ -260,6 +258,12 @@ static int decode_file(ie_ctx* c, const uint8_t* enc, size_t len, int n, bool vi
     if (pitch * size_t(sh.frames) > cap) return IE_ECAP;
     pix.assign(pitch * size_t(sh.frames), video ? 0x80 : 0);  // UV fill (Frame.cpp:121-124)
     if (!fbytes || !sh.frames) return IE_OK;
+    if (video && sh.gop > 1) {  // P-frames: frame by frame (Frame::loadFromStream, Frame.cpp:47-127)
+        if ((r = ie_decode_gop(c, src, srclen, sh.payload_bit, sh.w, sh.h, sh.frames, sh.gop, sh.merange, sh.rle,
+                               motioncomp ? 1 : 0, pix.data(), size_t(sh.w), pitch, nullptr)))
+            return (err = ie_last_error(c), r);
+        return IE_OK;
+    }
     if ((r = ie_decode_frames(c, src, srclen, sh.payload_bit, sh.w, sh.h, sh.frames, sh.rle, pix.data(), size_t(sh.w),
                               pitch, nullptr)))
         return (err = ie_last_error(c), r);
@@ -392,7 +396,8 @@ bool VideoDecoder::process() {
     if (!err_.empty()) return false;
     util::Logger::WriteLn("[VideoDecoder] Processing video...");
     StreamHeader sh;
-    if (decode_file(Device::get(), raw.data(), raw.size(), n_, true, sh, result_, err_) != IE_OK) return false;
+    if (decode_file(Device::get(), raw.data(), raw.size(), n_, true, sh, result_, err_, SIZE_MAX, motioncomp) != IE_OK)
+        return false;
     width = uint16_t(sh.w);
     height = uint16_t(sh.h);
     gop = uint16_t(sh.gop);

@@ -2120,9 +2120,12 @@ int finish_decode(ie_ctx* c, uint8_t* out, const uint8_t* dpix, bool out_dev, in
 
 extern "C" {
 
-int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,
-                     int use_rle, uint8_t* out, size_t stride, size_t frame_pitch, uint64_t* end_bit) {
-    if (!c || !in || !out) return IE_EINVAL;
+}  // extern "C"
+
+namespace {
+// add_base: P-frame error -- the decoded error is added to the pixels already in `out`
+int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,
+                       int use_rle, uint8_t* out, size_t stride, size_t frame_pitch, uint64_t* end_bit, int add_base) {
     int r = check_dims(c, w, h, nframes);
     if (r) return r;
     if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
@@ -2181,6 +2184,7 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
         dpix = c->d_pix;
     }
     ie::DecArgs da{};
+    da.add_base = add_base;
     da.nframes = nframes;
     da.bx = w / n;
     da.by = h / n;
@@ -2234,6 +2238,84 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
 #endif
     if (hm[2] < nblocks || end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
     return finish_decode(c, out, dpix, out_dev, nframes, w, h, stride, frame_pitch, end, end_bit);
+}
+}  // namespace
+
+extern "C" {
+
+int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,
+                     int use_rle, uint8_t* out, size_t stride, size_t frame_pitch, uint64_t* end_bit) {
+    if (!c || !in || !out) return IE_EINVAL;
+    return decode_frames_impl(c, in, len, start_bit, w, h, nframes, use_rle, out, stride, frame_pitch, end_bit, 0);
+}
+
+// Video decode with P-frames (VideoDecoder.cpp:28-58, Frame.cpp:47-127): frame by frame, each
+// starting at the previous frame's end; a P-frame's motion vectors and reference-block copies
+// (pf_mvcopy_kernel), then its records (every microblock's) decoded onto the copied pixels.
+int ie_decode_gop(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes, int gop,
+                  int merange, int use_rle, int motioncomp, uint8_t* out, size_t stride, size_t frame_pitch,
+                  uint64_t* end_bit) {
+    if (!c || !in || !out) return IE_EINVAL;
+    int r = check_dims(c, w, h, nframes);
+    if (r) return r;
+    gop = std::max(1, gop);
+    if (merange < 0 || merange > 32767) return fail(c, IE_EINVAL, "merange must be in [0, 32767]");
+    if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
+    if (nframes > 1 && frame_pitch < stride * size_t(h - 1) + size_t(w))
+        return fail(c, IE_EINVAL, "frame_pitch smaller than a frame");
+    if (gop > 1 && nframes > 1 && (w % 16 || h % 16))
+        return fail(c, IE_EINVAL, "P-frames decode for W and H multiples of 16 only: the reference's macroblocks are "
+                                  "misplaced otherwise and its uncovered microblocks read records never written");
+    if (start_bit > uint64_t(len) * 8) return fail(c, IE_EINVAL, "start_bit beyond the stream");
+    HIPCHK(c, hipSetDevice(c->device));
+    // the stream once on the device (zero padding for the vector reads), the frames decoded into
+    // a device buffer (P-frames read their predecessor there)
+    const size_t padded = len + 16;
+    if ((r = ensure(c, c->d_in, c->cap_in, padded))) return r;
+    HIPCHK(c, hipMemsetAsync(c->d_in + len, 0, 16, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_in, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                             c->stream));
+    const bool out_dev = is_device_ptr(out);
+    const size_t pix_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
+    uint8_t* dpix = out;
+    if (!out_dev) {
+        if ((r = ensure(c, c->d_gop_rec, c->cap_gop_rec, pix_bytes))) return r;
+        dpix = c->d_gop_rec;
+    }
+    const int n = c->n, mv = mvec_bits(merange);
+    const uint64_t nmb = uint64_t(w / 16) * (h / 16);
+    const uint64_t rec_bound = uint64_t(w / n) * (h / n) * bound_bits_per_block(n);
+    uint64_t pos = start_bit;
+    for (int f = 0; f < nframes; f++) {
+        uint8_t* fo = dpix + size_t(f) * frame_pitch;
+        const bool iframe = (f % gop) == 0;
+        if (!iframe) {
+            if (pos + nmb * 2u * uint64_t(mv) > uint64_t(len) * 8) return fail(c, IE_EFORMAT, "stream ends in the motion vectors");
+            ie::launch_pframe_mvcopy(c->d_in, pos, mv, fo - frame_pitch, stride, fo, stride, w, h, c->stream);
+            HIPCHK(c, hipGetLastError());
+            pos += nmb * 2u * uint64_t(mv);
+        }
+        // the records from the byte holding pos, at most this frame's bound of the stream
+        const size_t b0 = size_t(pos / 8);
+        const size_t flen = size_t(std::min<uint64_t>(uint64_t(len) - b0, (pos % 8 + rec_bound + 7) / 8 + 8));
+        uint64_t e = 0;
+        if (!iframe && !motioncomp) {
+            // the error is read (the stream must be consumed) but not applied: decode into scratch
+            if ((r = ensure(c, c->d_gop_coef, c->cap_gop_coef, (stride * size_t(h) + 1) / 2))) return r;
+            r = decode_frames_impl(c, c->d_in + b0, flen, pos % 8, w, h, 1, use_rle,
+                                   reinterpret_cast<uint8_t*>(c->d_gop_coef), stride, 0, &e, 0);
+        } else {
+            r = decode_frames_impl(c, c->d_in + b0, flen, pos % 8, w, h, 1, use_rle, fo, stride, 0, &e, iframe ? 0 : 1);
+        }
+        if (r) return r;
+        pos = uint64_t(b0) * 8 + e;
+    }
+    if (!out_dev)
+        for (int f = 0; f < nframes; f++)
+            HIPCHK(c, hipMemcpy2D(out + size_t(f) * frame_pitch, stride, dpix + size_t(f) * frame_pitch, stride,
+                                  size_t(w), size_t(h), hipMemcpyDeviceToHost));
+    if (end_bit) *end_bit = pos;
+    return IE_OK;
 }
 
 }  // extern "C"

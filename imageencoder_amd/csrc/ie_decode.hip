@@ -298,6 +298,7 @@ __device__ __forceinline__ uint32_t decode_record(const uint32_t* L, uint32_t p,
 #pragma unroll
         for (int j = 0; j < N; j++) {
             double x = t[i * N + j] + 128.0;
+            if (a.add_base) x = double(o[uint64_t(i) * a.stride + j]) + x;  // expandDifferences
             x = x < 0.0 ? 0.0 : (x > 255.0 ? 255.0 : x);
             const uint32_t b = uint32_t(uint8_t(x));
             if (j % 4 == 0) wv[j / 4] = b;

@@ -147,6 +147,7 @@ void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uin
 
 struct DecArgs {
     int nframes, bx, by, rle;
+    int add_base;            // P-frames: pixel = clamp(pixel already in out + (IDCT + 128)) (Block.cpp:110-119)
     uint8_t* out;
     uint64_t stride, frame_pitch;
     const EncTables* tab;
@@ -224,6 +225,11 @@ struct PfArgs {
     uint64_t* end;           // device: its end bit
 };
 void launch_pframe(const PfArgs& a, int n, uint64_t* tile_scratch, hipStream_t s);
+// P-frame decode, first half (Block.cpp:481-496): every macroblock's motion vector read from the
+// stream words (big-endian bytes) at start_bit, the previous decoded frame's block at the clamped
+// vector copied into place
+void launch_pframe_mvcopy(const uint8_t* stream, uint64_t start_bit, int mv_bits, const uint8_t* ref, uint64_t rs,
+                          uint8_t* out, uint64_t os, int w, int h, hipStream_t s);
 int pframe_tiles(int nb);    // tile_scratch entries
 
 }  // namespace ie

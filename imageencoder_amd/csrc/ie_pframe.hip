@@ -7,11 +7,11 @@
 // the decoded error added back (Frame.cpp:220-242, Block.cpp:110-128).  The payload is the
 // macroblocks' motion vectors followed by the covered microblocks' records in raster order.
 //
-// Layout of the work: one 256-thread workgroup per macroblock, one thread per pixel for the search
-// (the nine candidates of a pattern level are summed together: nine wave reductions, one LDS
-// exchange, every thread then picks the winner in the reference's order -- `<=`, later candidates
-// win ties), one thread per coefficient for the DCT and one per pixel for the inverse, the 4x4
-// microblocks' error staged in LDS as FP64.  The FP64 arithmetic is the reference's operation
+// Layout of the work: one wave per macroblock, four pixels per lane (a candidate's partial SAD is
+// one v_sad_u8; the nine candidates of a pattern level are reduced across the wave together and
+// every lane applies the reference's rule -- `<=`, later candidates win ties -- so the search needs
+// no LDS and no barrier), four coefficients per lane for the DCT and four pixels for the inverse,
+// the 4x4 microblocks' error and the FP64 transform rows staged in LDS.  The FP64 arithmetic is the reference's operation
 // order (compiled with -ffp-contract=off).  The frame's first bit lives on the device (the
 // previous frame's end), so consecutive frames chain without a host round trip; the records are
 // placed by a two-level scan of their lengths and ORed into the zeroed stream.
@@ -23,7 +23,8 @@ namespace ie {
 namespace {
 
 constexpr int kMB = 16;
-constexpr int kPfTileBlocks = 2048;  // record-length tile of the scan: 256 threads x 8 blocks
+constexpr int kPfPer = 2;                      // records per emitting thread
+constexpr int kPfTileBlocks = kTPB * kPfPer;  // record-length tile of the scan
 __constant__ int kSx[9] = {0, 1, 1, 0, -1, -1, -1, 0, 1};  // algo.cpp:90-100
 __constant__ int kSy[9] = {0, 0, 1, 1, 1, 0, -1, -1, -1};
 __constant__ int kZz4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};  // algo.cpp:68-87
@@ -87,17 +88,36 @@ __device__ __forceinline__ uint32_t rec_len(uint32_t s, int rle) {
     return 4u + (rle ? bl : 0u) + bl * lw;
 }
 
+// four horizontally adjacent pixels packed little-endian (byte j = pixel j), any alignment
+__device__ __forceinline__ uint32_t load4(const uint8_t* p) {
+    return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+}
+
+// One WAVE per macroblock (a 64-thread workgroup: its barriers cost nothing): lane l holds pixel row
+// l/4, columns 4(l%4)..+3 of the macroblock, whose SAD against a candidate is one v_sad_u8.
+constexpr int kMbTPB = 64;
+
 template <int N>
-__global__ __launch_bounds__(kTPB) void pf_macroblock_kernel(PfArgs a) {
-    __shared__ uint32_t red[4][9];
+__global__ __launch_bounds__(kMbTPB) void pf_macroblock_kernel(PfArgs a) {
     __shared__ double xs[256];
+    __shared__ double Ps[256], Rs[256], qs[16], Ss[16];
     __shared__ int16_t cq[256];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int l = threadIdx.x;
     const int mb = blockIdx.x;
     const int mx = (mb % a.mbx) * kMB, my = (mb / a.mbx) * kMB;
-    const int py = t >> 4, px = t & 15;
+    const int py = l >> 2, px = (l & 3) * 4;
     const int W16 = a.w - kMB, H16 = a.h - kMB;
-    const int c = a.cur[size_t(my + py) * a.cs + mx + px];
+    const uint32_t c4 = load4(a.cur + size_t(my + py) * a.cs + mx + px);
+    if constexpr (N == 4) {  // the FP64 rows of the forward and inverse transforms (EncTables)
+        for (int i = l; i < 256; i += kMbTPB) {
+            Ps[i] = a.tab->P[i];
+            Rs[i] = a.tab->R[i];
+        }
+        if (l < 16) {
+            qs[l] = a.tab->qd[l];
+            Ss[l] = a.tab->S[l];
+        }
+    }
 
     // ---- search (Block.cpp:272-329): the first best block is the one at ABSOLUTE (0, 0)
     int cx = 0, cy = 0, r = a.merange / 2;
@@ -110,30 +130,27 @@ __global__ __launch_bounds__(kTPB) void pf_macroblock_kernel(PfArgs a) {
         for (int p = 0; p < 9; p++) {
             qx[p] = clamp16(cx + kSx[p] * r + mx, W16);
             qy[p] = clamp16(cy + kSy[p] * r + my, H16);
-            d[p] = uint32_t(abs(c - int(a.ref[size_t(qy[p] + py) * a.rs + qx[p] + px])));
+            d[p] = __builtin_amdgcn_sad_u8(c4, load4(a.ref + size_t(qy[p] + py) * a.rs + qx[p] + px), 0u);
         }
 #pragma unroll
         for (int p = 0; p < 9; p++) {
             uint32_t v = d[p];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-            if (lane == 0) red[wv][p] = v;
+            d[p] = v;  // every lane holds the candidate's SAD
         }
-        __syncthreads();
         int np = -1, nbx = 0, nby = 0;
         uint32_t nd = best;
 #pragma unroll
         for (int p = 0; p < 9; p++) {
             if (p > 0 && qx[p] == mx && qy[p] == my) continue;  // Block.cpp:297-301
-            const uint32_t s = red[0][p] + red[1][p] + red[2][p] + red[3][p];
-            if (s <= nd) {
+            if (d[p] <= nd) {
                 np = p;
-                nd = s;
+                nd = d[p];
                 nbx = qx[p];
                 nby = qy[p];
             }
         }
-        __syncthreads();  // red is rewritten by the next level
         if (np < 0) break;
         cx += kSx[np] * r;
         cy += kSy[np] * r;
@@ -144,7 +161,7 @@ __global__ __launch_bounds__(kTPB) void pf_macroblock_kernel(PfArgs a) {
     }
     // the reference block at the motion vector (getCoordAfterMotion, Frame.cpp:221-224)
     const int ccx = clamp16(mx + cx, W16), ccy = clamp16(my + cy, H16);
-    if (t == 0) {
+    if (l == 0) {
         BitOr o(a.out, *a.start + uint64_t(mb) * 2u * uint32_t(a.mv_bits));  // streamMVec (Block.cpp:415-423)
         o.put(a.mv_bits, uint32_t(int32_t(int16_t(cx))));
         o.put(a.mv_bits, uint32_t(int32_t(int16_t(cy))));
@@ -153,54 +170,83 @@ __global__ __launch_bounds__(kTPB) void pf_macroblock_kernel(PfArgs a) {
     if constexpr (N != 4) {
         // micro_per_macro_row is 0 for 8x8 blocks (ImageBase.cpp:271): no error is coded and
         // expandDifferences adds the frame's own pixels to the copied reference block
-        const int base = a.ref[size_t(ccy + py) * a.rs + ccx + px];
-        a.rec[size_t(my + py) * a.w + mx + px] = uint8_t(min(base + c, 255));
+        const uint32_t b4 = load4(a.ref + size_t(ccy + py) * a.rs + ccx + px);
+        uint8_t* o = a.rec + size_t(my + py) * a.w + mx + px;
+#pragma unroll
+        for (int j = 0; j < 4; j++) o[j] = uint8_t(min(int((b4 >> (8 * j)) & 255u) + int((c4 >> (8 * j)) & 255u), 255));
         return;
     } else {
-        const EncTables* T = a.tab;
-        // ---- prediction error, microblock mi = (py/4, px/4), element k (expandDifferenceWith)
-        const int rb = a.ref[size_t(bby + py) * a.rs + bbx + px];
-        const int mi = (py >> 2) * 4 + (px >> 2);
-        xs[mi * 16 + (py & 3) * 4 + (px & 3)] = (double(c) - double(rb)) + double(-128);
-        __syncthreads();
-        // ---- forward DCT + quantiser, thread = (microblock t/16, coefficient t%16) (Block.cpp:139-153)
-        {
-            const int m = t >> 4, uv = t & 15;
-            const double* P = T->P + uv * 16;
-            const double* x = xs + m * 16;
-            double acc = 0.0;
+        // ---- prediction error (expandDifferenceWith): the lane's row of microblock
+        // (py/4, l%4), element row py%4
+        const uint32_t r4 = load4(a.ref + size_t(bby + py) * a.rs + bbx + px);
+        const int mi = (py >> 2) * 4 + (l & 3);
 #pragma unroll
-            for (int k = 0; k < 16; k++) acc = acc + P[k] * x[k];
-            const double D = acc * T->S[uv];
-            cq[t] = int16_t(round(D / T->qd[uv]));
+        for (int j = 0; j < 4; j++)
+            xs[mi * 16 + (py & 3) * 4 + j] =
+                (double(int((c4 >> (8 * j)) & 255u)) - double(int((r4 >> (8 * j)) & 255u))) + double(-128);
+        __syncthreads();
+        // ---- forward DCT + quantiser (Block.cpp:139-153): lane = (microblock l/4, coefficients
+        // 4(l%4)..+3), each in the reference's k order
+        const int m = l >> 2, g = (l & 3) * 4;
+        {
+            const double* x = xs + m * 16;
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const double xk = x[k];
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[j] = acc[j] + Ps[(g + j) * 16 + k] * xk;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) cq[m * 16 + g + j] = int16_t(round((acc[j] * Ss[g + j]) / qs[g + j]));
         }
         __syncthreads();
-        const int m = t >> 4, e = t & 15;
         const int gb = (my / 4 + (m >> 2)) * a.bx + (mx / 4 + (m & 3));
-        a.coef[size_t(gb) * 16 + e] = cq[t];
-        if (e == 0) a.bits[gb] = rec_len(size4(cq + m * 16, a.rle), a.rle);
-        // ---- inverse (Block.cpp:162-177), thread = (microblock t/16, pixel t%16), then
-        // expandDifferences over the copied reference block (Block.cpp:110-119)
-        double tt = 0.0;
 #pragma unroll
-        for (int uv = 0; uv < 16; uv++) tt = tt + T->R[uv * 16 + e] * (double(cq[m * 16 + uv]) * T->qd[uv]);
-        const double ex = tt + double(128);
-        const int ppy = (m >> 2) * 4 + (e >> 2), ppx = (m & 3) * 4 + (e & 3);
-        const double v = double(a.ref[size_t(ccy + ppy) * a.rs + ccx + ppx]) + ex;
-        a.rec[size_t(my + ppy) * a.w + mx + ppx] = uint8_t(v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v));
+        for (int j = 0; j < 4; j++) a.coef[size_t(gb) * 16 + g + j] = cq[m * 16 + g + j];
+        if (g == 0) a.bits[gb] = rec_len(size4(cq + m * 16, a.rle), a.rle);
+        // ---- inverse (Block.cpp:162-177): lane = (microblock l/4, pixel row l%4), uv ascending;
+        // then expandDifferences over the copied reference block (Block.cpp:110-119)
+        double tt[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int uv = 0; uv < 16; uv++) {
+            const double yv = double(cq[m * 16 + uv]) * qs[uv];
+#pragma unroll
+            for (int j = 0; j < 4; j++) tt[j] = tt[j] + Rs[uv * 16 + g + j] * yv;
+        }
+        const int ppy = (m >> 2) * 4 + (l & 3), ppx = (m & 3) * 4;
+        const uint32_t b4 = load4(a.ref + size_t(ccy + ppy) * a.rs + ccx + ppx);
+        uint8_t* o = a.rec + size_t(my + ppy) * a.w + mx + ppx;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const double v = double(int((b4 >> (8 * j)) & 255u)) + (tt[j] + double(128));
+            o[j] = uint8_t(v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v));
+        }
     }
 }
 
-// Pixels no macroblock covers (the right / bottom strips when W or H is not a multiple of 16):
-// their microblocks keep the frame's own pixels as "error" and have no record, so
-// expandDifferences doubles them (Block.cpp:52-55,110-119).
-__global__ __launch_bounds__(kTPB) void pf_strip_kernel(PfArgs a) {
+// Pixels no macroblock covers (the bottom strip, rows [16*mby, h), then the right strip of the
+// covered rows, columns [16*mbx, w)): their microblocks keep the frame's own pixels as "error" and
+// have no record (bits = 0, written here for 4x4 blocks), so expandDifferences doubles them
+// (Block.cpp:52-55,110-119).
+__global__ __launch_bounds__(kTPB) void pf_strip_kernel(PfArgs a, int n) {
     const size_t i = size_t(blockIdx.x) * kTPB + threadIdx.x;
-    if (i >= size_t(a.w) * a.h) return;
-    const int x = int(i % size_t(a.w)), y = int(i / size_t(a.w));
-    if (x < a.mbx * kMB && y < a.mby * kMB) return;
+    const int hc = a.mby * kMB, wc = a.mbx * kMB;
+    const size_t nbot = size_t(a.h - hc) * a.w, nright = size_t(hc) * (a.w - wc);
+    if (i >= nbot + nright) return;
+    int x, y;
+    if (i < nbot) {
+        y = hc + int(i / size_t(a.w));
+        x = int(i % size_t(a.w));
+    } else {
+        const size_t j = i - nbot;
+        const int rw = a.w - wc;
+        y = int(j / size_t(rw));
+        x = wc + int(j % size_t(rw));
+    }
     const int c = a.cur[size_t(y) * a.cs + x];
-    a.rec[i] = uint8_t(min(2 * c, 255));
+    a.rec[size_t(y) * a.w + x] = uint8_t(min(2 * c, 255));
+    if (n == 4 && (x & 3) == 0 && (y & 3) == 0) a.bits[size_t(y / 4) * a.bx + x / 4] = 0u;
 }
 
 // block-wide exclusive scan of one value per thread; returns the total in *tot
@@ -227,9 +273,9 @@ __device__ __forceinline__ uint64_t block_exscan(uint64_t v, uint64_t* sh, uint6
 
 __global__ __launch_bounds__(kTPB) void pf_tile_sum_kernel(const uint32_t* bits, int nb, uint64_t* tsum) {
     __shared__ uint64_t sh[kTPB / 64];
-    const int b0 = blockIdx.x * kPfTileBlocks + threadIdx.x * 8;
+    const int b0 = blockIdx.x * kPfTileBlocks + threadIdx.x * kPfPer;
     uint64_t s = 0;
-    for (int k = 0; k < 8; k++)
+    for (int k = 0; k < kPfPer; k++)
         if (b0 + k < nb) s += bits[b0 + k];
     uint64_t tot;
     block_exscan(s, sh, &tot);
@@ -254,15 +300,15 @@ __global__ __launch_bounds__(kTPB) void pf_tile_scan_kernel(uint64_t* tsum, int 
 
 __global__ __launch_bounds__(kTPB) void pf_emit_kernel(PfArgs a, int nb, const uint64_t* tpre, uint64_t head_bits) {
     __shared__ uint64_t sh[kTPB / 64];
-    const int b0 = blockIdx.x * kPfTileBlocks + threadIdx.x * 8;
+    const int b0 = blockIdx.x * kPfTileBlocks + threadIdx.x * kPfPer;
     uint64_t s = 0;
-    for (int k = 0; k < 8; k++)
+    for (int k = 0; k < kPfPer; k++)
         if (b0 + k < nb) s += a.bits[b0 + k];
     uint64_t tot;
     const uint64_t ex = block_exscan(s, sh, &tot);
     if (s == 0) return;
     BitOr o(a.out, *a.start + head_bits + tpre[blockIdx.x] + ex);
-    for (int k = 0; k < 8 && b0 + k < nb; k++) {
+    for (int k = 0; k < kPfPer && b0 + k < nb; k++) {
         if (!a.bits[b0 + k]) continue;  // no macroblock covered it: no record (Block.cpp:373-375)
         const int16_t* c = a.coef + size_t(b0 + k) * 16;
         const uint32_t sz = size4(c, a.rle);
@@ -279,7 +325,38 @@ __global__ void pf_end_kernel(const uint64_t* start, uint64_t* end, uint64_t hea
     if (threadIdx.x == 0) *end = *start + head_bits;
 }
 
+// P-frame decode, first half: lane l copies row l/4, pixels 4(l%4)..+3 of the reference block
+__global__ __launch_bounds__(kMbTPB) void pf_mvcopy_kernel(const uint8_t* in, uint64_t start_bit, int mv,
+                                                           const uint8_t* ref, uint64_t rs, uint8_t* out, uint64_t os,
+                                                           int w, int h, int mbx) {
+    const int l = threadIdx.x, mb = blockIdx.x;
+    const int mx = (mb % mbx) * kMB, my = (mb / mbx) * kMB;
+    const uint64_t p = start_bit + uint64_t(mb) * 2u * uint32_t(mv);
+    uint64_t win = 0;  // 64 stream bits from byte p/8 (2*mv <= 32 bits + 7 bits of offset)
+#pragma unroll
+    for (int k = 0; k < 8; k++) win = (win << 8) | in[(p >> 3) + k];
+    const uint32_t s = uint32_t(p & 7u);
+    const uint32_t rx = uint32_t(win >> (64 - s - uint32_t(mv))) & ((1u << mv) - 1u);
+    const uint32_t ry = uint32_t(win >> (64 - s - 2u * uint32_t(mv))) & ((1u << mv) - 1u);
+    const int vx = int(int16_t(uint16_t(rx << (16 - mv))) >> (16 - mv));  // shift_signed (utils.hpp:265-269)
+    const int vy = int(int16_t(uint16_t(ry << (16 - mv))) >> (16 - mv));
+    const int cx = clamp16(mx + vx, w - kMB), cy = clamp16(my + vy, h - kMB);
+    const int py = l >> 2, px = (l & 3) * 4;
+    const uint8_t* sp = ref + size_t(cy + py) * rs + cx + px;
+    uint8_t* dp = out + size_t(my + py) * os + mx + px;
+#pragma unroll
+    for (int j = 0; j < 4; j++) dp[j] = sp[j];
+}
+
 }  // namespace
+
+void launch_pframe_mvcopy(const uint8_t* stream, uint64_t start_bit, int mv_bits, const uint8_t* ref, uint64_t rs,
+                          uint8_t* out, uint64_t os, int w, int h, hipStream_t s) {
+    const int nmb = (w / kMB) * (h / kMB);
+    if (nmb > 0)
+        hipLaunchKernelGGL(pf_mvcopy_kernel, dim3(nmb), dim3(kMbTPB), 0, s, stream, start_bit, mv_bits, ref, rs, out, os,
+                           w, h, w / kMB);
+}
 
 void launch_pframe(const PfArgs& a, int n, uint64_t* tsum, hipStream_t s) {
     const int nmb = a.mbx * a.mby;
@@ -287,17 +364,13 @@ void launch_pframe(const PfArgs& a, int n, uint64_t* tsum, hipStream_t s) {
     const int nb = a.bx * (a.h / n);
     if (nmb > 0) {
         if (n == 4) {
-            // blocks no macroblock covers keep bits = 0 (no record)
-            if (a.w % kMB || a.h % kMB) (void)hipMemsetAsync(a.bits, 0, size_t(nb) * sizeof(uint32_t), s);
-            hipLaunchKernelGGL(pf_macroblock_kernel<4>, dim3(nmb), dim3(kTPB), 0, s, a);
+            hipLaunchKernelGGL(pf_macroblock_kernel<4>, dim3(nmb), dim3(kMbTPB), 0, s, a);
         } else {
-            hipLaunchKernelGGL(pf_macroblock_kernel<8>, dim3(nmb), dim3(kTPB), 0, s, a);
+            hipLaunchKernelGGL(pf_macroblock_kernel<8>, dim3(nmb), dim3(kMbTPB), 0, s, a);
         }
     }
-    if (a.w % kMB || a.h % kMB || nmb == 0) {
-        const size_t px = size_t(a.w) * a.h;
-        hipLaunchKernelGGL(pf_strip_kernel, dim3(unsigned((px + kTPB - 1) / kTPB)), dim3(kTPB), 0, s, a);
-    }
+    const size_t px = size_t(a.w) * a.h - size_t(nmb) * kMB * kMB;  // pixels no macroblock covers
+    if (px) hipLaunchKernelGGL(pf_strip_kernel, dim3(unsigned((px + kTPB - 1) / kTPB)), dim3(kTPB), 0, s, a, n);
     if (n == 4 && nmb > 0) {
         const int ntiles = (nb + kPfTileBlocks - 1) / kPfTileBlocks;
         hipLaunchKernelGGL(pf_tile_sum_kernel, dim3(ntiles), dim3(kTPB), 0, s, a.bits, nb, tsum);

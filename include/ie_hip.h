@@ -247,6 +247,16 @@ int ie_decode_frames(ie_ctx* ctx, const uint8_t* in, size_t len, uint64_t start_
                      int nframes, int use_rle, uint8_t* out, size_t stride, size_t frame_pitch,
                      uint64_t* end_bit);
 
+/* Video payload with P-frames (VideoDecoder.cpp:28-58, Frame.cpp:47-127, Block.cpp:441-496): frame f
+ * an I-frame when f % gop == 0 (decoded as ie_decode_frames), otherwise a P-frame: its motion vectors
+ * (bits_needed(merange) bits each), the previous decoded frame's blocks at the clamped vectors copied
+ * into place, then a record for every microblock whose decoded error (IDCT + 128) is added to the
+ * copied pixels (motioncomp != 0) or read and dropped (motioncomp == 0).  W and H multiples of 16
+ * when P-frames exist (IE_EINVAL otherwise).  end_bit optional. */
+int ie_decode_gop(ie_ctx* ctx, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,
+                  int gop, int merange, int use_rle, int motioncomp, uint8_t* out, size_t stride,
+                  size_t frame_pitch, uint64_t* end_bit);
+
 /* Chunks and composition levels of the last ie_decode_frames call's exact parse (diagnostics: the
  * stream is cut into chunks of about 32 (4x4) / 16 (8x8) records, each tabulated over every entry
  * offset; the tables are composed G at a time, level after level). */
