@@ -298,26 +298,44 @@ __global__ __launch_bounds__(kTPB) void pf_tile_scan_kernel(uint64_t* tsum, int 
     if (threadIdx.x == 0) *end = *start + head_bits + carry;
 }
 
+// A tile's records are ORed into an LDS bit image (the image starts at the tile's first bit rounded
+// down to a word), then the image goes out in whole words: plain stores for the words the tile owns
+// alone, global ORs only for its first and last word (shared with the neighbouring tiles).
+constexpr int kPfImgWords = (kPfTileBlocks * 259 + 31) / 32 + 2;  // 259 = the longest 4x4 record
 __global__ __launch_bounds__(kTPB) void pf_emit_kernel(PfArgs a, int nb, const uint64_t* tpre, uint64_t head_bits) {
     __shared__ uint64_t sh[kTPB / 64];
-    const int b0 = blockIdx.x * kPfTileBlocks + threadIdx.x * kPfPer;
+    __shared__ uint32_t img[kPfImgWords];
+    const int t = threadIdx.x;
+    const int b0 = blockIdx.x * kPfTileBlocks + t * kPfPer;
     uint64_t s = 0;
     for (int k = 0; k < kPfPer; k++)
         if (b0 + k < nb) s += a.bits[b0 + k];
     uint64_t tot;
     const uint64_t ex = block_exscan(s, sh, &tot);
-    if (s == 0) return;
-    BitOr o(a.out, *a.start + head_bits + tpre[blockIdx.x] + ex);
-    for (int k = 0; k < kPfPer && b0 + k < nb; k++) {
-        if (!a.bits[b0 + k]) continue;  // no macroblock covered it: no record (Block.cpp:373-375)
-        const int16_t* c = a.coef + size_t(b0 + k) * 16;
-        const uint32_t sz = size4(c, a.rle);
-        const int bl = int(sz & 0xFFu), lw = int(sz >> 8);
-        o.put(4, uint32_t(bl));  // Block::streamEncoded (Block.cpp:372-413)
-        if (a.rle) o.put(bl, uint32_t(lw));
-        for (int i = 0; i < lw; i++) o.put(bl, uint32_t(int32_t(c[kZz4[i]])));
+    const uint64_t S = *a.start + head_bits + tpre[blockIdx.x];  // the tile's first bit
+    const uint32_t o0 = uint32_t(S & 31u);
+    const uint32_t nw = uint32_t((o0 + tot + 31) / 32);
+    for (uint32_t i = t; i < nw; i += kTPB) img[i] = 0u;
+    __syncthreads();
+    if (s) {
+        BitOr o(img, o0 + ex);
+        for (int k = 0; k < kPfPer && b0 + k < nb; k++) {
+            if (!a.bits[b0 + k]) continue;  // no macroblock covered it: no record (Block.cpp:373-375)
+            const int16_t* c = a.coef + size_t(b0 + k) * 16;
+            const uint32_t sz = size4(c, a.rle);
+            const int bl = int(sz & 0xFFu), lw = int(sz >> 8);
+            o.put(4, uint32_t(bl));  // Block::streamEncoded (Block.cpp:372-413)
+            if (a.rle) o.put(bl, uint32_t(lw));
+            for (int i = 0; i < lw; i++) o.put(bl, uint32_t(int32_t(c[kZz4[i]])));
+        }
+        o.flush();
     }
-    o.flush();
+    __syncthreads();
+    uint32_t* g = a.out + (S >> 5);
+    for (uint32_t i = t; i < nw; i += kTPB) {
+        if (i == 0 || i == nw - 1) atomicOr(g + i, img[i]);
+        else g[i] = img[i];
+    }
 }
 
 // the frame's end bit when it carries no records (8x8 blocks, or no macroblock)
