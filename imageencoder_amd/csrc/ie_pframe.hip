@@ -8,7 +8,7 @@
 // macroblocks' motion vectors followed by the covered microblocks' records in raster order.
 //
 // Layout of the work: one wave per macroblock, four pixels per lane (a candidate's partial SAD is
-// one v_sad_u8; the nine candidates of a pattern level are reduced across the wave together and
+// one v_sad_u8; the nine candidates of a pattern level are reduced across the wave by DPP and
 // every lane applies the reference's rule -- `<=`, later candidates win ties -- so the search needs
 // no LDS and no barrier), four coefficients per lane for the DCT and four pixels for the inverse,
 // the 4x4 microblocks' error and the FP64 transform rows staged in LDS.  The FP64 arithmetic is the reference's operation
@@ -88,6 +88,19 @@ __device__ __forceinline__ uint32_t rec_len(uint32_t s, int rle) {
     return 4u + (rle ? bl : 0u) + bl * lw;
 }
 
+// Sum over the wave by DPP (quad permutes, row shifts, row broadcasts: no LDS traffic), the total
+// read from lane 63 as a wave-uniform value.  Lanes whose DPP source is outside the row add 0.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    int x = int(v);
+    x += __builtin_amdgcn_update_dpp(0, x, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8 (row sum in lane 15)
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xf, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xf, 0xf, false);  // row_bcast:31 (total in lane 63)
+    return uint32_t(__builtin_amdgcn_readlane(x, 63));
+}
+
 // four horizontally adjacent pixels packed little-endian (byte j = pixel j), any alignment
 __device__ __forceinline__ uint32_t load4(const uint8_t* p) {
     return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
@@ -133,12 +146,7 @@ __global__ __launch_bounds__(kMbTPB) void pf_macroblock_kernel(PfArgs a) {
             d[p] = __builtin_amdgcn_sad_u8(c4, load4(a.ref + size_t(qy[p] + py) * a.rs + qx[p] + px), 0u);
         }
 #pragma unroll
-        for (int p = 0; p < 9; p++) {
-            uint32_t v = d[p];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-            d[p] = v;  // every lane holds the candidate's SAD
-        }
+        for (int p = 0; p < 9; p++) d[p] = wave_sum(d[p]);  // the candidate's SAD, wave-uniform
         int np = -1, nbx = 0, nby = 0;
         uint32_t nd = best;
 #pragma unroll
