@@ -157,3 +157,29 @@ def test_cli_video_gop1(work, name, chunk_mb):
     assert r.returncode == 0, r.stdout + r.stderr
     dec = np.frombuffer(open(os.path.join(work, "v.dec"), "rb").read(), np.uint8)
     assert dec.size == c["input"]["frames"] * w * h * 3 // 2
+
+
+# P-frame videos through the reference-shaped command lines: the settings file's gop / merange
+# select I/P-frames (VideoEncoder), motioncompensation the decoder's handling of the coded error
+GOP_CLI = ["gopP64x48x5_g3_m8", "gopM64x48x5_g2_m0", "gopP64x40x4_g4_m8"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", GOP_CLI)
+def test_cli_video_pframes(work, name):
+    c = next(c for c in O.manifest_gop() if c["name"] == name)
+    w, h = c["w"], c["h"]
+    open(os.path.join(work, "in.yuv"), "wb").write(O.case_input(c))
+    conf = _write_conf(work, rawfile="in.yuv", encfile="v.enc", decfile="v.dec", width=w, height=h, rle=c["rle"],
+                       quantfile=c["matrix"], logfile="", gop=c["gop"], merange=c["merange"])
+    r = _run(_bin("encoder_nohuff"), conf, work)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert open(os.path.join(work, "v.enc"), "rb").read() == O.case_expected(c)
+    if "dec1_md5" not in c:
+        return
+    for mc in (1, 0):
+        conf = _write_conf(work, encfile="v.enc", decfile="v.dec", motioncompensation=mc)
+        r = _run(_bin("decoder"), conf, work)
+        assert r.returncode == 0, r.stdout + r.stderr
+        dec = open(os.path.join(work, "v.dec"), "rb").read()
+        assert hashlib.md5(dec).hexdigest() == c[f"dec{mc}_md5"], mc
