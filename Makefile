@@ -59,8 +59,8 @@ ref:
 	$(MAKE) -C oracle ref
 
 # Check the exact FP64 paths really are unfused: dump the gfx950 ISA of the
-# encode and decode kernels and scan it (tools/asmcheck.py; also reports VGPRs / scratch).
-ASMS := $(OBJDIR)/asm/ie_encode.s $(OBJDIR)/asm/ie_decode.s
+# encode, decode and P-frame kernels and scan it (tools/asmcheck.py; also reports VGPRs / scratch).
+ASMS := $(OBJDIR)/asm/ie_encode.s $(OBJDIR)/asm/ie_decode.s $(OBJDIR)/asm/ie_pframe.s
 $(OBJDIR)/asm/%.s: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp $(CSRC)/ie_dct.h
 	@mkdir -p $(OBJDIR)/asm
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o $@

@@ -20,23 +20,26 @@ def scan(path):
     bad = []
     kernels = {}
     cur = None
-    in_div = False  # inside a v_div_scale_f64 .. v_div_fixup_f64 sequence (IEEE division)
+    scales = fixups = 0  # v_div_scale_f64 / v_div_fixup_f64 seen in this kernel (two scales per division)
     for ln in open(path):
         m = re.match(r"^(_Z\S+):", ln)
         if m:
             cur = m.group(1)
             kernels[cur] = {}
+            scales = fixups = 0
             continue
         s = ln.strip()
         op = s.split(None, 1)[0] if s and not s.startswith((";", ".")) else ""
         # The correctly rounded FP64 division (v_div_scale, v_rcp, Newton steps as FMAs,
         # v_div_fmas, v_div_fixup) returns the IEEE quotient: its FMAs are part of ONE rounded
         # operation, as in the reference's `/`, and are exempt.
+        # The scheduler may interleave several divisions, so "inside" means: some division whose
+        # scales were seen has not reached its fixup yet.
         if op.startswith("v_div_scale_f64"):
-            in_div = True
+            scales += 1
         elif op.startswith("v_div_fixup_f64"):
-            in_div = False
-        elif (op in FORBIDDEN or any(op.startswith(f + "_") for f in FORBIDDEN)) and not in_div:
+            fixups += 1
+        elif (op in FORBIDDEN or any(op.startswith(f + "_") for f in FORBIDDEN)) and (scales + 1) // 2 <= fixups:
             bad.append((cur, s))
         if cur:
             for key in ("NumVgprs", "ScratchSize", "Occupancy"):
