@@ -210,8 +210,12 @@ __global__ __launch_bounds__(kMbTPB) void pf_macroblock_kernel(PfArgs a) {
         }
         __syncthreads();
         const int gb = (my / 4 + (m >> 2)) * a.bx + (mx / 4 + (m & 3));
+        {  // the lane's four coefficients in one 8-byte store (coef rows are 32-byte aligned)
+            uint64_t c4 = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) a.coef[size_t(gb) * 16 + g + j] = cq[m * 16 + g + j];
+            for (int j = 0; j < 4; j++) c4 |= uint64_t(uint16_t(cq[m * 16 + g + j])) << (16 * j);
+            *reinterpret_cast<uint64_t*>(a.coef + size_t(gb) * 16 + g) = c4;
+        }
         if (g == 0) a.bits[gb] = rec_len(size4(cq + m * 16, a.rle), a.rle);
         // ---- inverse (Block.cpp:162-177): lane = (microblock l/4, pixel row l%4), uv ascending;
         // then expandDifferences over the copied reference block (Block.cpp:110-119)
@@ -224,12 +228,13 @@ __global__ __launch_bounds__(kMbTPB) void pf_macroblock_kernel(PfArgs a) {
         }
         const int ppy = (m >> 2) * 4 + (l & 3), ppx = (m & 3) * 4;
         const uint32_t b4 = load4(a.ref + size_t(ccy + ppy) * a.rs + ccx + ppx);
-        uint8_t* o = a.rec + size_t(my + ppy) * a.w + mx + ppx;
+        uint32_t o4 = 0;  // four reconstructed pixels, one 4-byte store (W % 4 == 0, mx + ppx % 4 == 0)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const double v = double(int((b4 >> (8 * j)) & 255u)) + (tt[j] + double(128));
-            o[j] = uint8_t(v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v));
+            o4 |= uint32_t(uint8_t(v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v))) << (8 * j);
         }
+        *reinterpret_cast<uint32_t*>(a.rec + size_t(my + ppy) * a.w + mx + ppx) = o4;
     }
 }
 
