@@ -18,7 +18,7 @@ all: lib host oracle
 
 lib: $(LIBDIR)/libie_hip.so
 
-$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp include/ie_hip.h
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp $(CSRC)/ie_dct.h include/ie_hip.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -59,6 +59,7 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.ie_set_stream.argtypes = [vp, vp]
     L.ie_sync.argtypes = [vp]
     L.ie_set_quant.argtypes = [vp, u16p, C.c_int]
+    L.ie_cos_table.argtypes = [vp, vp]
     L.ie_stream_bound.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
     L.ie_stream_bound.restype = C.c_size_t
     L.ie_encode_frames.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
@@ -316,6 +317,12 @@ class Codec:
         assert q.size == n * n
         self._chk(self.L.ie_set_quant(self.h, q.ctypes.data, n))
         self.n = n
+
+    def cos_table(self) -> np.ndarray:
+        """The cos table the kernels use (read back from the device; ie_cos_table), n x n doubles."""
+        out = np.zeros(self.n * self.n, np.float64)
+        self._chk(self.L.ie_cos_table(self.h, out.ctypes.data))
+        return out.reshape(self.n, self.n)
 
     def encode_frames(self, y, w: int, h: int, out, start_bit: int = 0, stride: int | None = None,
                       frame_pitch: int | None = None, nframes: int = 1, rle: bool = True,

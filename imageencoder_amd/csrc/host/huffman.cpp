@@ -301,59 +301,11 @@ int Huffman::encode(ie_ctx* c, const uint8_t* in, size_t n, std::vector<uint8_t>
 // after the stop bit).  The bit walk -- O(stream bits), serial in the reference -- runs on the
 // device (ie_huffman_decode) over a 15-bit prefix table built from the tree.
 int Huffman::decode_table(const uint8_t* in, size_t n, uint16_t* lut, bool& passthrough, size_t& start_bit) {
-    util::BitStreamReader rd(in, n);
-    struct T {
-        int child[2] = {-1, -1};
-        int sym = -1;
-    };
-    std::vector<T> tree(1);
-    bool any = false;
-    while (rd.get_bit()) {
-        uint32_t cnt = rd.get(7);
-        const uint32_t bl = rd.get(4);
-        while (cnt--) {
-            const uint32_t key = rd.get(8), word = rd.get(bl);
-            any = true;
-            int cur = 0;
-            // treeAddLeaf (Huffman.cpp:143-173): bl = 0 puts the leaf under the root's left edge
-            const int steps = bl ? int(bl) : 1;
-            for (int b = steps - 1; b >= 0; b--) {
-                const int dir = bl ? int((word >> b) & 1u) : 0;
-                if (tree[cur].child[dir] < 0) {
-                    tree[cur].child[dir] = int(tree.size());
-                    tree.emplace_back();
-                }
-                cur = tree[cur].child[dir];
-            }
-            tree[cur].sym = int(key);
-        }
-    }
-    passthrough = !any;
-    start_bit = rd.get_position();
-    if (!any) return IE_OK;
-    // lut[p] = sym | len << 8 for the leaf reached by the 15-bit string p (codes are <= 15 bits:
-    // 4-bit lengths in the dictionary); 0 where the walk falls off the tree or needs more bits
-    constexpr int K = 15;
-    std::fill(lut, lut + (size_t(1) << K), uint16_t(0));
-    std::vector<std::pair<int, int>> stack{{0, 0}};  // (node, depth); prefix filled per leaf
-    std::vector<uint32_t> path(tree.size(), 0);
-    while (!stack.empty()) {
-        const auto [nd, depth] = stack.back();
-        stack.pop_back();
-        const T& t = tree[size_t(nd)];
-        const bool leaf = t.child[0] < 0 && t.child[1] < 0;
-        if (leaf) {
-            if (depth == 0 || depth > K || t.sym < 0) continue;  // a lone root / over-long code: no entry
-            const uint32_t lo = path[size_t(nd)] << (K - depth), span = 1u << (K - depth);
-            for (uint32_t q = 0; q < span; q++) lut[lo + q] = uint16_t(uint32_t(t.sym) | (uint32_t(depth) << 8));
-            continue;
-        }
-        for (int d = 0; d < 2; d++)
-            if (t.child[d] >= 0) {
-                path[size_t(t.child[d])] = (path[size_t(nd)] << 1) | uint32_t(d);
-                stack.push_back({t.child[d], depth + 1});
-            }
-    }
+    uint64_t from = 0;
+    const int r = ie_huffman_table(in, n, 0, lut, &from);  // the dictionary parse lives in the C ABI
+    if (r < 0) return r;
+    passthrough = r == 1;
+    start_bit = size_t(from);
     return IE_OK;
 }
 

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <atomic>
 #include <mutex>
@@ -45,6 +46,8 @@ struct ie_ctx {
     int last_fix_words = 0;
     unsigned err_seen[66] = {};         // counter values at the previous read
     bool use_ticket = false;            // order tiles with an atomic ticket (after a timeout)
+    int fake_timeouts = 0;              // debug (IE_FAKE_TIMEOUTS): report this many look-back timeouts
+    bool fake_fired = false;            // a faked timeout was reported (the redo paths dirty the output first)
     // Asynchronous launches (no read-back) since the last error read: a look-back timeout found
     // at the next read is charged to them (their output is invalid), never silently retried away.
     unsigned async_pending = 0;
@@ -396,7 +399,12 @@ int read_errors(ie_ctx* c, unsigned* timeouts, uint64_t* fallbacks) {
         HIPCHK(c, hipMemcpy(w.data(), c->d_wave_fix, w.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
         for (uint32_t v : w) f += v;
     }
-    const unsigned t = e[0] - c->err_seen[0];
+    unsigned t = e[0] - c->err_seen[0];
+    if (c->fake_timeouts > 0 && timeouts && !c->async_pending) {  // debug: IE_FAKE_TIMEOUTS
+        c->fake_timeouts--;
+        c->fake_fired = true;
+        t++;
+    }
     if (timeouts) *timeouts = t;
     if (fallbacks) *fallbacks = f;
     std::memcpy(c->err_seen, e, sizeof(e));
@@ -1401,6 +1409,9 @@ int ie_create(int device, ie_ctx** out) {
     // Debug switch: order tiles by the atomic ticket from the first launch (exercises the
     // timeout-recovery path, which dispatch order otherwise never needs)
     if (const char* ft = getenv("IE_FORCE_TICKET")) c->use_ticket = atoi(ft) != 0;
+    // Debug switch: the next k synchronous error checks report a look-back timeout (exercises the
+    // redo-in-ticket-mode paths and their output clearing)
+    if (const char* ft = getenv("IE_FAKE_TIMEOUTS")) c->fake_timeouts = atoi(ft);
     if (r == IE_OK) chk(hipMalloc(&c->d_tab, sizeof(ie::EncTables)), "hipMalloc(tables)");
     if (r == IE_OK) chk(hipHostMalloc(&c->h_tab, sizeof(ie::EncTables)), "hipHostMalloc(tables)");
     if (r == IE_OK) chk(hipMalloc(&c->d_ticket, sizeof(unsigned long long)), "hipMalloc(ticket)");
@@ -1503,6 +1514,17 @@ int ie_set_quant(ie_ctx* c, const uint16_t* q, int n) {
     HIPCHK(c, hipMemcpy(c->d_tab, c->h_tab, sizeof(ie::EncTables), hipMemcpyHostToDevice));
     c->n = n;
     std::memcpy(c->q, q, sizeof(uint16_t) * n * n);
+    return IE_OK;
+}
+
+int ie_cos_table(ie_ctx* c, double* out) {
+    if (!c || !out) return IE_EINVAL;
+    if (c->n == 0) return fail(c, IE_ENOQUANT, "ie_set_quant not called");
+    // read back from the DEVICE table: the values every kernel's FP64 path multiplies with
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, reinterpret_cast<const char*>(c->d_tab) + offsetof(ie::EncTables, c),
+                        sizeof(double) * size_t(c->n) * size_t(c->n), hipMemcpyDeviceToHost));
     return IE_OK;
 }
 
@@ -1640,7 +1662,33 @@ int ie_encode_gop(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size
     unsigned timeouts = 0;
     if ((r = read_errors(c, &timeouts, nullptr))) return r;
     if (timeouts) {
+        if (c->use_ticket) return fail(c, IE_EDEVICE, "tile look-back timed out");
         c->use_ticket = true;  // an I-frame's tiles did not run in order: redo in ticket mode
+        if (out_dev) {
+            // the first attempt ORed vectors and P-frame records at positions derived from a bad end
+            // bit: clear the caller's stream from start_bit on (the bits before it are the caller's)
+            const size_t b0 = size_t(start_bit / 8), b1 = size_t((start_bit + 7) / 8);
+            if (c->fake_fired) {  // debug: a faked timeout stands for a bad first attempt -- leave junk
+                c->fake_fired = false;
+                HIPCHK(c, hipMemsetAsync(out + b0 + (b1 > b0 ? 1 : 0), 0xA5, need - b1, c->stream));
+                if (b1 > b0) {
+                    uint8_t lead = 0;
+                    HIPCHK(c, hipMemcpyAsync(&lead, out + b0, 1, hipMemcpyDeviceToHost, c->stream));
+                    HIPCHK(c, hipStreamSynchronize(c->stream));
+                    lead |= uint8_t(0xFFu >> (start_bit % 8));
+                    HIPCHK(c, hipMemcpyAsync(out + b0, &lead, 1, hipMemcpyHostToDevice, c->stream));
+                }
+            }
+            if (need > b1) HIPCHK(c, hipMemsetAsync(out + b1, 0, need - b1, c->stream));
+            if (b1 > b0) {
+                uint8_t lead = 0;
+                HIPCHK(c, hipMemcpyAsync(&lead, out + b0, 1, hipMemcpyDeviceToHost, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                lead &= uint8_t(0xFF00u >> (start_bit % 8));
+                HIPCHK(c, hipMemcpyAsync(out + b0, &lead, 1, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+            }
+        }
         return ie_encode_gop(c, y, w, h, stride, frame_pitch, nframes, gop, merange, use_rle, mode, out, out_cap,
                              start_bit, frame_bits, end_bit);
     }
@@ -2039,6 +2087,80 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
                                      start_bit, end_bit);
     }
     for (size_t k = 0; k < K; k++) end_bit[k] = n[k] ? ends[k] : start_bit[k];
+    return IE_OK;
+}
+
+int ie_huffman_table(const uint8_t* in, size_t len, uint64_t start_bit, uint16_t* lut, uint64_t* code_start) {
+    if ((!in && len) || !lut || !code_start) return IE_EINVAL;
+    // MSB-first reads (BitStreamReader::get, BitStream.cpp:14-40); past the end: malformed
+    uint64_t pos = start_bit;
+    bool over = false;
+    auto get = [&](unsigned nb) {
+        uint32_t v = 0;
+        for (unsigned k = 0; k < nb; k++, pos++) {
+            if (pos >= uint64_t(len) * 8) {
+                over = true;
+                return 0u;
+            }
+            v = (v << 1) | ((in[pos >> 3] >> (7 - (pos & 7))) & 1u);
+        }
+        return v;
+    };
+    // Huffman::buildTree (Huffman.cpp:120-143): groups of {1, count:7, bits:4} headers, each
+    // followed by count {key:8, code:bits} entries, ended by a '0' bit; treeAddLeaf (:143-173)
+    // grows the tree along the code's bits MSB first (bits = 0 hangs the leaf on the root's left)
+    struct Node {
+        int child[2] = {-1, -1};
+        int sym = -1;
+    };
+    std::vector<Node> tree(1);
+    bool any = false;
+    // (an empty stream, or one ending right after its last group, reads as the stop bit)
+    while (pos < uint64_t(len) * 8 && get(1)) {
+        uint32_t cnt = get(7);
+        const uint32_t bl = get(4);
+        while (cnt-- && !over) {
+            const uint32_t key = get(8), word = get(bl);
+            any = true;
+            int cur = 0;
+            const int steps = bl ? int(bl) : 1;
+            for (int b = steps - 1; b >= 0; b--) {
+                const int dir = bl ? int((word >> b) & 1u) : 0;
+                if (tree[size_t(cur)].child[dir] < 0) {
+                    tree[size_t(cur)].child[dir] = int(tree.size());
+                    tree.emplace_back();
+                }
+                cur = tree[size_t(cur)].child[dir];
+            }
+            tree[size_t(cur)].sym = int(key);
+        }
+        if (over) return IE_EFORMAT;
+    }
+    if (over) return IE_EFORMAT;
+    *code_start = pos;
+    if (!any) return 1;  // no dictionary: the data follows uncompressed (Huffman.cpp:361-371)
+    // lut[p] = sym | len << 8 for the leaf the 15-bit string p walks to (codes are <= 15 bits: a
+    // 4-bit length field, Huffman.cpp:41-42); 0 where the walk leaves the tree
+    constexpr int K = 15;
+    std::fill(lut, lut + (size_t(1) << K), uint16_t(0));
+    std::vector<std::pair<int, int>> stack{{0, 0}};
+    std::vector<uint32_t> path(tree.size(), 0);
+    while (!stack.empty()) {
+        const auto [nd, depth] = stack.back();
+        stack.pop_back();
+        const Node& t = tree[size_t(nd)];
+        if (t.child[0] < 0 && t.child[1] < 0) {
+            if (depth == 0 || depth > K || t.sym < 0) continue;  // a lone root / over-long code: no entry
+            const uint32_t lo = path[size_t(nd)] << (K - depth), span = 1u << (K - depth);
+            for (uint32_t q = 0; q < span; q++) lut[lo + q] = uint16_t(uint32_t(t.sym) | (uint32_t(depth) << 8));
+            continue;
+        }
+        for (int d = 0; d < 2; d++)
+            if (t.child[d] >= 0) {
+                path[size_t(t.child[d])] = (path[size_t(nd)] << 1) | uint32_t(d);
+                stack.push_back({t.child[d], depth + 1});
+            }
+    }
     return IE_OK;
 }
 

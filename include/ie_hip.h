@@ -72,6 +72,12 @@ int ie_sync(ie_ctx* ctx);
  * with std::cos in the reference's exact expression (algo.cpp:312,318-319).  q[k] must be > 0. */
 int ie_set_quant(ie_ctx* ctx, const uint16_t* q, int n);
 
+/* The cos table of the current quant matrix as the kernels use it, read back from the device:
+ * out[u*n + i] = std::cos(((2.0*i + 1.0) * u) * (M_PI_2 / n)) evaluated by THIS host's libm when
+ * ie_set_quant ran (algo.cpp:312,318-319), n*n doubles.  Lets a caller pin the machine's libm
+ * against the reference's values (tests/golden/cos_table.json). */
+int ie_cos_table(ie_ctx* ctx, double* out);
+
 /* Upper bound in bytes of an output buffer for nframes frames of w x h encoded from start_bit
  * (4 + 17*16 bits per 4x4 block, 4 + 65*16 per 8x8 block, rounded up to whole 32-bit words). */
 size_t ie_stream_bound(int w, int h, int n, int nframes, uint64_t start_bit);
@@ -236,6 +242,13 @@ int ie_bitcopy(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint8_t* out, size_t
  * 15-bit string p (len 0: none; codes are <= 15 bits, Huffman.cpp:41-42), built by the caller from
  * the dictionary.  out (host or device, out_cap bytes) receives the symbols; *nout their count
  * (also when IE_ECAP is returned).  IE_EFORMAT: a bit string that no code prefixes. */
+/* The dictionary half of Huffman<uint8_t>::decode (buildTree, Huffman.cpp:120-173): parse the
+ * dictionary of a Huffman-coded stream from bit start_bit of `in` (host memory, len bytes) into
+ * ie_huffman_decode's prefix table lut (32768 entries); *code_start = the bit after its stop bit.
+ * Returns 0, 1 when the stream has no dictionary (the data follows uncompressed from *code_start,
+ * Huffman.cpp:361-371), or IE_EFORMAT when the dictionary runs past the buffer. */
+int ie_huffman_table(const uint8_t* in, size_t len, uint64_t start_bit, uint16_t* lut, uint64_t* code_start);
+
 int ie_huffman_decode(ie_ctx* ctx, const uint8_t* in, size_t len, uint64_t start_bit, const uint16_t* lut,
                       uint8_t* out, size_t out_cap, size_t* nout);
 

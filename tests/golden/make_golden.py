@@ -13,7 +13,7 @@ oracle/_ref exist (the build container); its outputs are committed as data:
                             pinned by md5 only);
 * ``cos_table.json``        the reference's cos values as exact hex doubles.
 
-Inputs taken from the reference are its example assets (bin/ex0.raw, bin/ex6.raw and the
+Inputs taken from the reference are its example assets (bin/ex0-ex4.raw, bin/ex6.raw and the
 quantisation matrices) -- data files, copied as fixtures.
 
 Usage:  python tests/golden/make_golden.py      (rewrites tests/golden/)
@@ -38,7 +38,7 @@ REF_BIN = "/root/reference/bin"
 REF = os.path.join(ROOT, "oracle", "_ref")
 STORE_LIMIT = 64 * 1024  # outputs up to this size are stored whole
 
-ASSETS = ["ex0.raw", "ex6.raw", "matrix.txt", "matrix4_2.txt", "matrix8_1.txt", "matrix8_2.txt"]
+ASSETS = ["ex0.raw", "ex1.raw", "ex2.raw", "ex3.raw", "ex4.raw", "ex6.raw", "matrix.txt", "matrix4_2.txt", "matrix8_1.txt", "matrix8_2.txt"]
 
 
 def md5(b: bytes) -> str:
@@ -124,6 +124,13 @@ def cases():
         add(f"ex0_8x8{hs}", ex0, 8, 8, 8, 1, "matrix8_1.txt", huff, decode=True)
         add(f"ex6_4x4{hs}", ex6, 512, 256, 4, 1, "matrix.txt", huff, decode=True)
         add(f"ex6_8x8{hs}", ex6, 512, 256, 8, 1, "matrix8_1.txt", huff, decode=True)
+    # the reference's published example images (README.md:175-183; natural content at real
+    # scale: long zero runs, smooth gradients), the sizes/md5s of SURVEY Appendix B
+    for i, (w, h) in ((1, (936, 936)), (2, (512, 512)), (3, (400, 400)), (4, (4096, 912))):
+        exi = dict(kind="asset", file=f"ex{i}.raw")
+        add(f"ex{i}_4x4", exi, w, h, 4, 1, "matrix.txt", decode=True)
+        add(f"ex{i}_4x4_huff", exi, w, h, 4, 1, "matrix.txt", True, decode=True)
+        add(f"ex{i}_8x8", exi, w, h, 8, 1, "matrix8_1.txt", decode=True)
     add("ex6_4x4_m2", ex6, 512, 256, 4, 1, "matrix4_2.txt", decode=True)
     add("ex6_4x4_norle", ex6, 512, 256, 4, 0, "matrix.txt", decode=True)
     add("ex6_8x8_m2", ex6, 512, 256, 8, 1, "matrix8_2.txt", decode=True)

@@ -1,0 +1,42 @@
+"""tools/asmcheck.py (the build's guard that the exact FP64 paths carry no fused multiply-add,
+SURVEY Appendix C.4): a correctly rounded division's own Newton steps pass, a contracted a*b+c
+scheduled inside a division's window does not."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+DIV = """\tv_div_scale_f64 v[16:17], s[22:23], v[12:13], v[12:13], v[10:11]
+\tv_rcp_f64_e32 v[38:39], v[16:17]
+\tv_div_scale_f64 v[40:41], vcc, v[10:11], v[12:13], v[10:11]
+\tv_fma_f64 v[42:43], -v[16:17], v[38:39], 1.0
+\tv_fmac_f64_e32 v[38:39], v[38:39], v[42:43]
+{inject}\tv_fma_f64 v[42:43], -v[16:17], v[38:39], 1.0
+\tv_fmac_f64_e32 v[38:39], v[38:39], v[42:43]
+\tv_mul_f64 v[42:43], v[40:41], v[38:39]
+\tv_fma_f64 v[16:17], -v[16:17], v[42:43], v[40:41]
+\tv_div_fmas_f64 v[16:17], v[16:17], v[38:39], v[42:43]
+\tv_div_fixup_f64 v[16:17], v[16:17], v[12:13], v[10:11]
+"""
+
+
+def _run(tmp_path, body):
+    p = tmp_path / "k.s"
+    p.write_text("_Zkern:\n" + body)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asmcheck.py"), str(p)],
+                          capture_output=True, text=True, timeout=60)
+
+
+def test_division_steps_pass(tmp_path):
+    assert _run(tmp_path, DIV.format(inject="")).returncode == 0
+
+
+def test_contracted_fma_inside_division_window_fails(tmp_path):
+    r = _run(tmp_path, DIV.format(inject="\tv_fma_f64 v[50:51], v[2:3], v[4:5], v[6:7]\n"))
+    assert r.returncode == 1 and "v[50:51]" in r.stderr
+
+
+def test_fma_outside_any_division_fails(tmp_path):
+    r = _run(tmp_path, "\tv_fmac_f64_e32 v[2:3], v[4:5], v[6:7]\n" + DIV.format(inject=""))
+    assert r.returncode == 1

@@ -106,7 +106,9 @@ def test_exit_5_bad_number(work):
 
 
 # ------------------------------------------------------------------ byte-identical files (GPU)
-CLI_CASES = [c for c in O.manifest() if c["input"]["kind"] == "asset" and "file" in c]
+# every reference asset: ex0, ex6 and the published example images ex1-ex4 (README.md:175-183);
+# large outputs are pinned by md5
+CLI_CASES = [c for c in O.manifest() if c["input"]["kind"] == "asset"]
 
 
 @pytest.mark.gpu
@@ -119,7 +121,11 @@ def test_cli_encode_decode_golden(work, c):
     r = _run(enc_exe, conf, work, env)
     assert r.returncode == 0, r.stdout + r.stderr
     got = open(os.path.join(work, "out.enc"), "rb").read()
-    assert got == O.case_expected(c), c["name"]
+    want = O.case_expected(c)
+    if want is None:
+        assert len(got) == c["size"] and hashlib.md5(got).hexdigest() == c["md5"], c["name"]
+    else:
+        assert got == want, c["name"]
     if c.get("decode"):
         r = _run(_bin("decoder"), conf, work, env)
         assert r.returncode == 0, r.stdout + r.stderr

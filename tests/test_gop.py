@@ -199,3 +199,38 @@ def test_gpu_gop_roundtrip_1080_multiple_of_16(codec):
     assert enc == O.load().encode_video_gop(synth.yuv420(y), w, h, 4, q, gop=4, merange=16)
     dec, _ = codec.decode_video_file(enc, 4)
     assert dec.tobytes() == O.load().decode_video_gop(enc, 4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fake", [1, 2])
+def test_gpu_gop_timeout_redo_clears_stream(fake, monkeypatch):
+    """The look-back timeout recovery of ie_encode_gop (IE_FAKE_TIMEOUTS reports k timeouts): one
+    timeout redoes the video in ticket mode on a device-resident stream whose first attempt already
+    ORed vectors and records in -- the redo clears it from start_bit on and the result equals the
+    reference's payload, the caller's bits before start_bit kept; a second timeout in ticket mode
+    fails with IE_EDEVICE instead of recursing."""
+    import torch
+    from imageencoder_amd import Codec, IEError
+    c = next(c for c in CASES if c["name"] == "gopP64x48x5_g3_m8")
+    q = O.read_matrix(c["matrix"], 4)
+    y = _frames(c)
+    f = y.shape[0]
+    hdr, hb = O.load().header(4, q, c["rle"], c["w"], c["h"], video=True, frames=f, gop=c["gop"],
+                              merange=c["merange"])
+    monkeypatch.setenv("IE_FAKE_TIMEOUTS", str(fake))
+    codec = Codec(0, q, 4)
+    try:
+        cap = codec.gop_stream_bound(c["w"], c["h"], f, c["merange"], hb)
+        head = np.zeros(cap, np.uint8)
+        head[: len(hdr)] = hdr[:cap]
+        out = torch.from_numpy(head).cuda()
+        dy = torch.from_numpy(np.ascontiguousarray(y)).cuda()
+        if fake == 2:
+            with pytest.raises(IEError):
+                codec.encode_gop(dy, c["w"], c["h"], out, c["gop"], c["merange"], start_bit=hb, nframes=f)
+            return
+        _, end = codec.encode_gop(dy, c["w"], c["h"], out, c["gop"], c["merange"], start_bit=hb, nframes=f)
+        got = out.cpu().numpy()[: (end + 7) // 8].tobytes()
+        assert got == O.case_expected(c)
+    finally:
+        codec.close()

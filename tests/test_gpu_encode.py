@@ -58,14 +58,34 @@ def _golden(nonhuff_only=True, big=False):
     return cs
 
 
+EX_DIMS = {"ex0": (8, 8), "ex1": (936, 936), "ex2": (512, 512), "ex3": (400, 400), "ex4": (4096, 912),
+           "ex6": (512, 256)}
+
+
+@pytest.mark.parametrize("n,matrix", [(4, "matrix.txt"), (8, "matrix8_1.txt"), (4, "matrix4_2.txt"),
+                                      (8, "matrix8_2.txt")])
+def test_cos_table_pinned_on_device(codec, n, matrix):
+    """the cos table this box's libm produced for ie_set_quant -- read back from the
+    device, i.e. what the FP64 paths multiply with -- equals the reference's values (exact hex
+    doubles printed by the reference build, tests/golden/cos_table.json)."""
+    import json
+    ref = json.load(open(f"{O.GOLDEN}/cos_table.json"))[str(n)]
+    codec.set_quant(O.read_matrix(matrix, n), n)
+    got = codec.cos_table().ravel()
+    exp = np.array([float.fromhex(x) for x in ref])
+    assert np.array_equal(got.view(np.uint64), exp.view(np.uint64)), \
+        [(i, got[i].hex(), exp[i].hex()) for i in np.nonzero(got != exp)[0][:4]]
+
+
 @pytest.mark.parametrize("mode", [MODE_FAST, MODE_EXACT], ids=["fast", "exact"])
 @pytest.mark.parametrize("n,matrix", [(4, "matrix.txt"), (8, "matrix8_1.txt")])
-@pytest.mark.parametrize("kind", ["ex0", "ex6", "U", "M"])
+@pytest.mark.parametrize("kind", ["ex0", "ex1", "ex2", "ex3", "ex4", "ex6", "U", "M"])
 def test_quantized_coefficients(codec, oracle, kind, n, matrix, mode):
-    """Block::processDCTDivQ alone: every quantised coefficient vs the oracle."""
+    """Block::processDCTDivQ alone: every quantised coefficient vs the oracle (the reference's
+    example images ex0-ex4 and ex6, README.md:175-183, and seeded synthetic frames)."""
     if kind.startswith("ex"):
         raw = open(f"{O.GOLDEN}/{kind}.raw", "rb").read()
-        w, h = (8, 8) if kind == "ex0" else (512, 256)
+        w, h = EX_DIMS[kind]
         y = np.frombuffer(raw, dtype=np.uint8).reshape(h, w)
     else:
         y = synth.frame(kind, 320, 240, seed=5)

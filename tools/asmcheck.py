@@ -16,31 +16,60 @@ import sys
 FORBIDDEN = ("v_fma_f64", "v_fmac_f64", "v_fma_mix", "v_pk_fma_f64")
 
 
+def _regs(operands):
+    """Register names of an instruction's operands (modifiers stripped): 'v[16:17]', 's[22:23]'."""
+    out = []
+    for o in operands:
+        o = o.strip().lstrip("-").strip("|")
+        if re.match(r"^[vs](\[\d+:\d+\]|\d+)$", o):
+            out.append(o)
+    return out
+
+
+# A correctly rounded FP64 division on gfx950 is v_div_scale_f64 x2, v_rcp_f64, two Newton
+# rounds on the reciprocal (v_fma_f64 error + v_fmac_f64 update each), v_mul_f64, one residual
+# v_fma_f64, v_div_fmas_f64, v_div_fixup_f64: its five fused ops are part of ONE IEEE-rounded
+# operation, as the reference's `/`, and are exempt -- but only those:
+DIV_FMAS = 5
+
+
 def scan(path):
     bad = []
     kernels = {}
     cur = None
-    scales = fixups = 0  # v_div_scale_f64 / v_div_fixup_f64 seen in this kernel (two scales per division)
     for ln in open(path):
         m = re.match(r"^(_Z\S+):", ln)
         if m:
             cur = m.group(1)
             kernels[cur] = {}
-            scales = fixups = 0
+            scales = fixups = 0   # v_div_scale_f64 / v_div_fixup_f64 seen (two scales per division)
+            exempt = 0            # FMAs accepted as division steps so far in this kernel
+            taint = set()         # registers written by an open division's scale / rcp / steps
             continue
         s = ln.strip()
         op = s.split(None, 1)[0] if s and not s.startswith((";", ".")) else ""
-        # The correctly rounded FP64 division (v_div_scale, v_rcp, Newton steps as FMAs,
-        # v_div_fmas, v_div_fixup) returns the IEEE quotient: its FMAs are part of ONE rounded
-        # operation, as in the reference's `/`, and are exempt.
-        # The scheduler may interleave several divisions, so "inside" means: some division whose
-        # scales were seen has not reached its fixup yet.
-        if op.startswith("v_div_scale_f64"):
-            scales += 1
+        args = s.split(None, 1)[1].split(",") if op and len(s.split(None, 1)) > 1 else []
+        regs = _regs(args)
+        fused = op in FORBIDDEN or any(op.startswith(f + "_") for f in FORBIDDEN)
+        # "inside a division": some division whose scales were seen has not reached its fixup yet
+        # (the scheduler may interleave several).  An FMA there is a division step only if it reads
+        # a register the division's own scale / rcp / earlier steps wrote, and no division may
+        # carry more than its DIV_FMAS steps: a contracted a*b+c scheduled into the window is not.
+        if op.startswith(("v_div_scale_f64", "v_rcp_f64")) and regs:
+            scales += op.startswith("v_div_scale_f64")
+            taint.add(regs[0])
         elif op.startswith("v_div_fixup_f64"):
             fixups += 1
-        elif (op in FORBIDDEN or any(op.startswith(f + "_") for f in FORBIDDEN)) and (scales + 1) // 2 <= fixups:
-            bad.append((cur, s))
+            if (scales + 1) // 2 <= fixups:
+                taint.clear()
+        elif fused:
+            inside = (scales + 1) // 2 > fixups
+            step = inside and any(r in taint for r in regs[1:]) and exempt < DIV_FMAS * ((scales + 1) // 2)
+            if step:
+                exempt += 1
+                taint.add(regs[0])
+            else:
+                bad.append((cur, s))
         if cur:
             for key in ("NumVgprs", "ScratchSize", "Occupancy"):
                 m = re.match(rf"^; {key}: (\d+)", s)
