@@ -672,6 +672,16 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     uint32_t* ctl = misc + 16;     // [4] ticket, [5..6] exclusive prefix, [7] predecessor tail
     // FAST mode: the structural coefficients' FP64 rows (P[3][NN], then S[3], rq[3], qd[3])
     double* const srow = reinterpret_cast<double*>(misc + 32 + (HIST ? 256 : 0));
+    // 4x4 FAST: all NN rows of P, then S, rq, qd of every coefficient (kRowDoubles); 8x8: the three
+    // structural rows, then their S, rq, qd (3 * NN + 9)
+    constexpr bool kFullRows = N == 4 && !EXACT;
+    constexpr int kRowDoubles = kFullRows ? NN * NN + 3 * NN : 3 * NN + 9;
+    // row / S / rq / qd of structural coefficient s (kFullRows: of coefficient k = s)
+    auto rowP = [&](int k) -> const double* { return kFullRows ? srow + k * NN : srow + k * NN; };
+    auto rowS = [&](int k) { return kFullRows ? srow[NN * NN + k] : srow[3 * NN + k]; };
+    auto rowRq = [&](int k) { return kFullRows ? srow[NN * NN + NN + k] : srow[3 * NN + 3 + k]; };
+    auto rowQd = [&](int k) { return kFullRows ? srow[NN * NN + 2 * NN + k] : srow[3 * NN + 6 + k]; };
+    (void)kRowDoubles;
 
     const int tid = threadIdx.x;
     // Profiling hooks (IE_ABLATE / IE_STAMPS) exist only in IE_PROFILE builds (tools/variants.sh):
@@ -698,7 +708,13 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     uint32_t* const hl = misc + 32;  // HIST: the tile's byte histogram
     if constexpr (HIST)
         for (int i = tid; i < 256; i += TPB) hl[i] = 0u;  // (visible after the scan's barriers)
-    if constexpr (!EXACT) {
+    if constexpr (kFullRows) {
+        // 4x4: every coefficient's FP64 row P[k][*] and its S, rq, qd (304 doubles): the fix-up's
+        // structural AND whole-block evaluations read them from LDS, never from global memory
+        for (int i = tid; i < kRowDoubles; i += TPB)
+            srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
+                    : (i < NN * NN + 2 * NN) ? tab->rq[i - NN * NN - NN] : tab->qd[i - NN * NN - 2 * NN];
+    } else if constexpr (!EXACT) {
         // issued before the pixel loads, so waiting for it does not wait for them
         for (int i = tid; i < 3 * NN + 9; i += TPB) srow[i] = tab->srow[i];
     }
@@ -714,7 +730,9 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     uint32_t seg[N][WPR];
     if constexpr (kLdsPix) {
         static_assert(BPT == 4 && WPR == 4 && TPB % 64 == 0, "LDS pixel layout: 16 bytes per lane per row");
-        if (!__ballot(!(a.vec_ok && nblk == BPT))) {  // every group of the wave is whole: DMA
+        if (kProf && (ablate & 4096)) {
+            // profiling: no pixel loads at all (the LDS holds whatever the previous tile left)
+        } else if (!__ballot(!(a.vec_ok && nblk == BPT))) {  // every group of the wave is whole: DMA
             const uint8_t* base =
                 a.y + size_t(frame) * a.frame_pitch + size_t(byi) * N * a.stride + size_t(bx0) * N;
 #pragma unroll
@@ -742,6 +760,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     if constexpr (kLdsPix) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
 
     asm volatile("; PHASE load_done" ::: "memory");
+    if (kProf && (ablate & 512)) return;  // profiling: instruction count of the prologue + load alone
     if (stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
         uint32_t acc = 0;
 #pragma unroll
@@ -798,6 +817,15 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         }
     }
     asm volatile("; PHASE quant_done" ::: "memory");
+    if (kProf && (ablate & 1024)) {  // profiling: ... + transform + rounding (keep the results live)
+        uint32_t acc = flags;
+#pragma unroll
+        for (int b = 0; b < BPT; b++)
+#pragma unroll
+            for (int j = 0; j < NP; j++) acc ^= zp[b][j];
+        if (acc == 0x9E3779B9u) a.err[1] = acc;
+        return;
+    }
     STAMP(3);
 
     // ---------------------------------------------------------------- 1b. FP64 fix-up
@@ -973,10 +1001,12 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                     const uint32_t tk = task[lane];
                     const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
                     const BlockPx<N> px = block_px(b, owner);
+                    const int ks = kFullRows ? Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) +
+                                                   Structural<N>::k[2] * (s == 2)
+                                             : s;
                     res[lane] = (ablate & 256) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
-                                                 : uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s],
-                                                                              srow[3 * NN + 3 + s], srow[3 * NN + 6 + s],
-                                                                              px)) & 0xFFFFu;
+                                                 : uint32_t(exact_coef_row<N>(rowP(ks), rowS(ks), rowRq(ks),
+                                                                              rowQd(ks), px)) & 0xFFFFu;
                 }
                 wave_sync();
                 m = sf;
@@ -1026,8 +1056,9 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                         const uint32_t tk = task[lane >> 4];
                         const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
                         const BlockPx<N> px = block_px(b, owner);
-                        res[lane] = uint32_t(exact_coef_row<N>(tab->P + k * NN, tab->S[k], tab->rq[k], tab->qd[k], px)) &
-                                    0xFFFFu;
+                        res[lane] = uint32_t(kFullRows ? exact_coef_row<N>(rowP(k), rowS(k), rowRq(k), rowQd(k), px)
+                                                       : exact_coef_row<N>(tab->P + k * NN, tab->S[k], tab->rq[k],
+                                                                           tab->qd[k], px)) & 0xFFFFu;
                     }
                     wave_sync();
                     m = wf;
@@ -1069,8 +1100,10 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                         for (int bb = 1; bb < BPT; bb++) v = (b == bb) ? seg[r][(bb * N) / 4 + m] : v;
                         px.w[r * (N / 4) + m] = v;
                     }
-                const uint32_t v = uint32_t(exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
-                                                              srow[3 * NN + 6 + s], px)) & 0xFFFFu;
+                const int ks = kFullRows ? Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) +
+                                               Structural<N>::k[2] * (s == 2)
+                                         : s;
+                const uint32_t v = uint32_t(exact_coef_row<N>(rowP(ks), rowS(ks), rowRq(ks), rowQd(ks), px)) & 0xFFFFu;
 #pragma unroll
                 for (int bb = 0; bb < BPT; bb++)
 #pragma unroll
@@ -1134,6 +1167,15 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         mybits += rbits[b];
     }
     asm volatile("; PHASE size_done" ::: "memory");
+    if (kProf && (ablate & 2048)) {  // profiling: ... + FP64 fix-up + sizing
+        uint32_t acc = mybits;
+#pragma unroll
+        for (int b = 0; b < BPT; b++)
+#pragma unroll
+            for (int j = 0; j < NP; j++) acc ^= zp[b][j] + blw[b];
+        if (acc == 0x9E3779B9u) a.err[1] = acc;
+        return;
+    }
     STAMP(5);
     // (the fix-up slots alias the tile image: the scan's barrier below orders them before the
     // image is zeroed)
@@ -1249,8 +1291,8 @@ void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s) {
     a.img_words = image_words_for(4, 4, IE_STATIC_IMG4);
     const size_t lds = 0;
 #else
-    const size_t lds = (size_t(a.img_words) + 32 + (a.hist ? 256 : 0)) * sizeof(uint32_t) +
-                       (exact ? 0 : size_t(3 * n * n + 9) * sizeof(double));
+    const size_t rows = exact ? 0 : (n == 4 ? size_t(n * n * n * n + 3 * n * n) : size_t(3 * n * n + 9));
+    const size_t lds = (size_t(a.img_words) + 32 + (a.hist ? 256 : 0)) * sizeof(uint32_t) + rows * sizeof(double);
 #endif
     const dim3 grid(a.ntiles), block(kEncTPB);
     if (a.hist) {  // segmented 4x4 FAST launches only (ie_encode_images_counted; 8x8 would spill)

@@ -10,8 +10,8 @@
 //   dc::VideoProcessor            VideoBase.hpp:17-48       base of the video encoder / decoder
 //   algo::Huffman                 Huffman.hpp:109-142       byte Huffman post-pass (tree on the host)
 //   dc::ImageEncoder/ImageDecoder ImageEncoder.hpp, ImageDecoder.hpp
-//   dc::VideoEncoder/VideoDecoder VideoEncoder.hpp, VideoDecoder.hpp (the encoder takes any gop;
-//                                 the decoder reads gop = 1 streams)
+//   dc::VideoEncoder/VideoDecoder VideoEncoder.hpp, VideoDecoder.hpp (any gop: I-frames and
+//                                 P-frames with motion compensation on / off, ie_decode_gop)
 // Every block-level operation (DCT, quantisation, RLE, bit packing, the inverse) runs on the
 // GPU; there is no CPU fallback.
 #pragma once

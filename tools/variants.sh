@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   d=build/var_$name; mkdir -p $d
-  for k in ie_encode ie_huffman ie_decode ie_capi; do
+  for k in ie_encode ie_huffman ie_decode ie_pframe ie_capi; do
     src=imageencoder_amd/csrc/$k.hip; [ -f $src ] || src=imageencoder_amd/csrc/$k.cpp
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -mcode-object-version=5 -O3 -std=c++17 -fPIC -Iinclude -Iimageencoder_amd/csrc -ffp-contract=off $flags -c $src -o $d/$k.o &
   done
