@@ -46,6 +46,8 @@ struct ie_ctx {
     int last_fix_words = 0;
     unsigned err_seen[66] = {};         // counter values at the previous read
     bool use_ticket = false;            // order tiles with an atomic ticket (after a timeout)
+    hipEvent_t stage_ev[4] = {};        // timing events around the last batched histogram [0,1] / pack [2,3]
+    bool stage_rec[2] = {false, false};
     int fake_timeouts = 0;              // debug (IE_FAKE_TIMEOUTS): report this many look-back timeouts
     bool fake_fired = false;            // a faked timeout was reported (the redo paths dirty the output first)
     // Asynchronous launches (no read-back) since the last error read: a look-back timeout found
@@ -389,6 +391,14 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
 // [0] look-back timeouts; sum of [2..65] = FP64 re-evaluations.  Synchronises the stream.
 // The device counters only ever grow (no per-launch reset kernel in the launch path); a read
 // reports the increments since the previous read.
+// Timing marks around the batched Huffman stages (ie_last_stage_ms): event i on the context's stream.
+int stage_mark(ie_ctx* c, int i) {
+    if (!c->stage_ev[i]) HIPCHK(c, hipEventCreate(&c->stage_ev[i]));
+    HIPCHK(c, hipEventRecord(c->stage_ev[i], c->stream));
+    if (i & 1) c->stage_rec[i >> 1] = true;
+    return IE_OK;
+}
+
 int read_errors(ie_ctx* c, unsigned* timeouts, uint64_t* fallbacks) {
     unsigned e[kErrWords];
     HIPCHK(c, hipMemcpyAsync(e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
@@ -1363,7 +1373,9 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
         a.chain_end = c->d_chain_end;
         a.err = c->d_err;
         a.maxlen = int(maxlen);
+        if ((r = stage_mark(c, 2))) return r;
         ie::launch_pack(a, c->stream);
+        if ((r = stage_mark(c, 3))) return r;
         HIPCHK(c, hipGetLastError());
         if (c->use_ticket) c->ticket_base += uint64_t(ntiles);
         if (!end_bit && out_dev) {
@@ -1459,6 +1471,8 @@ int ie_destroy(ie_ctx* c) {
         if (c->ev_hist[i]) (void)hipEventDestroy(c->ev_hist[i]);
         if (c->ev_pack[i]) (void)hipEventDestroy(c->ev_pack[i]);
     }
+    for (hipEvent_t e : c->stage_ev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipFree(c->d_first);
     (void)hipFree(c->d_dec);
     (void)hipFree(c->d_walk);
@@ -1514,6 +1528,14 @@ int ie_set_quant(ie_ctx* c, const uint16_t* q, int n) {
     HIPCHK(c, hipMemcpy(c->d_tab, c->h_tab, sizeof(ie::EncTables), hipMemcpyHostToDevice));
     c->n = n;
     std::memcpy(c->q, q, sizeof(uint16_t) * n * n);
+    return IE_OK;
+}
+
+int ie_last_stage_ms(ie_ctx* c, int stage, float* ms) {
+    if (!c || !ms || stage < 0 || stage > 1) return IE_EINVAL;
+    if (!c->stage_rec[stage]) return fail(c, IE_EINVAL, "no batched Huffman stage recorded yet");
+    HIPCHK(c, hipEventSynchronize(c->stage_ev[2 * stage + 1]));
+    HIPCHK(c, hipEventElapsedTime(ms, c->stage_ev[2 * stage], c->stage_ev[2 * stage + 1]));
     return IE_OK;
 }
 
@@ -1952,9 +1974,11 @@ int ie_huffman_hist_batch_ends_async(ie_ctx* c, const uint8_t* in, size_t in_pit
     auto* df = reinterpret_cast<unsigned long long*>(c->d_batch + hb);
     auto* dn = reinterpret_cast<uint64_t*>(c->d_batch + hb + fb);
     auto* du = reinterpret_cast<unsigned*>(c->d_batch + hb + fb + nb);
+    if ((r = stage_mark(c, 0))) return r;
     ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream, fused ? nullptr : dh, df);
     ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream, !fused);
     HIPCHK(c, hipGetLastError());
+    if ((r = stage_mark(c, 1))) return r;
     // histograms and first positions are contiguous on the device: one read-back
     HIPCHK(c, hipMemcpyAsync(c->h_hist[slot], c->d_batch, hb + fb, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_hist[slot], c->stream));

@@ -730,7 +730,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     uint32_t seg[N][WPR];
     if constexpr (kLdsPix) {
         static_assert(BPT == 4 && WPR == 4 && TPB % 64 == 0, "LDS pixel layout: 16 bytes per lane per row");
-        if (kProf && (ablate & 4096)) {
+        if (IE_PROFILE && (ablate & 4096)) {
             // profiling: no pixel loads at all (the LDS holds whatever the previous tile left)
         } else if (!__ballot(!(a.vec_ok && nblk == BPT))) {  // every group of the wave is whole: DMA
             const uint8_t* base =
@@ -760,7 +760,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     if constexpr (kLdsPix) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
 
     asm volatile("; PHASE load_done" ::: "memory");
-    if (kProf && (ablate & 512)) return;  // profiling: instruction count of the prologue + load alone
+    if (IE_PROFILE && (ablate & 512)) return;  // profiling: instruction count of the prologue + load alone
     if (stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
         uint32_t acc = 0;
 #pragma unroll
@@ -817,7 +817,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         }
     }
     asm volatile("; PHASE quant_done" ::: "memory");
-    if (kProf && (ablate & 1024)) {  // profiling: ... + transform + rounding (keep the results live)
+    if (IE_PROFILE && (ablate & 1024)) {  // profiling: ... + transform + rounding (keep the results live)
         uint32_t acc = flags;
 #pragma unroll
         for (int b = 0; b < BPT; b++)
@@ -1167,7 +1167,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         mybits += rbits[b];
     }
     asm volatile("; PHASE size_done" ::: "memory");
-    if (kProf && (ablate & 2048)) {  // profiling: ... + FP64 fix-up + sizing
+    if (IE_PROFILE && (ablate & 2048)) {  // profiling: ... + FP64 fix-up + sizing
         uint32_t acc = mybits;
 #pragma unroll
         for (int b = 0; b < BPT; b++)

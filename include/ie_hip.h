@@ -229,6 +229,11 @@ int ie_huffman_pack_batch(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const
                           const uint32_t* code, const uint8_t* len, const uint8_t* prefix, size_t prefix_pitch,
                           uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit);
 
+/* Device time of the last batched Huffman stage on the context's stream (HIP events around its
+ * launches): stage 0 = the histogram / first-occurrence kernels of ie_huffman_hist_batch_ends_async,
+ * stage 1 = the pack kernel of ie_huffman_pack_batch.  Waits for the stage to finish. */
+int ie_last_stage_ms(ie_ctx* ctx, int stage, float* ms);
+
 /* Copy n bytes into out starting at bit start_bit, i.e. shifted by start_bit % 8 (the "no gain"
  * path of Huffman.cpp:329-341 writes '0' + the input: start_bit = 1).  Device input and output:
  * asynchronous on the context's stream, like an encode without sizes (checked at ie_sync). */

@@ -40,3 +40,36 @@ def test_contracted_fma_inside_division_window_fails(tmp_path):
 def test_fma_outside_any_division_fails(tmp_path):
     r = _run(tmp_path, "\tv_fmac_f64_e32 v[2:3], v[4:5], v[6:7]\n" + DIV.format(inject=""))
     assert r.returncode == 1
+
+
+def _budget_asm(occ, scratch):
+    name = "_ZN2ie13encode_kernelILi8ELb0ELb0EEEvNS_7EncArgsEPKNS_9EncTablesE"
+    return (f"{name}:\n\ts_endpgm\n; NumVgprs: 121\n; ScratchSize: {scratch}\n; Occupancy: {occ}\n")
+
+
+def test_register_budget_holds(tmp_path):
+    p = tmp_path / "k.s"
+    p.write_text(_budget_asm(4, 68))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asmcheck.py"), str(p)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+
+
+def test_spilling_kernel_over_budget_fails(tmp_path):
+    p = tmp_path / "k.s"
+    p.write_text(_budget_asm(4, 308))  # the spill an unguarded profiling branch once caused
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asmcheck.py"), str(p)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "over budget" in r.stderr
+
+
+def test_built_kernels_within_budget():
+    """The in-tree build's assembly (make asm, run by build()) meets the budgets."""
+    import glob
+    import pytest
+    files = sorted(glob.glob(os.path.join(ROOT, "build", "asm", "*.s")))
+    if not files:
+        pytest.skip("no build/asm (run __graft_entry__.build())")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asmcheck.py")] + files,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -91,6 +91,15 @@ def static_lds(path):
     return out
 
 
+# Register budgets of the hot kernels (occupancy >= waves per SIMD, scratch bytes <= limit): a
+# change that makes the compiler spill or drop a wave shows up in the CPU build, not only on a GPU
+# (an unguarded profiling branch once took the 8x8 kernel from 68 to 308 B of scratch, 2x slower).
+BUDGETS = {
+    "_ZN2ie13encode_kernelILi4ELb0ELb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (5, 0),
+    "_ZN2ie13encode_kernelILi8ELb0ELb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (4, 96),
+}
+
+
 def main(paths):
     rc = 0
     for p in paths:
@@ -101,6 +110,12 @@ def main(paths):
                 rc = 1
                 print(f"{p}: {name} allocates {size} B of static LDS (scatter_bits assumes 0)", file=sys.stderr)
         bad, kernels = scan(p)
+        for name, (waves, scratch) in BUDGETS.items():
+            info = kernels.get(name)
+            if info and (info.get("Occupancy", 0) < waves or info.get("ScratchSize", 0) > scratch):
+                rc = 1
+                print(f"{p}: {name[:60]} over budget: occupancy {info.get('Occupancy')} (>= {waves}), "
+                      f"scratch {info.get('ScratchSize')} B (<= {scratch})", file=sys.stderr)
         for name, info in kernels.items():
             if info:
                 print(f"{p}: {name[:70]:70s} vgpr={info.get('NumVgprs')} scratch={info.get('ScratchSize')} "
