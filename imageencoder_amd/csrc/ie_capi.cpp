@@ -2092,7 +2092,9 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         a.prefix_pitch_words = pw;
         a.prefix = reinterpret_cast<const uint32_t*>(d + o_pre);
         a.maxlen = int(maxlen_all);
+        if ((r = stage_mark(c, 2))) return r;
         ie::launch_pack(a, c->stream);
+        if ((r = stage_mark(c, 3))) return r;
         HIPCHK(c, hipGetLastError());
         if (c->use_ticket) c->ticket_base += ntiles;
     }
@@ -2363,6 +2365,16 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
         pa.stats = reinterpret_cast<unsigned long long*>(c->d_misc + 3);  // [3..7]
         HIPCHK(c, hipMemsetAsync(c->d_misc + 3, 0, 5 * sizeof(uint64_t), c->stream));
     }
+    static const char* dstamps = getenv("IE_DEC_STAMPS");  // file: [table waves][8] u64 per call
+    uint64_t* d_ws = nullptr;
+    int tm_ = 1, hb_ = 0;
+    ie::rec_table_geometry(uint32_t(C), n, &tm_, &hb_);
+    const size_t nws = size_t(nchunks + tm_ - 1) / size_t(tm_) * 8;
+    if (dstamps) {
+        HIPCHK(c, hipMalloc(&d_ws, nws * 8));
+        HIPCHK(c, hipMemsetAsync(d_ws, 0, nws * 8, c->stream));
+        pa.wstamp = reinterpret_cast<unsigned long long*>(d_ws);
+    }
 #endif
     if (ie::launch_rec_parse_decode(pa, da, n, c->stream) < 0) return fail(c, IE_EINVAL, "stream too long for one decode call");
     HIPCHK(c, hipGetLastError());
@@ -2380,6 +2392,15 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
                 "wave max steps avg %.1f max %llu\n", nchunks, unsigned(C), double(st[0]) / nchunks, double(st[1]) / nchunks,
                 double(st[2]) / nchunks, double(st[3]) / nchunks, (unsigned long long)st[4]);
         HIPCHK(c, hipMemsetAsync(c->d_misc + 3, 0, sizeof(uint64_t), c->stream));
+    }
+    if (d_ws) {
+        std::vector<uint64_t> hws(nws);
+        HIPCHK(c, hipMemcpy(hws.data(), d_ws, nws * 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipFree(d_ws));
+        if (FILE* f = fopen(dstamps, "ab")) {
+            fwrite(hws.data(), 8, nws, f);
+            fclose(f);
+        }
     }
 #endif
     if (hm[2] < nblocks || end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");

@@ -19,8 +19,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "ie_common.hpp"
 #include "ie_device.h"
+#include "ie_recbits.h"
 
 namespace ie {
 
@@ -338,6 +342,15 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
     __shared__ uint16_t tgt[E];
     const int lane = threadIdx.x, k0 = blockIdx.x * M;
     const int m = min(M, a.nchunks - k0);           // chunks of this wave
+#if IE_PROFILE  // per-wave phase times (IE_DEC_STAMPS): realtime (100 MHz) and cycle counters
+    unsigned long long* ws = a.wstamp ? a.wstamp + size_t(blockIdx.x) * 8 : nullptr;
+    auto wstamp = [&](int i) {
+        if (ws && lane == 0) ws[i] = __builtin_amdgcn_s_memrealtime();
+    };
+    wstamp(0);
+#else
+    auto wstamp = [](int) {};
+#endif
     const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
     const uint64_t base = c0 & ~31ull;
     const uint32_t s0 = uint32_t(c0 - base), C = a.C, CW = C >> 5;
@@ -347,6 +360,7 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
     stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, (a.nbits + 31) >> 5, lane, 64);
     for (int i = lane; i < M * HS; i += 64) (&H[0][0])[i] = 0xFFFFFFFFu;
     __syncthreads();
+    wstamp(1);
     // 1. valid headers of every position (the 32 headers of a word from one 64-bit window)
     for (uint32_t i = lane; i < uint32_t(m) * CW; i += 64) {
         const uint32_t p0 = s0 + (i << 5);
@@ -364,6 +378,7 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
         VB[i] = msk;
     }
     __syncthreads();
+    wstamp(2);
     // 2. the walks
     {
         // entry e is offset e / M of chunk e % M: the first offsets of all M chunks -- where
@@ -424,6 +439,18 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
         (void)nsteps;
         (void)nwin;
         (void)nbey;
+#if IE_PROFILE
+        if (ws) {
+            const uint32_t mx = __reduce_max_sync(~0ull, nsteps);
+            const uint32_t sm = __reduce_add_sync(~0ull, nsteps);
+            if (lane == 0) {
+                ws[6] = (uint64_t(mx) << 32) | sm;
+                uint32_t hw;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                ws[7] = hw;
+            }
+        }
+#endif
 #if IE_PROFILE  // walk statistics (IE_DEC_STATS in a profiling build)
         if (a.stats) {
             const uint32_t mx = __reduce_max_sync(~0ull, nsteps);
@@ -435,6 +462,7 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
 #endif
     }
     __syncthreads();
+    wstamp(3);
     // 3. an entry takes its owner's exit once the owner is resolved; else it jumps to its owner's
     //    owner (owner chains climb to strictly later positions, so they end; pointer jumping
     //    halves them every round)
@@ -472,8 +500,10 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
         }
         if (!__syncthreads_or(pend)) break;
     }
+    wstamp(4);
     uint16_t* T = a.tab + size_t(k0) * D;
     for (int e = lane; e < m * D; e += 64) T[e] = res[e];
+    wstamp(5);
 }
 
 // One composition level over n tables ([n][D], 16-bit exits): prefix maps written over the
@@ -620,6 +650,217 @@ __device__ __forceinline__ int stage_words16(uint32_t* L, const uint32_t* W, uin
     return off;
 }
 
+// Table pass, round 3: one wave tabulates tm consecutive chunks (runtime, rec_table_geometry) and
+// walks only from positions where a record can start.  Entry d of a chunk first slides to the next
+// valid position nv(d) -- every entry between two valid positions shares one walk -- so the walks
+// start at the valid positions of [0, min(D, C)) plus, for the entries past the last of them, the
+// first valid position after (v*, entry slot D of the chunk).  The walk list is compacted from the
+// bitmap and lanes take walks from it as theirs end, across all tm chunks, so a wave's 64 lanes
+// carry several chunks' surviving walks side by side.  Claims: one open-addressing table per wave,
+// keyed by the wave-relative position (walks of different chunks never meet: a walk stops at its
+// chunk's end).  Results: a walk that merged takes its owner's exit (owner chains are read-only
+// chases; only non-roots are written).  The valid-header bitmap comes 32 positions at a time from
+// bitwise operations on shifted windows (valid_mask32, ie_recbits.h).
+template <int N>
+__device__ __forceinline__ uint32_t next_valid(const uint32_t* VB, uint32_t p, uint32_t ce) {
+    if (p >= ce) return p;
+    uint32_t wi = p >> 5, msk = VB[wi] & (0xFFFFFFFFu << (p & 31u));
+    const uint32_t wend = ce >> 5;
+    while (!msk && ++wi < wend) msk = VB[wi];
+    return msk ? (wi << 5) + uint32_t(__builtin_ctz(msk)) : ce;
+}
+
+__host__ __device__ constexpr int rec_table2_words(uint32_t C, int D, int tm, int hbits) {
+    // L (stream words, 16-byte aligned staging: +4), VB, claims, then u16 res / tgt and u32 walk list
+    return (rec_table_stream_words(uint32_t(tm) * C) + 4 + 3) / 4 * 4 + tm * int(C >> 5) + (1 << hbits) +
+           2 * tm * (D + 1);
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
+    constexpr int D = RecGeom<N>::D, D1 = D + 1;
+    extern __shared__ __attribute__((aligned(16))) uint32_t Ls[];
+    const int lane = threadIdx.x, tm = a.tm;
+    const int k0 = blockIdx.x * tm;
+    const int m = min(tm, a.nchunks - k0);
+    const uint32_t C = a.C, CW = C >> 5;
+#if IE_PROFILE
+    unsigned long long* ws = a.wstamp ? a.wstamp + size_t(blockIdx.x) * 8 : nullptr;
+    auto wstamp = [&](int i) {
+        if (ws && lane == 0) ws[i] = __builtin_amdgcn_s_memrealtime();
+    };
+    wstamp(0);
+#else
+    auto wstamp = [](int) {};
+#endif
+    const int SW = (rec_table_stream_words(uint32_t(tm) * C) + 4 + 3) / 4 * 4;
+    uint32_t* L = Ls;
+    uint32_t* VB = Ls + SW;
+    uint32_t* H = VB + tm * int(CW);
+    const uint32_t HM = (1u << a.hbits) - 1u;
+    uint16_t* res = reinterpret_cast<uint16_t*>(H + HM + 1);
+    uint16_t* tgt = res + tm * D1;
+    uint32_t* wl = H + HM + 1 + tm * D1;  // after res + tgt (tm * D1 words together)
+    const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
+    const uint64_t base = c0 & ~31ull;
+    const int off = stage_words16(L, a.words, base >> 5, int(((c0 - base) + uint64_t(m) * C + 64) >> 5) + 2,
+                                  (a.nbits + 31) >> 5, lane);
+    const uint32_t s0 = uint32_t(c0 - base) + 32u * uint32_t(off);  // the wave's first bit in L
+    // positions below are relative to s0; no record starts at or past the stream's end
+    const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - c0, uint64_t(m) * C));
+    for (uint32_t i = lane; i <= HM; i += 64) H[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    wstamp(1);
+    // 1. valid-header bitmap, 32 positions per word
+    for (uint32_t i = lane; i < uint32_t(m) * CW; i += 64) {
+        const uint32_t p0 = i << 5;
+        uint32_t msk = 0;
+        if (p0 < lim) {
+            const uint32_t q = s0 + p0, w0 = q >> 5, sb = q & 31u;
+            const uint64_t v = (((uint64_t(L[w0]) << 32) | L[w0 + 1]) << sb) |
+                               (sb ? (uint64_t(L[w0 + 2]) >> (32 - sb)) : 0ull);
+            msk = valid_mask32<N>(v, a.rle);
+            const uint32_t cut = lim - p0;
+            if (cut < 32u) msk &= (1u << cut) - 1u;
+        }
+        VB[i] = msk;
+    }
+    __syncthreads();
+    wstamp(2);
+    // 2. the walk list: valid positions of [0, min(D, C)) of every chunk, then every chunk's v*
+    const uint32_t De = min(uint32_t(D), C), DW = (De + 31) >> 5;
+    uint32_t nw = 0;  // (wave-uniform)
+    for (uint32_t i0 = 0; i0 < uint32_t(m) * DW; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        uint32_t bits = 0, j = 0, w = 0;
+        if (i < uint32_t(m) * DW) {
+            j = i / DW;
+            w = i - j * DW;
+            bits = VB[j * CW + w];
+            const uint32_t rem = De - (w << 5);
+            if (rem < 32u) bits &= (1u << rem) - 1u;
+        }
+        const uint32_t cnt = __popc(bits);
+        uint32_t incl = cnt;  // inclusive scan over the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += o;
+        }
+        uint32_t at = nw + incl - cnt;
+        while (bits) {
+            const uint32_t b = __builtin_ctz(bits);
+            bits &= bits - 1u;
+            const uint32_t pos = j * C + (w << 5) + b;
+            wl[at++] = (pos << 16) | (j * D1 + (w << 5) + b);
+        }
+        nw += __shfl(incl, 63, 64);
+    }
+    {
+        uint32_t vs = 0xFFFFFFFFu;
+        if (lane < m && De < C) {
+            const uint32_t cs = uint32_t(lane) * C, ce = cs + C;
+            const uint32_t v = next_valid<N>(VB, cs + De, ce);
+            if (v < ce) vs = v;
+        }
+        const uint64_t bm = __ballot(vs != 0xFFFFFFFFu);
+        if (vs != 0xFFFFFFFFu) {
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u));
+            wl[nw + r] = (vs << 16) | (uint32_t(lane) * D1 + D);
+        }
+        nw += uint32_t(__popcll(bm));
+    }
+    __syncthreads();
+    wstamp(3);
+    // 3. the walks: lanes take the next walk of the list as theirs ends
+    {
+        uint32_t nxt = 0, p = 0, id = 0, ce = 0, nsteps = 0;
+        bool act = false;
+        for (;;) {
+            const uint64_t need = __ballot(!act);
+            if (!act) {
+                const uint32_t r = nxt + __builtin_amdgcn_mbcnt_hi(uint32_t(need >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(need), 0u));
+                if (r < nw) {
+                    const uint32_t e = wl[r];
+                    p = e >> 16;
+                    id = e & 0xFFFFu;
+                    ce = (id / D1 + 1u) * C;
+                    act = true;
+                }
+            }
+            nxt += uint32_t(__popcll(need));
+            if (!__ballot(act)) break;
+            if (act) {
+                nsteps++;
+                if (p >= ce) {  // left the chunk
+                    res[id] = uint16_t(p - ce);
+                    tgt[id] = uint16_t(kNoOwner);
+                    act = false;
+                } else {
+                    // the record's header read before the claim (independent of it, so both LDS
+                    // round trips overlap)
+                    const uint32_t head = lbits(L, s0 + p, 20);
+                    const uint32_t key = (p << 16) | id;
+                    uint32_t h = (p * 2654435761u) >> 16 & HM;
+                    uint32_t own = kNoOwner;
+                    for (int probe = 0; probe < 8; probe++) {
+                        const uint32_t o = atomicCAS(&H[h], 0xFFFFFFFFu, key);
+                        if (o == 0xFFFFFFFFu) break;                          // claimed
+                        if ((o >> 16) == p) { own = o & 0xFFFFu; break; }     // owned: merge
+                        h = (h + 1u) & HM;                                    // (a full table: walk on)
+                    }
+                    if (own != kNoOwner) {
+                        tgt[id] = uint16_t(own);
+                        act = false;
+                    } else {
+                        p += rec_len_head<N>(head, a.rle);  // p is valid: a record starts here
+                        p = next_valid<N>(VB, p, ce);
+                    }
+                }
+            }
+        }
+#if IE_PROFILE
+        if (ws) {
+            const uint32_t mx = __reduce_max_sync(~0ull, nsteps);
+            const uint32_t sm = __reduce_add_sync(~0ull, nsteps);
+            if (lane == 0) {
+                ws[6] = (uint64_t(mx) << 32) | sm;
+                uint32_t hw;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                ws[7] = hw;
+            }
+        }
+#endif
+        (void)nsteps;
+    }
+    __syncthreads();
+    wstamp(4);
+    // 4. merged walks take their root's exit (read-only chases; only non-roots are written)
+    for (uint32_t r = lane; r < nw; r += 64) {
+        const uint32_t id = wl[r] & 0xFFFFu;
+        uint32_t x = tgt[id];
+        if (x == kNoOwner) continue;
+        for (uint32_t y = tgt[x]; y != kNoOwner; y = tgt[x]) x = y;
+        res[id] = res[x];
+    }
+    __syncthreads();
+    // 5. every entry: its walk's exit
+    uint16_t* T = a.tab + size_t(k0) * D;
+    for (uint32_t e = lane; e < uint32_t(m) * D; e += 64) {
+        const uint32_t j = e / D, d = e - j * D;
+        uint32_t out;
+        if (d >= C) {
+            out = d - C;
+        } else {
+            const uint32_t cs = j * C, ce = cs + C;
+            const uint32_t nv = next_valid<N>(VB, cs + d, ce);
+            out = (nv >= ce) ? nv - ce : res[j * D1 + min(nv - cs, uint32_t(D))];
+        }
+        T[e] = uint16_t(out);
+    }
+    wstamp(5);
+}
+
 // Count pass: each wave stages `seg` consecutive chunks' bits in LDS and one lane per chunk walks
 // its true records from its entry (the prefix maps applied to its top-level entry), storing up to
 // kRecPosCap record positions (relative to the chunk's first word) and the count; the workgroup
@@ -732,6 +973,19 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
 
 int rec_group_chunks(int n) { return n == 4 ? RecGeom<4>::G : RecGeom<8>::G; }
 int rec_entry_span(int n) { return n == 4 ? RecGeom<4>::D : RecGeom<8>::D; }
+int rec_table_chunks(int n) { return n == 4 ? RecGeom<4>::M : RecGeom<8>::M; }
+// chunks per table wave and claim slots: tm chunks' positions fit the 16-bit claim keys; the
+// claim table holds about twice the walk steps of tm chunks (IE_REC_TM / IE_REC_HB override)
+void rec_table_geometry(uint32_t C, int n, int* tm, int* hbits) {
+    static const char* et = getenv("IE_REC_TM");
+    static const char* eh = getenv("IE_REC_HB");
+    int t = et ? atoi(et) : 2;
+    while (t > 1 && uint64_t(t) * C > 65535u) t--;
+    t = std::max(1, t);
+    int hb = eh ? atoi(eh) : ((n == 4 ? 9 : 11) + (t >= 4 ? 2 : t >= 2 ? 1 : 0));
+    *tm = t;
+    *hbits = std::min(14, std::max(6, hb));
+}
 size_t rec_table_lds(uint32_t C, int n) {
     const int M = n == 4 ? RecGeom<4>::M : RecGeom<8>::M;
     return size_t(rec_table_stream_words(uint32_t(M) * C) + M * (C >> 5)) * 4;
@@ -742,8 +996,17 @@ int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t
     if (a.nchunks <= 0) return 0;
     const int nb = (a.nchunks + kRecWPB - 1) / kRecWPB;  // blocks of kRecWPB chunk waves
     const int nt = (a.nchunks + RecGeom<4>::M - 1) / RecGeom<4>::M;  // table waves (M chunks each)
+#if IE_REC_V1
     if (n == 4) hipLaunchKernelGGL((rec_table_kernel<4>), dim3(nt), dim3(64), rec_table_lds(a.C, 4), s, a);
     else hipLaunchKernelGGL((rec_table_kernel<8>), dim3(nt), dim3(64), rec_table_lds(a.C, 8), s, a);
+#else
+    (void)nt;
+    rec_table_geometry(a.C, n, &a.tm, &a.hbits);
+    const int nt2 = (a.nchunks + a.tm - 1) / a.tm;
+    const size_t l2 = size_t(rec_table2_words(a.C, rec_entry_span(n), a.tm, a.hbits)) * 4;
+    if (n == 4) hipLaunchKernelGGL((rec_table2_kernel<4>), dim3(nt2), dim3(64), l2, s, a);
+    else hipLaunchKernelGGL((rec_table2_kernel<8>), dim3(nt2), dim3(64), l2, s, a);
+#endif
     const int levels = (n == 4) ? launch_compose<RecGeom<4>::D, RecGeom<4>::G>(a.tab, a.nchunks, a.E, a.ticket + 1, a.lvl, s)
                                 : launch_compose<RecGeom<8>::D, RecGeom<8>::G>(a.tab, a.nchunks, a.E, a.ticket + 1, a.lvl, s);
     if (levels < 0) return -1;

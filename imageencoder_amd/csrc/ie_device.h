@@ -188,9 +188,15 @@ struct RecParseArgs {
     uint64_t* total;        // records on the true path
     uint64_t* end_out;      // end bit of the last block's record
     unsigned long long* stats;  // diagnostics (IE_DEC_STATS): walk steps; nullptr = off
+    unsigned long long* wstamp; // diagnostics (IE_DEC_STAMPS): [table waves][8] phase times; nullptr = off
+    int tm;                 // chunks per table wave (rec_table_geometry)
+    int hbits;              // log2 of a table wave's claim slots
 };
+// Table-wave geometry for chunks of C bits: chunks per wave (tm) and log2 claim slots (hbits).
+void rec_table_geometry(uint32_t C, int n, int* tm, int* hbits);
 int rec_group_chunks(int n);
 int rec_entry_span(int n);
+int rec_table_chunks(int n);  // chunks per table wave
 size_t rec_table_lds(uint32_t C, int n);
 size_t rec_decode_lds(uint32_t C, int n);
 int rec_count_seg(uint32_t C);
