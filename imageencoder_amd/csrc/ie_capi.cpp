@@ -101,6 +101,8 @@ struct ie_ctx {
     size_t cap_rpos = 0;
     uint64_t* d_misc = nullptr;        // [0] end bit, [1] changed / invalid flags or decode tickets, [2] symbol /
                                        // record count, [3] histogram ticket
+    uint64_t* h_decres = nullptr;      // record decode results, pinned host memory the device writes
+    uint64_t* d_decres = nullptr;      // directly ([0] end bit, [1] record total): no read-back copy
     uint16_t* d_hlut = nullptr;        // Huffman decode prefix table (32768 entries)
     size_t cap_hlut = 0;
     uint8_t* d_hout = nullptr;         // Huffman decode output staging (host destinations)
@@ -1480,6 +1482,7 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_rtab);
     (void)hipFree(c->d_rpos);
     (void)hipFree(c->d_misc);
+    if (c->h_decres) (void)hipHostFree(c->h_decres);
     (void)hipFree(c->d_hlut);
     (void)hipFree(c->d_hout);
     (void)hipFree(c->d_pix);
@@ -2264,13 +2267,7 @@ int finish_decode(ie_ctx* c, uint8_t* out, const uint8_t* dpix, bool out_dev, in
     if (end_bit) *end_bit = end;
     return IE_OK;
 }
-}  // namespace
 
-extern "C" {
-
-}  // extern "C"
-
-namespace {
 // add_base: P-frame error -- the decoded error is added to the pixels already in `out`
 int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,
                        int use_rle, uint8_t* out, size_t stride, size_t frame_pitch, uint64_t* end_bit, int add_base) {
@@ -2282,12 +2279,18 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     if (start_bit > uint64_t(len) * 8) return fail(c, IE_EINVAL, "start_bit beyond the stream");
     HIPCHK(c, hipSetDevice(c->device));
     const int n = c->n;
-    // stream: staged (device copy or H2D) with two zero words of padding for the bit reader
-    const size_t padded = (len + 3) / 4 * 4 + 16;
-    if ((r = ensure(c, c->d_dec, c->cap_dec, padded))) return r;
-    HIPCHK(c, hipMemsetAsync(c->d_dec + (len / 4) * 4, 0, padded - (len / 4) * 4, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_dec, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                             c->stream));
+    // stream: a 4-byte aligned device stream is read in place (the kernels read whole aligned words
+    // up to the one holding the last byte -- never past its page -- and clear the bits past the
+    // stream themselves); anything else is staged (device copy or H2D) with zero padding
+    const uint8_t* words = in;
+    if (!is_device_ptr(in) || (reinterpret_cast<uintptr_t>(in) & 3u)) {
+        const size_t padded = (len + 3) / 4 * 4 + 16;
+        if ((r = ensure(c, c->d_dec, c->cap_dec, padded))) return r;
+        HIPCHK(c, hipMemsetAsync(c->d_dec + (len / 4) * 4, 0, padded - (len / 4) * 4, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_dec, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                 c->stream));
+        words = c->d_dec;
+    }
     const uint64_t nbits = uint64_t(len) * 8;
     const uint64_t span = nbits - start_bit;
     const uint64_t nblocks = uint64_t(nframes) * (w / n) * (h / n);
@@ -2342,7 +2345,7 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     da.frame_pitch = frame_pitch;
     da.tab = c->d_tab;
     ie::RecParseArgs pa{};
-    pa.words = reinterpret_cast<const uint32_t*>(c->d_dec);
+    pa.words = reinterpret_cast<const uint32_t*>(words);
     pa.nbits = nbits;
     pa.start_bit = start_bit;
     pa.C = uint32_t(C);
@@ -2355,10 +2358,19 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     pa.E = reinterpret_cast<uint32_t*>(c->d_walk + e_at);
     pa.cnt = reinterpret_cast<uint32_t*>(c->d_walk + cnt_at);
     pa.pos = c->d_rpos;
+    if (!c->h_decres) {
+        void* hp = nullptr;
+        HIPCHK(c, hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        c->h_decres = static_cast<uint64_t*>(hp);
+        void* dp = nullptr;
+        HIPCHK(c, hipHostGetDevicePointer(&dp, hp, 0));
+        c->d_decres = static_cast<uint64_t*>(dp);
+    }
     pa.ticket = reinterpret_cast<unsigned*>(c->d_misc + 1);
-    pa.total = c->d_misc + 2;
-    pa.end_out = c->d_misc;
-    HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 3 * sizeof(uint64_t), c->stream));
+    pa.total = c->d_decres + 1;
+    pa.end_out = c->d_decres;
+    // (d_misc needs no clearing: the last chunk's decode wave always writes the record total, and
+    // the end bit is read only when that total covers the last block, whose decode writes it)
 #if IE_PROFILE  // walk statistics of the table pass (profiling builds only)
     static const bool dstats = getenv("IE_DEC_STATS") != nullptr;
     if (dstats) {
@@ -2380,10 +2392,8 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     HIPCHK(c, hipGetLastError());
     c->last_chunks = nchunks;
     c->last_groups = levels;
-    uint64_t hm[3] = {0, 0, 0};
-    HIPCHK(c, hipMemcpyAsync(hm, c->d_misc, sizeof(hm), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const uint64_t end = hm[0];
+    const uint64_t end = c->h_decres[0], total = c->h_decres[1];
 #if IE_PROFILE
     if (dstats) {
         uint64_t st[5];
@@ -2403,7 +2413,7 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
         }
     }
 #endif
-    if (hm[2] < nblocks || end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
+    if (total < nblocks || end > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
     return finish_decode(c, out, dpix, out_dev, nframes, w, h, stride, frame_pitch, end, end_bit);
 }
 }  // namespace

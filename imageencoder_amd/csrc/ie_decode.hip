@@ -235,11 +235,20 @@ int rec_count_seg(uint32_t C) {  // chunks per count wave: <= 16, a wave's bits 
 }
 
 
-// words [w0, w0 + nw) of the stream, byte-swapped to MSB-first, zeros past the stream
-__device__ __forceinline__ void stage_words(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nwords,
+// The stream word w (byte-swapped to MSB-first) with its bits at or past nbits cleared: the last
+// word may be read in place from a caller's buffer, whose bytes past the stream are not zero.
+__device__ __forceinline__ uint32_t tail_word(uint32_t raw, uint64_t w, uint64_t nbits) {
+    const uint32_t b = bswap32(raw);
+    const uint64_t vb = nbits - (w << 5);  // valid bits of this word (>= 1)
+    return vb >= 32 ? b : (b & ~(0xFFFFFFFFu >> uint32_t(vb)));
+}
+
+// words [w0, w0 + nw) of the stream, byte-swapped to MSB-first, zeros past the stream's nbits
+__device__ __forceinline__ void stage_words(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nbits,
                                             int tid, int nthreads) {
+    const uint64_t nwords = (nbits + 31) >> 5;
     for (int i = tid; i < nw; i += nthreads)
-        L[i] = (w0 + i < nwords) ? bswap32(__builtin_nontemporal_load(W + w0 + i)) : 0u;
+        L[i] = (w0 + i < nwords) ? tail_word(__builtin_nontemporal_load(W + w0 + i), w0 + i, nbits) : 0u;
 }
 
 // zig-zag rank of every coefficient position (the inverse of kZZ4 / kZZ8)
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
     const uint64_t lim64 = a.nbits - base;          // stream end relative to L: no record starts there or later
     const uint32_t lim = uint32_t(min<uint64_t>(lim64, uint64_t(s0) + uint64_t(m) * C));
     uint32_t* VB = L + rec_table_stream_words(uint32_t(M) * C);
-    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, (a.nbits + 31) >> 5, lane, 64);
+    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, lane, 64);
     for (int i = lane; i < M * HS; i += 64) (&H[0][0])[i] = 0xFFFFFFFFu;
     __syncthreads();
     wstamp(1);
@@ -509,13 +518,24 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
 // One composition level over n tables ([n][D], 16-bit exits): prefix maps written over the
 // tables, composites into comp ([ceil(n/G)][D]).  Shared by the record parse (D = the longest
 // record) and the Huffman decode (D = the longest code).
+// n 16-bit entries from global memory into LDS, 16 bytes per load where both sides allow it
+__device__ __forceinline__ void stage_u16(uint16_t* S, const uint16_t* T, int n, int tid) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    int head = 0;
+    if (((reinterpret_cast<uintptr_t>(T) | reinterpret_cast<uintptr_t>(S)) & 15u) == 0) {
+        head = n & ~7;
+        for (int i = tid; i < head / 8; i += kTPB) reinterpret_cast<u4*>(S)[i] = reinterpret_cast<const u4*>(T)[i];
+    }
+    for (int i = head + tid; i < n; i += kTPB) S[i] = T[i];
+}
+
 template <int D, int G>
 __global__ __launch_bounds__(kTPB) void compose_kernel(uint16_t* tab, int n, uint16_t* comp) {
-    __shared__ uint16_t S[G * D];
+    __shared__ __attribute__((aligned(16))) uint16_t S[G * D];
     const int tid = threadIdx.x, g = blockIdx.x;
     const int k0 = g * G, nk = min(G, n - k0);
     uint16_t* T = tab + size_t(k0) * D;
-    for (int i = tid; i < nk * D; i += kTPB) S[i] = T[i];
+    stage_u16(S, T, nk * D, tid);
     __syncthreads();
     // every entry chased through the group's tables; a thread's entries (tid, tid + kTPB, ...) are
     // chased side by side, so their dependent LDS reads overlap
@@ -545,8 +565,8 @@ __global__ __launch_bounds__(kTPB) void compose_kernel(uint16_t* tab, int n, uin
 // a device-wide fence in every composing workgroup).
 template <int D, int G>
 __global__ __launch_bounds__(kTPB) void compose_top_kernel(const uint16_t* comp, int ng, uint32_t* E) {
-    __shared__ uint16_t S[G * D];
-    for (int i = threadIdx.x; i < ng * D; i += kTPB) S[i] = comp[i];
+    __shared__ __attribute__((aligned(16))) uint16_t S[G * D];
+    stage_u16(S, comp, ng * D, threadIdx.x);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t x = 0;
@@ -615,13 +635,14 @@ __device__ __forceinline__ uint32_t rec_chunk_entry(const RecParseArgs& a, int k
 // L[i] = bswap(W[w0 + i]) for i < nw (zeros past nwords) by one wave with 16-byte loads, four
 // per lane in flight; L must be 16-byte aligned.  The copy starts at the aligned word w0 & ~3:
 // returns the offset of word w0 in L (0..3).
-__device__ __forceinline__ int stage_words16(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nwords,
+__device__ __forceinline__ int stage_words16(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nbits,
                                              int lane) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     const uint64_t wa = w0 & ~3ull;
     const int off = int(w0 - wa);
     const int nq = (nw + off + 3) >> 2;  // 16-byte groups
-    const uint64_t nfull = nwords >> 2;  // groups wholly inside the stream
+    const uint64_t nwords = (nbits + 31) >> 5;
+    const uint64_t nfull = (nbits >> 5) >> 2;  // groups of whole words wholly inside the stream
     for (int q0 = 0; q0 < nq; q0 += 64 * 4) {
         u4 v[4];
 #pragma unroll
@@ -631,10 +652,10 @@ __device__ __forceinline__ int stage_words16(uint32_t* L, const uint32_t* W, uin
             if (q < nq && g < nfull) {
                 v[u] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(W) + g);
             } else {
-                u4 z = {0u, 0u, 0u, 0u};
+                u4 z = {0u, 0u, 0u, 0u};  // (kept byte-swapped back: the store below swaps again)
                 if (q < nq)
                     for (int e = 0; e < 4; e++)
-                        if (4 * g + e < nwords) z[e] = W[4 * g + e];
+                        if (4 * g + e < nwords) z[e] = bswap32(tail_word(W[4 * g + e], 4 * g + e, nbits));
                 v[u] = z;
             }
         }
@@ -704,7 +725,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
     const int off = stage_words16(L, a.words, base >> 5, int(((c0 - base) + uint64_t(m) * C + 64) >> 5) + 2,
-                                  (a.nbits + 31) >> 5, lane);
+                                  a.nbits, lane);
     const uint32_t s0 = uint32_t(c0 - base) + 32u * uint32_t(off);  // the wave's first bit in L
     // positions below are relative to s0; no record starts at or past the stream's end
     const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - c0, uint64_t(m) * C));
@@ -801,14 +822,10 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
                     // round trips overlap)
                     const uint32_t head = lbits(L, s0 + p, 20);
                     const uint32_t key = (p << 16) | id;
-                    uint32_t h = (p * 2654435761u) >> 16 & HM;
-                    uint32_t own = kNoOwner;
-                    for (int probe = 0; probe < 8; probe++) {
-                        const uint32_t o = atomicCAS(&H[h], 0xFFFFFFFFu, key);
-                        if (o == 0xFFFFFFFFu) break;                          // claimed
-                        if ((o >> 16) == p) { own = o & 0xFFFFu; break; }     // owned: merge
-                        h = (h + 1u) & HM;                                    // (a full table: walk on)
-                    }
+                    // direct-mapped and lossy: a slot another position holds is not probed on --
+                    // the walk goes on unclaimed here and meets its owner's claims further on
+                    const uint32_t o = atomicCAS(&H[(p * 2654435761u) >> 16 & HM], 0xFFFFFFFFu, key);
+                    const uint32_t own = (o != 0xFFFFFFFFu && (o >> 16) == p) ? (o & 0xFFFFu) : kNoOwner;
                     if (own != kNoOwner) {
                         tgt[id] = uint16_t(own);
                         act = false;
@@ -879,7 +896,7 @@ __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
         const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
         const uint64_t base = c0 & ~31ull;
         const int off = stage_words16(L, a.words, base >> 5, int(((c0 - base) + uint64_t(m) * a.C + 64) >> 5) + 2,
-                                      (a.nbits + 31) >> 5, lane);
+                                      a.nbits, lane);
         s0 = uint32_t(c0 - base) + 32u * uint32_t(off);  // the wave's first bit, relative to L
     }
     const int k = k0 + lane;
@@ -914,75 +931,99 @@ __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
     if (tid == 0) a.wgsum[blockIdx.x] = tot;
 }
 
+// Decode pass: a wave decodes the records of kDecChunks consecutive chunks (about 64 records: a
+// chunk holds about 32), one record per lane, so the FP64 IDCT -- the pass's cost -- runs on full
+// waves.  Record positions come from the count pass (relative to each chunk's first word; chunk j
+// of the wave starts j * C bits after chunk 0, C a multiple of 32).
 template <int N>
 __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a, DecArgs d) {
     constexpr int D = RecGeom<N>::D;
-    extern __shared__ uint32_t dyn_all[];  // per wave: the chunk's bits + D + 64 (the last record's body)
+    constexpr int P = kDecChunks;
+    extern __shared__ uint32_t dyn_all[];  // per wave: the P chunks' bits + D + 64 (the last record's body)
     const const_f64 sR = (const_f64)(d.tab->R);
     const const_f64 sq = (const_f64)(d.tab->qd);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = blockIdx.x * kRecWPB + wv;
-    if (k >= a.nchunks) return;
-    uint32_t* L = dyn_all + size_t(wv) * rec_decode_stream_words(a.C, D);
-    const uint64_t c0 = a.start_bit + uint64_t(k) * a.C;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int k0 = (blockIdx.x * kRecWPB + wv) * P;
+    if (k0 >= a.nchunks) return;
+    const int m = min(P, a.nchunks - k0);
+    uint32_t* L = dyn_all + size_t(wv) * rec_decode_stream_words(uint32_t(P) * a.C, D);
+    const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
     const uint64_t base = c0 & ~31ull;
-    const uint32_t s0 = uint32_t(c0 - base), end = s0 + a.C;
-    // first block index: the totals of the count pass's workgroups before this chunk's, plus the
-    // records before it in its own (no separate scan launch)
+    const uint32_t s0 = uint32_t(c0 - base), end = s0 + uint32_t(m) * a.C;
+    // first block index: the totals of the count pass's workgroups before chunk k0's, plus the
+    // records before it in its own (no separate scan launch); the next chunks follow on
     uint64_t part = 0;
-    for (int g = lane; g < k / (4 * a.seg); g += 64) part += a.wgsum[g];
-    const uint64_t first = wave_sum64(part) + a.lbase[k];
-    const uint32_t R = a.cnt[k];
-    if (k == a.nchunks - 1 && lane == 0) *a.total = first + R;
-    stage_words(L, a.words, base >> 5, int((end + D + 64) >> 5) + 2, (a.nbits + 31) >> 5, lane, 64);
+    for (int g = lane; g < k0 / (4 * a.seg); g += 64) part += a.wgsum[g];
+    const uint64_t first = wave_sum64(part) + a.lbase[k0];
+    uint32_t R[P], Rall = 0;
+    bool listed = true;
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        R[j] = j < m ? a.cnt[k0 + j] : 0u;
+        Rall += R[j];
+        listed = listed && R[j] <= uint32_t(kRecPosCap);
+    }
+    if (k0 + m == a.nchunks && lane == 0) *a.total = first + Rall;
+    stage_words(L, a.words, base >> 5, int((end + D + 64) >> 5) + 2, a.nbits, lane, 64);
     wave_sync();
     const uint64_t nblocks = uint64_t(d.nframes) * d.bx * d.by;
-    if (R <= uint32_t(kRecPosCap)) {
-        const uint16_t* pos = a.pos + size_t(k) * kRecPosCap;
-        for (uint32_t i = lane; i < R; i += 64) {
+    if (listed) {
+        for (uint32_t i = lane; i < Rall; i += 64) {
             const uint64_t b = first + i;
             if (b >= nblocks) break;
-            const uint32_t q = decode_record<N>(L, pos[i], b, d, sR, sq);
+            uint32_t j = 0, r = i;
+#pragma unroll
+            for (int jj = 0; jj < P - 1; jj++)
+                if (j == uint32_t(jj) && r >= R[jj]) {
+                    r -= R[jj];
+                    j++;
+                }
+            const uint32_t q = decode_record<N>(L, j * a.C + a.pos[size_t(k0 + j) * kRecPosCap + r], b, d, sR, sq);
             if (b == nblocks - 1) *a.end_out = base + q;
         }
         return;
     }
-    // more records than the position list holds: walk them again, 64 at a time
-    uint32_t p = s0 + rec_chunk_entry<N>(a, k);
-    const uint32_t wend = uint32_t(min<uint64_t>(end, a.nbits - base));
+    // a chunk with more records than its position list holds: walk the chunks again, 64 records
+    // at a time
     uint64_t gi = first;
-    while (p < wend && gi < nblocks) {
-        uint32_t mine = 0, n = 0;
-        while (n < 64u && p < wend) {
-            const uint32_t len = rec_len<N>(L, p, d.rle);
-            if (!len) {
-                p++;
-                continue;
+    for (int j = 0; j < m; j++) {
+        uint32_t p = s0 + uint32_t(j) * a.C + rec_chunk_entry<N>(a, k0 + j);
+        const uint32_t wend = uint32_t(min<uint64_t>(s0 + uint64_t(j + 1) * a.C, a.nbits - base));
+        while (p < wend && gi < nblocks) {
+            uint32_t mine = 0, n = 0;
+            while (n < 64u && p < wend) {
+                const uint32_t len = rec_len<N>(L, p, d.rle);
+                if (!len) {
+                    p++;
+                    continue;
+                }
+                if (n == uint32_t(lane)) mine = p;
+                n++;
+                p += len;
             }
-            if (n == uint32_t(lane)) mine = p;
-            n++;
-            p += len;
+            const uint64_t b = gi + lane;
+            if (uint32_t(lane) < n && b < nblocks) {
+                const uint32_t q = decode_record<N>(L, mine, b, d, sR, sq);
+                if (b == nblocks - 1) *a.end_out = base + q;
+            }
+            gi += n;
         }
-        const uint64_t b = gi + lane;
-        if (uint32_t(lane) < n && b < nblocks) {
-            const uint32_t q = decode_record<N>(L, mine, b, d, sR, sq);
-            if (b == nblocks - 1) *a.end_out = base + q;
-        }
-        gi += n;
     }
 }
 
 int rec_group_chunks(int n) { return n == 4 ? RecGeom<4>::G : RecGeom<8>::G; }
 int rec_entry_span(int n) { return n == 4 ? RecGeom<4>::D : RecGeom<8>::D; }
 int rec_table_chunks(int n) { return n == 4 ? RecGeom<4>::M : RecGeom<8>::M; }
-// chunks per table wave and claim slots: tm chunks' positions fit the 16-bit claim keys; the
-// claim table holds about twice the walk steps of tm chunks (IE_REC_TM / IE_REC_HB override)
+// chunks per table wave and claim slots: tm chunks' positions fit the 16-bit claim keys.  The
+// claim table is small on purpose (lossy, direct-mapped): measured on 4K streams, the occupancy a
+// small LDS footprint buys beats the merges a larger table finds (IE_REC_TM / IE_REC_HB override)
 void rec_table_geometry(uint32_t C, int n, int* tm, int* hbits) {
     static const char* et = getenv("IE_REC_TM");
     static const char* eh = getenv("IE_REC_HB");
-    int t = et ? atoi(et) : 2;
+    int t = et ? atoi(et) : (n == 4 ? 2 : 1);
     while (t > 1 && uint64_t(t) * C > 65535u) t--;
     t = std::max(1, t);
-    int hb = eh ? atoi(eh) : ((n == 4 ? 9 : 11) + (t >= 4 ? 2 : t >= 2 ? 1 : 0));
+    int hb = eh ? atoi(eh) : ((n == 4 ? 7 : 9) + (t >= 4 ? 2 : t >= 2 ? 1 : 0));
     *tm = t;
     *hbits = std::min(14, std::max(6, hb));
 }
@@ -990,11 +1031,13 @@ size_t rec_table_lds(uint32_t C, int n) {
     const int M = n == 4 ? RecGeom<4>::M : RecGeom<8>::M;
     return size_t(rec_table_stream_words(uint32_t(M) * C) + M * (C >> 5)) * 4;
 }
-size_t rec_decode_lds(uint32_t C, int n) { return size_t(rec_decode_stream_words(C, rec_entry_span(n))) * 4 * kRecWPB; }
+size_t rec_decode_lds(uint32_t C, int n) {
+    return size_t(rec_decode_stream_words(uint32_t(kDecChunks) * C, rec_entry_span(n))) * 4 * kRecWPB;
+}
 
 int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t s) {
     if (a.nchunks <= 0) return 0;
-    const int nb = (a.nchunks + kRecWPB - 1) / kRecWPB;  // blocks of kRecWPB chunk waves
+    const int nb = (a.nchunks + kRecWPB * kDecChunks - 1) / (kRecWPB * kDecChunks);  // decode blocks
     const int nt = (a.nchunks + RecGeom<4>::M - 1) / RecGeom<4>::M;  // table waves (M chunks each)
 #if IE_REC_V1
     if (n == 4) hipLaunchKernelGGL((rec_table_kernel<4>), dim3(nt), dim3(64), rec_table_lds(a.C, 4), s, a);
@@ -1040,7 +1083,7 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
     const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
     const uint32_t s0 = uint32_t(c0 - base);
-    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, (a.nbits + 31) >> 5, tid, kTPB);
+    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
     __syncthreads();
     if (d >= kHufD || kc >= m) return;
     const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(s0) + uint64_t(m) * C));

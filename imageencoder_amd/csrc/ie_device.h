@@ -169,6 +169,10 @@ template <int N> struct RecGeom {
 constexpr int kRecMaxLevels = 4;
 constexpr int kRecPosCap = 256;  // record positions kept per chunk (more: the decode walks again)
 constexpr int kRecWPB = 4;       // chunk waves per block of the per-chunk passes
+#ifndef IE_DEC_CHUNKS
+#define IE_DEC_CHUNKS 2
+#endif
+constexpr int kDecChunks = IE_DEC_CHUNKS;  // chunks per decode wave (about 32 records each)
 struct RecParseArgs {
     const uint32_t* words;  // stream as stored (big-endian bytes), zero-padded by >= 2 words
     uint64_t nbits, start_bit;

@@ -512,3 +512,32 @@ def test_decode_truncated_stream_fails(codec, n):
         codec.decode_image_file(enc[: len(enc) * 9 // 10], n)
     # the context stays usable
     assert np.array_equal(codec.decode_image_file(enc, n), O.load().decode_image(enc, n))
+
+
+@pytest.mark.parametrize("n", [4, 8])
+@pytest.mark.parametrize("k", [0, 1, 2, 3])
+def test_decode_device_stream_in_place(codec, n, k):
+    """An aligned device stream is parsed in place: bytes past its length in the last word (here
+    0xFF) are cleared by the kernels, so the pixels and end bit equal those of the staged copy
+    (host bytes) and of an unaligned device view (staged on the device)."""
+    import torch
+
+    from imageencoder_amd import Codec, stream_bound
+    w, h = 264, 136
+    y = synth.frame("M", w, h, seed=11 + n)
+    c = Codec(0, O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n), n)
+    dev = torch.zeros(stream_bound(w, h, n, 1, 0) + 64, dtype=torch.uint8, device="cuda")
+    _, end = c.encode_frames(torch.from_numpy(y).cuda(), w, h, dev)
+    length = (end + 7) // 8 + k
+    dev[length:length + 16] = 0xFF
+    host = dev[:length].cpu().numpy().copy()
+    pix_h = torch.zeros((h, w), dtype=torch.uint8, device="cuda")
+    pix_d = torch.zeros_like(pix_h)
+    pix_u = torch.zeros_like(pix_h)
+    e_h = c.decode_frames(host, w, h, pix_h, length=length)
+    e_d = c.decode_frames(dev, w, h, pix_d, length=length)
+    shifted = torch.full((length + 17,), 0xFF, dtype=torch.uint8, device="cuda")
+    shifted[1:length + 1] = dev[:length]
+    e_u = c.decode_frames(shifted[1:], w, h, pix_u, length=length)
+    assert e_h == e_d == e_u == end
+    assert torch.equal(pix_h, pix_d) and torch.equal(pix_h, pix_u)
