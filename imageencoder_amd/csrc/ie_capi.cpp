@@ -11,6 +11,7 @@
 #include <cstddef>
 #include <cstring>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -2269,8 +2270,26 @@ int finish_decode(ie_ctx* c, uint8_t* out, const uint8_t* dpix, bool out_dev, in
 }
 
 // add_base: P-frame error -- the decoded error is added to the pixels already in `out`
+#if IE_PROFILE  // host-side phase times of the record decode (IE_DEC_HOST=1): entry, launches, sync
+struct DecHostTimes {
+    double pre = 0, launch = 0, sync = 0;
+    long n = 0;
+    ~DecHostTimes() {
+        if (n) fprintf(stderr, "[dec host] %ld calls: before the first launch %.1f us, launches %.1f us, sync %.1f us\n", n,
+                       pre / n, launch / n, sync / n);
+    }
+};
+static DecHostTimes g_dht;
+static double dht_now() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define DHT(x) const double x = dht_now()
+#else
+#define DHT(x)
+#endif
 int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes,
                        int use_rle, uint8_t* out, size_t stride, size_t frame_pitch, uint64_t* end_bit, int add_base) {
+    DHT(t0);
     int r = check_dims(c, w, h, nframes);
     if (r) return r;
     if (stride < size_t(w)) return fail(c, IE_EINVAL, "stride < width");
@@ -2388,11 +2407,22 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
         pa.wstamp = reinterpret_cast<unsigned long long*>(d_ws);
     }
 #endif
+    DHT(t1);
     if (ie::launch_rec_parse_decode(pa, da, n, c->stream) < 0) return fail(c, IE_EINVAL, "stream too long for one decode call");
     HIPCHK(c, hipGetLastError());
     c->last_chunks = nchunks;
     c->last_groups = levels;
+    DHT(t2);
     HIPCHK(c, hipStreamSynchronize(c->stream));
+#if IE_PROFILE
+    {
+        DHT(t3);
+        g_dht.pre += t1 - t0;
+        g_dht.launch += t2 - t1;
+        g_dht.sync += t3 - t2;
+        g_dht.n++;
+    }
+#endif
     const uint64_t end = c->h_decres[0], total = c->h_decres[1];
 #if IE_PROFILE
     if (dstats) {

@@ -225,7 +225,8 @@ __device__ __forceinline__ uint32_t rec_len(const uint32_t* L, uint32_t p, int r
 }
 
 __host__ __device__ constexpr int rec_table_stream_words(uint32_t C) { return int((C + 95) >> 5) + 3; }
-__host__ __device__ constexpr int rec_decode_stream_words(uint32_t C, int D) { return int((C + D + 95) >> 5) + 3; }
+// (a multiple of 4 words, with room for stage_words16's alignment offset)
+__host__ __device__ constexpr int rec_decode_stream_words(uint32_t C, int D) { return (int((C + D + 95) >> 5) + 3 + 3 + 3) & ~3; }
 // a count wave's LDS words: seg chunks' bits + 64 + alignment slack, a multiple of 4 (16-byte rows)
 __host__ __device__ constexpr int rec_count_wave_words(uint32_t C, int seg) {
     return (int((uint64_t(seg) * C + 95) >> 5) + 3 + 3 + 3) & ~3;
@@ -519,12 +520,29 @@ __global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
 // tables, composites into comp ([ceil(n/G)][D]).  Shared by the record parse (D = the longest
 // record) and the Huffman decode (D = the longest code).
 // n 16-bit entries from global memory into LDS, 16 bytes per load where both sides allow it
+// (eight 16-byte loads per thread in flight before their LDS stores: one load-to-store round trip
+// per 32 KiB instead of one per 4 KiB)
 __device__ __forceinline__ void stage_u16(uint16_t* S, const uint16_t* T, int n, int tid) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     int head = 0;
     if (((reinterpret_cast<uintptr_t>(T) | reinterpret_cast<uintptr_t>(S)) & 15u) == 0) {
         head = n & ~7;
-        for (int i = tid; i < head / 8; i += kTPB) reinterpret_cast<u4*>(S)[i] = reinterpret_cast<const u4*>(T)[i];
+        const int nv = head / 8;
+        const u4* src = reinterpret_cast<const u4*>(T);
+        u4* dst = reinterpret_cast<u4*>(S);
+        for (int i0 = 0; i0 < nv; i0 += 8 * kTPB) {
+            u4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = i0 + u * kTPB + tid;
+                if (i < nv) v[u] = src[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = i0 + u * kTPB + tid;
+                if (i < nv) dst[i] = v[u];
+            }
+        }
     }
     for (int i = head + tid; i < n; i += kTPB) S[i] = T[i];
 }
@@ -562,7 +580,9 @@ __global__ __launch_bounds__(kTPB) void compose_kernel(uint16_t* tab, int n, uin
 
 // The top chase: the stream's start (entry 0) through the ng <= G top-level composites, E[q] = the
 // entry of composite q (one workgroup; a launch of its own, so the composites are visible without
-// a device-wide fence in every composing workgroup).
+// a device-wide fence in every composing workgroup).  (A segmented chase -- every entry through
+// each of 8 segments, then entry 0 through the segment maps -- measured slower here and in
+// compose_kernel: 9.2 -> 11.6 and 15.2 -> 18.1 us.)
 template <int D, int G>
 __global__ __launch_bounds__(kTPB) void compose_top_kernel(const uint16_t* comp, int ng, uint32_t* E) {
     __shared__ __attribute__((aligned(16))) uint16_t S[G * D];
@@ -795,7 +815,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     wstamp(3);
     // 3. the walks: lanes take the next walk of the list as theirs ends
     {
-        uint32_t nxt = 0, p = 0, id = 0, ce = 0, nsteps = 0;
+        uint32_t nxt = 0, p = 0, id = 0, ce = 0, nsteps = 0, wsteps = 0, rsteps = 0;
         bool act = false;
         for (;;) {
             const uint64_t need = __ballot(!act);
@@ -813,10 +833,13 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
             if (!__ballot(act)) break;
             if (act) {
                 nsteps++;
+                wsteps++;
                 if (p >= ce) {  // left the chunk
                     res[id] = uint16_t(p - ce);
                     tgt[id] = uint16_t(kNoOwner);
                     act = false;
+                    rsteps += wsteps;  // (profiling: steps of walks that reached the chunk's end)
+                    wsteps = 0;
                 } else {
                     // the record's header read before the claim (independent of it, so both LDS
                     // round trips overlap)
@@ -829,6 +852,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
                     if (own != kNoOwner) {
                         tgt[id] = uint16_t(own);
                         act = false;
+                        wsteps = 0;
                     } else {
                         p += rec_len_head<N>(head, a.rle);  // p is valid: a record starts here
                         p = next_valid<N>(VB, p, ce);
@@ -840,15 +864,15 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         if (ws) {
             const uint32_t mx = __reduce_max_sync(~0ull, nsteps);
             const uint32_t sm = __reduce_add_sync(~0ull, nsteps);
+            const uint32_t rs = __reduce_add_sync(~0ull, rsteps);
             if (lane == 0) {
                 ws[6] = (uint64_t(mx) << 32) | sm;
-                uint32_t hw;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-                ws[7] = hw;
+                ws[7] = (uint64_t(nw) << 32) | rs;  // walks, steps of the walks that left the chunk
             }
         }
 #endif
         (void)nsteps;
+        (void)rsteps;
     }
     __syncthreads();
     wstamp(4);
@@ -871,7 +895,11 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         } else {
             const uint32_t cs = j * C, ce = cs + C;
             const uint32_t nv = next_valid<N>(VB, cs + d, ce);
-            out = (nv >= ce) ? nv - ce : res[j * D1 + min(nv - cs, uint32_t(D))];
+            if (nv >= ce) {
+                out = nv - ce;
+            } else {
+                out = res[j * D1 + min(nv - cs, uint32_t(D))];
+            }
         }
         T[e] = uint16_t(out);
     }
@@ -939,7 +967,7 @@ template <int N>
 __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a, DecArgs d) {
     constexpr int D = RecGeom<N>::D;
     constexpr int P = kDecChunks;
-    extern __shared__ uint32_t dyn_all[];  // per wave: the P chunks' bits + D + 64 (the last record's body)
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn_all[];  // per wave: the P chunks' bits + D + 64
     const const_f64 sR = (const_f64)(d.tab->R);
     const const_f64 sq = (const_f64)(d.tab->qd);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -949,7 +977,13 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
     uint32_t* L = dyn_all + size_t(wv) * rec_decode_stream_words(uint32_t(P) * a.C, D);
     const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
     const uint64_t base = c0 & ~31ull;
-    const uint32_t s0 = uint32_t(c0 - base), end = s0 + uint32_t(m) * a.C;
+    // the chunks' bits first (16-byte loads in flight while the indices below are read); bit
+    // positions in L are relative to word `off` of L, which holds the first chunk's first word
+    const int off = stage_words16(L, a.words, base >> 5, int((uint32_t(c0 - base) + uint32_t(m) * a.C + D + 64) >> 5) + 2,
+                                  a.nbits, lane);
+    const uint32_t ob = 32u * uint32_t(off);
+    const uint32_t s0 = uint32_t(c0 - base) + ob, end = s0 + uint32_t(m) * a.C;
+    const uint64_t lbase0 = base - ob;  // stream bit of L's bit 0
     // first block index: the totals of the count pass's workgroups before chunk k0's, plus the
     // records before it in its own (no separate scan launch); the next chunks follow on
     uint64_t part = 0;
@@ -964,7 +998,6 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
         listed = listed && R[j] <= uint32_t(kRecPosCap);
     }
     if (k0 + m == a.nchunks && lane == 0) *a.total = first + Rall;
-    stage_words(L, a.words, base >> 5, int((end + D + 64) >> 5) + 2, a.nbits, lane, 64);
     wave_sync();
     const uint64_t nblocks = uint64_t(d.nframes) * d.bx * d.by;
     if (listed) {
@@ -978,8 +1011,8 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
                     r -= R[jj];
                     j++;
                 }
-            const uint32_t q = decode_record<N>(L, j * a.C + a.pos[size_t(k0 + j) * kRecPosCap + r], b, d, sR, sq);
-            if (b == nblocks - 1) *a.end_out = base + q;
+            const uint32_t q = decode_record<N>(L, ob + j * a.C + a.pos[size_t(k0 + j) * kRecPosCap + r], b, d, sR, sq);
+            if (b == nblocks - 1) *a.end_out = lbase0 + q;
         }
         return;
     }
@@ -988,7 +1021,7 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
     uint64_t gi = first;
     for (int j = 0; j < m; j++) {
         uint32_t p = s0 + uint32_t(j) * a.C + rec_chunk_entry<N>(a, k0 + j);
-        const uint32_t wend = uint32_t(min<uint64_t>(s0 + uint64_t(j + 1) * a.C, a.nbits - base));
+        const uint32_t wend = uint32_t(min<uint64_t>(s0 + uint64_t(j + 1) * a.C, a.nbits - lbase0));
         while (p < wend && gi < nblocks) {
             uint32_t mine = 0, n = 0;
             while (n < 64u && p < wend) {
@@ -1004,7 +1037,7 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
             const uint64_t b = gi + lane;
             if (uint32_t(lane) < n && b < nblocks) {
                 const uint32_t q = decode_record<N>(L, mine, b, d, sR, sq);
-                if (b == nblocks - 1) *a.end_out = base + q;
+                if (b == nblocks - 1) *a.end_out = lbase0 + q;
             }
             gi += n;
         }

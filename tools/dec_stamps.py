@@ -48,16 +48,16 @@ life = t[:, 5] - t[:, 0]
 print(f"wave life mean {life.mean():.2f} us  p50 {np.median(life):.2f}  p90 {np.percentile(life, 90):.2f}")
 it = st[:, 6]
 mx, sm = it >> 32, it & 0xFFFFFFFF
+tmc = max(1, round(chunks / len(st)))
 print(f"walk iterations per wave: max-lane mean {mx.mean():.1f} p90 {np.percentile(mx, 90):.0f} max {mx.max()}; "
-      f"lane-steps per chunk {sm.mean():.1f}")
+      f"lane-steps per chunk {sm.mean() / tmc:.1f}")
 # concurrency: waves alive at 200 sample times
 ts = np.linspace(0, t[:, 5].max(), 200)
 alive = [(np.sum((t[:, 0] <= x) & (t[:, 5] > x))) for x in ts]
 print("alive waves over the launch (every 10th sample):", [int(a) for a in alive[::10]])
-hw = st[:, 7]
-cu = (hw >> 8) & 0xF
-se = (hw >> 13) & 0x7
-print(f"distinct (se,cu) {len(set(zip(se.tolist(), cu.tolist())))}")
+nwk, rst = st[:, 7] >> 32, st[:, 7] & 0xFFFFFFFF
+print(f"per chunk: walks {nwk.mean() / tmc:.1f}, steps of walks that left the chunk {rst.mean() / tmc:.1f}, "
+      f"steps of merged walks {(sm.mean() - rst.mean()) / tmc:.1f}")
 first = t[:, 0]
 print(f"wave start times: p10 {np.percentile(first, 10):.1f} p50 {np.median(first):.1f} p90 {np.percentile(first, 90):.1f} "
       f"max {first.max():.1f} us")
