@@ -447,9 +447,9 @@ struct Geometry {
     int bx, by, gpr, gpf, tpf, ntiles;
 };
 
-Geometry geometry(int w, int h, int n, int nframes) {
+Geometry geometry(int w, int h, int n, int nframes, int bpt = 0) {
     Geometry g;
-    const int bpt = ie::encode_blocks_per_thread(n);
+    if (!bpt) bpt = ie::encode_blocks_per_thread(n);
     g.bx = w / n;
     g.by = h / n;
     g.gpr = (g.bx + bpt - 1) / bpt;
@@ -491,8 +491,10 @@ struct Launch {
 };
 
 int launch_chain(ie_ctx* c, const Launch& L) {
-    const Geometry g = geometry(L.w, L.h, c->n, L.nframes);
     const int bpt = ie::encode_blocks_per_thread(c->n);
+    const Geometry g = geometry(L.w, L.h, c->n, L.nframes, bpt);
+    // a launch too small to fill the chip: its tiles reach the look-back together (deep windows)
+    const bool small = g.ntiles < ie::encode_small_tiles();
     const bool vec_ok = (reinterpret_cast<uintptr_t>(L.dy) % size_t(bpt * c->n) == 0) &&
                         (L.stride % (bpt * c->n) == 0) && (L.nframes == 1 || L.frame_pitch % (bpt * c->n) == 0);
     int r;
@@ -561,7 +563,8 @@ int launch_chain(ie_ctx* c, const Launch& L) {
         HIPCHK(c, hipMemsetAsync(d_stamps, 0, size_t(g.ntiles) * ie::kStamps * sizeof(uint64_t), c->stream));
     }
     a.stamps = d_stamps;
-    ie::launch_encode(a, c->n, L.mode == IE_MODE_EXACT, c->stream);
+    a.deep_lb = small ? 1 : 0;
+    ie::launch_encode(a, c->n, L.mode == IE_MODE_EXACT, c->stream, bpt);
     HIPCHK(c, hipGetLastError());
     if (d_stamps) {
         std::vector<uint64_t> hs(size_t(g.ntiles) * ie::kStamps);
@@ -1677,6 +1680,12 @@ int ie_encode_gop(ie_ctx* c, const uint8_t* y, int w, int h, size_t stride, size
             a.out = dout;
             a.start = c->d_gop_pos + f;
             a.end = c->d_gop_pos + f + 1;
+            if (n == 4 && !c->use_ticket) {  // the record tiles' scan by look-back (one launch)
+                if ((r = prepare_state(c, ie::pframe_tiles(nb), 1))) return r;
+                a.st = c->d_state;
+                a.tag = c->tag;
+                a.err = c->d_err;
+            }
             ie::launch_pframe(a, n, c->d_gop_tile, c->stream);
             HIPCHK(c, hipGetLastError());
             ref = a.rec;

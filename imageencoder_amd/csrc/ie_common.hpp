@@ -177,17 +177,35 @@ __device__ __forceinline__ Probe probe_issue(const uint64_t* st, int t, int chai
     return p;
 }
 
+// Later look-back windows are issued kLbAhead at a time (64 predecessors each, all loads in
+// flight together): a tile far from the nearest resolved predecessor -- a launch whose tiles all
+// reach their look-back at once, e.g. one frame -- walks back 64 * kLbAhead tiles per round trip.
+#ifndef IE_LB_AHEAD
+#define IE_LB_AHEAD 8
+#endif
+constexpr int kLbAhead = IE_LB_AHEAD;
+
 // Exclusive prefix of tile t, executed by ONE wave from a first probe (width kProbe0): the sum of
 // aggregates up to the nearest inclusive value (predecessors publish their aggregate as soon as
 // their bit count is known).  Later windows read 64 predecessors.  Returns the prefix in every
 // lane.
+// deep: the launch's tiles all reach their look-back at about the same time (a launch too small to
+// fill the chip), so a tile's nearest inclusive predecessor is far away: the windows after the
+// first probe are issued at once, before it is evaluated.
 __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
-                                  unsigned* err, unsigned* rounds = nullptr) {
+                                  unsigned* err, unsigned* rounds = nullptr, bool deep = false) {
     const int lane = lane_id();
     uint64_t excl = 0;
     int d0 = 0, width = kProbe0;
     unsigned spins = 0;
+    Probe ahead[kLbAhead];  // windows d0 + 64, d0 + 128, ... already in flight
+    int nahead = 0;
     if (rounds) *rounds = 0;
+    if (deep && chain_pos > kProbe0) {
+#pragma unroll
+        for (int k = kLbAhead - 1; k >= 0; k--) ahead[k] = probe_issue(st, t, chain_pos, step, kProbe0 + 64 * (kLbAhead - 1 - k), 64);
+        nahead = kLbAhead;
+    }
     for (;;) {
         const int d = d0 + lane;
         int status = 2;  // before the chain start: a virtual inclusive prefix of 0
@@ -219,8 +237,18 @@ __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_
         if (dP < width) return excl;
         d0 += width;
         width = 64;
-        p = probe_issue(st, t, chain_pos, step, d0, width);
-        if (rounds) *rounds += 0x10000;
+        if (nahead == 0) {  // the next kLbAhead windows in one round trip
+#pragma unroll
+            for (int k = kLbAhead - 1; k >= 0; k--) ahead[k] = probe_issue(st, t, chain_pos, step, d0 + 64 * (kLbAhead - 1 - k), 64);
+            nahead = kLbAhead;
+            if (rounds) *rounds += 0x10000;
+        }
+        // (ahead[nahead - 1] is window d0; a window read ahead may be re-probed by the spin above)
+        p = ahead[0];
+#pragma unroll
+        for (int k = 1; k < kLbAhead; k++)
+            if (k == nahead - 1) p = ahead[k];
+        nahead--;
     }
 }
 
@@ -255,7 +283,7 @@ __device__ __forceinline__ void chain_publish_count(uint64_t* st, int t, int cha
 __device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
                                                   const uint32_t* img, uint32_t A, const uint32_t* out,
                                                   uint64_t start, unsigned* err, uint32_t* misc, const Probe& pr,
-                                                  uint64_t* dbg = nullptr, bool defer_tail = false) {
+                                                  uint64_t* dbg = nullptr, bool defer_tail = false, bool deep = false) {
     const int tid = threadIdx.x;
     if (tid == 0) {
         const uint32_t my_tail = image_tail32(img, A);
@@ -275,7 +303,7 @@ __device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain
     }
     if (chain_pos != 0 && tid < 64) {
         unsigned rounds = 0, polls = 0;
-        const uint64_t excl = lookback_wave(pr, st, t, chain_pos, step, tag, err, dbg ? &rounds : nullptr);
+        const uint64_t excl = lookback_wave(pr, st, t, chain_pos, step, tag, err, dbg ? &rounds : nullptr, deep);
         if (tid == 0) {
             publish(st, t, 1, tag, excl + A);
             const bool have = uint32_t(pr.gt >> 56) == tag;

@@ -84,6 +84,7 @@ struct EncArgs {
     int16_t* coef;           // optional: quantised coefficients, natural order, [nframes*bx*by][N*N]
     int ablate;              // profiling only (IE_ABLATE): 1 no FP64, 2 no emission, 4 no look-back, 8 no store, 16 no DCT, 128 no pixel loads
     uint64_t* stamps;        // profiling only (IE_STAMPS): [tile][kStamps] s_memtime per phase, thread 0
+    int deep_lb;             // the launch does not fill the chip: look-back windows issued at once
     int rec_bits;            // = tab->rec_bits (host copy): launch_encode sizes the LDS tile image from it
     int tri;                 // 4x4: every bl <= 11 (from rec_bits): records emitted three coefficients per field
     int img_words;           // set by launch_encode
@@ -95,8 +96,10 @@ struct EncArgs {
 constexpr int kStamps = 16;
 // chain-state words per tile (the host allocates; ie_common.hpp kGran must not exceed it)
 constexpr int kStateWordsPerTile = 16;
-void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s);
-int encode_blocks_per_thread(int n);
+// bpt: blocks per thread, encode_blocks_per_thread(n, ntiles at the default) for the launch
+void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s, int bpt);
+int encode_blocks_per_thread(int n);  // the batch default (4x4: 4, 8x8: 1)
+int encode_small_tiles();             // a launch of fewer tiles does not fill the chip (deep look-back)
 void launch_word_scatter(const uint32_t* src, uint32_t* dst, uint64_t pitch_words, int n, hipStream_t s);  // horizontally adjacent blocks per lane (Geo<N>::BPT)
 int encode_threads_per_tile();       // threads per encoder workgroup (= tile)
 
@@ -233,6 +236,9 @@ struct PfArgs {
     uint32_t* out;           // stream words (zero from the frame's first bit on)
     const uint64_t* start;   // device: the frame's first bit
     uint64_t* end;           // device: its end bit
+    uint64_t* st;            // record tiles' chain state (look-back scan); nullptr = separate scan launches
+    uint32_t tag;            // the state's epoch
+    unsigned* err;           // [0]: look-back spin timeouts
 };
 void launch_pframe(const PfArgs& a, int n, uint64_t* tile_scratch, hipStream_t s);
 // P-frame decode, first half (Block.cpp:481-496): every macroblock's motion vector read from the

@@ -102,9 +102,9 @@ constexpr int image_words_for(int n, int bpt, int rec_bits) {
 #ifndef IE_LDS_PIX
 #define IE_LDS_PIX 1
 #endif
-constexpr int kFixPix = 0;                               // [BPT][TPB] x 4 words: the pixels
-constexpr int kFixTasks = kFixPix + IE_BPT4 * kEncTPB * 4;  // per wave: [64] tasks, [64] results
-constexpr int kFixWords = kFixTasks + (kEncTPB / 64) * 128;   // the image is never smaller
+constexpr int kFixPix = 0;  // [BPT][TPB] x 4 words: the pixels
+template <int B> constexpr int fix_tasks() { return kFixPix + B * kEncTPB * 4; }  // per wave: [64] tasks, [64] results
+template <int B> constexpr int fix_words() { return fix_tasks<B>() + (kEncTPB / 64) * 128; }  // the image is never smaller
 // 8x8: one 16-word block per lane at a 20-word stride (16-byte writes land on distinct banks)
 #ifndef IE_FIX_COMPACT8
 #define IE_FIX_COMPACT8 1
@@ -206,9 +206,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Load the pixel rows of one group: seg[r][m] = bytes [4m, 4m+4) of the group's row r.
-template <int N, int WPR>
+template <int N, int WPR, int BPT = Geo<N>::BPT>
 __device__ __forceinline__ void load_group(const EncArgs& a, const uint8_t* base, int nblk, uint32_t (&seg)[N][WPR]) {
-    constexpr int BPT = Geo<N>::BPT;
     if (a.vec_ok && nblk == BPT) {
 #pragma unroll
         for (int r = 0; r < N; r++) {
@@ -531,7 +530,7 @@ struct TileGeo {
     int nblk, byi, bx0;  // blocks of this thread's group (nblk = 0: none)
 };
 
-template <int N>
+template <int N, int BPT = Geo<N>::BPT>
 __device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
     TileGeo g;
     // Independent images interleave their tiles (frame = t % nframes), so every frame's chain
@@ -557,18 +556,18 @@ __device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
     g.nblk = g.byi = g.bx0 = 0;
     if (gi < a.groups_per_frame) {
         g.byi = q0 + int(dq);
-        g.bx0 = int(r - dq * uint32_t(a.gpr)) * Geo<N>::BPT;
-        g.nblk = min(Geo<N>::BPT, a.bx - g.bx0);
+        g.bx0 = int(r - dq * uint32_t(a.gpr)) * BPT;
+        g.nblk = min(BPT, a.bx - g.bx0);
     }
     return g;
 }
 
-template <int N, int WPR>
+template <int N, int WPR, int BPT = Geo<N>::BPT>
 __device__ __forceinline__ void load_tile(const EncArgs& a, const TileGeo& g, uint32_t (&seg)[N][WPR]) {
     if (g.nblk) {
         const uint8_t* base =
             a.y + size_t(g.frame) * a.frame_pitch + size_t(g.byi) * N * a.stride + size_t(g.bx0) * N;
-        load_group<N, WPR>(a, base, g.nblk, seg);
+        load_group<N, WPR, BPT>(a, base, g.nblk, seg);
     } else {
 #pragma unroll
         for (int r = 0; r < N; r++)
@@ -653,11 +652,14 @@ struct HistCount {
     }
 };
 
-template <int N, bool EXACT, bool HIST = false>
+// BB: blocks per thread (4x4: 4; the LDS pixel layout also takes 1 -- measured on one 4K frame,
+// 2 025 tiles of one block per lane took 36 us against 20 us for 506 tiles of four: the longer
+// look-back chain costs more than the shorter tiles save)
+template <int N, bool EXACT, bool HIST = false, int BB = Geo<N>::BPT>
 __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     constexpr int NN = N * N;
     constexpr int NP = NN / 2;
-    constexpr int BPT = Geo<N>::BPT;
+    constexpr int BPT = BB;
     constexpr int WPR = BPT * N / 4;
     constexpr int TPB = kEncTPB;
 #ifdef IE_STATIC_IMG4  // A/B aid: a static image of this many bits per block (4x4 only)
@@ -718,18 +720,20 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         // issued before the pixel loads, so waiting for it does not wait for them
         for (int i = tid; i < 3 * NN + 9; i += TPB) srow[i] = tab->srow[i];
     }
-    const TileGeo g = tile_geo<N>(a, t, tid);
+    const TileGeo g = tile_geo<N, BPT>(a, t, tid);
     // the chain's first bit: the host's value, or (streamed video, ie_vstream_*) the previous
     // launch's chain end on the device, written before this launch started (stream order)
     const uint64_t start_bit = a.start_dev ? *a.start_dev : a.start_bit;
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
     constexpr bool kLdsPix = IE_LDS_PIX && N == 4 && !EXACT;
-    uint32_t* const pwave = img + kFixPix + (tid >> 6) * 1024;  // kLdsPix: this wave's [4][64][4] words
+    // kLdsPix: this wave's [4 rows][64 lanes][BPT] words; block b of a lane = word b of each row
+    constexpr int kRowW = 64 * BPT;
+    uint32_t* const pwave = img + kFixPix + (tid >> 6) * (N * kRowW);
     const int lane = tid & 63;
     uint32_t seg[N][WPR];
     if constexpr (kLdsPix) {
-        static_assert(BPT == 4 && WPR == 4 && TPB % 64 == 0, "LDS pixel layout: 16 bytes per lane per row");
+        static_assert((BPT == 4 || BPT == 1) && WPR == BPT && TPB % 64 == 0, "LDS pixel layout: 4 * BPT bytes per lane per row");
         if (IE_PROFILE && (ablate & 4096)) {
             // profiling: no pixel loads at all (the LDS holds whatever the previous tile left)
         } else if (!__ballot(!(a.vec_ok && nblk == BPT))) {  // every group of the wave is whole: DMA
@@ -737,15 +741,23 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                 a.y + size_t(frame) * a.frame_pitch + size_t(byi) * N * a.stride + size_t(bx0) * N;
 #pragma unroll
             for (int r = 0; r < N; r++)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
-                                                 (__attribute__((address_space(3))) void*)(pwave + r * 256), 16, 0, 0);
+                if constexpr (BPT == 4)
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
+                                                     (__attribute__((address_space(3))) void*)(pwave + r * kRowW), 16, 0, 0);
+                else
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
+                                                     (__attribute__((address_space(3))) void*)(pwave + r * kRowW), 4, 0, 0);
         } else {  // ragged (frame edge, unaligned rows): through registers
-            load_tile<N, WPR>(a, g, seg);
+            load_tile<N, WPR, BPT>(a, g, seg);
 #pragma unroll
             for (int r = 0; r < N; r++) {
-                u32x4 v;
-                v.x = seg[r][0]; v.y = seg[r][1]; v.z = seg[r][2]; v.w = seg[r][3];
-                *reinterpret_cast<u32x4*>(pwave + r * 256 + lane * 4) = v;
+                if constexpr (BPT == 4) {
+                    u32x4 v;
+                    v.x = seg[r][0]; v.y = seg[r][1]; v.z = seg[r][2]; v.w = seg[r][3];
+                    *reinterpret_cast<u32x4*>(pwave + r * kRowW + lane * 4) = v;
+                } else {
+                    pwave[r * kRowW + lane] = seg[r][0];
+                }
             }
         }
     } else if (ablate & 128) {  // profiling: no pixel loads (synthetic pixels from the thread id)
@@ -754,7 +766,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
 #pragma unroll
             for (int m = 0; m < WPR; m++) seg[r][m] = (uint32_t(tid) * 0x9E3779B1u + uint32_t(t) * 0x85EBCA77u) ^ (r * 0x27D4EB2Fu + m);
     } else {
-        load_tile<N, WPR>(a, g, seg);
+        load_tile<N, WPR, BPT>(a, g, seg);
     }
     if constexpr (!EXACT) lds_barrier();  // srow visible (the pixel loads stay in flight)
     if constexpr (kLdsPix) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
@@ -796,7 +808,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
             if constexpr (kLdsPix) {
                 uint32_t rows[N][1];
 #pragma unroll
-                for (int r = 0; r < N; r++) rows[r][0] = pwave[r * 256 + lane * 4 + b];
+                for (int r = 0; r < N; r++) rows[r][0] = pwave[r * kRowW + lane * BPT + b];
                 block_pixels<N, 1>(rows, 0, x);
             } else {
                 block_pixels<N, WPR>(seg, b, x);
@@ -970,7 +982,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                 BlockPx<N> px;
                 if constexpr (kLdsPix) {
 #pragma unroll
-                    for (int r = 0; r < N; r++) px.w[r] = pwave[r * 256 + (owner & 63) * 4 + b];
+                    for (int r = 0; r < N; r++) px.w[r] = pwave[r * kRowW + (owner & 63) * BPT + b];
                 } else {
                     const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
                     px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
@@ -986,7 +998,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                 pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
                 total += uint32_t(__popcll(bm)) << k;
             }
-            uint32_t* task = img + kFixTasks + (tid >> 6) * 128;  // [64] tasks, then [64] results
+            uint32_t* task = img + fix_tasks<BPT>() + (tid >> 6) * 128;  // [64] tasks, then [64] results
             uint32_t* res = task + 64;
             for (uint32_t r0 = 0; r0 < total; r0 += 64) {
                 uint32_t m = sf, i = pre - r0;
@@ -1234,7 +1246,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         excl = uint64_t(tif) * (110u * TPB);
     } else {
         excl = chain_resolve(a.st, t, chain_pos, step, a.tag, img, A, out, start_bit, a.err, ctl, pr,
-                             stamps ? &stamps[size_t(t) * kStamps + 1] : nullptr, true);
+                             stamps ? &stamps[size_t(t) * kStamps + 1] : nullptr, true, a.deep_lb != 0);
     }
     if (tid == 0) {
         const uint64_t P = start_bit + excl;
@@ -1278,14 +1290,21 @@ void launch_word_scatter(const uint32_t* src, uint32_t* dst, uint64_t pitch_word
 }
 
 int encode_blocks_per_thread(int n) { return n == 4 ? Geo<4>::BPT : Geo<8>::BPT; }
+#ifndef IE_SMALL_TILES
+#define IE_SMALL_TILES 1024
+#endif
+int encode_small_tiles() {
+    static const char* e = getenv("IE_SMALL_TILES");  // (A/B aid: 0 disables the small-launch geometry)
+    static const int v = e ? atoi(e) : IE_SMALL_TILES;
+    return v;
+}
 
 int encode_threads_per_tile() { return kEncTPB; }
 
-void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s) {
+void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt) {
     EncArgs a = a0;
-    const int bpt = encode_blocks_per_thread(n);
     a.img_words = image_words_for(n, bpt, a.rec_bits);
-    if (n == 4 && a.img_words < kFixWords) a.img_words = kFixWords;
+    if (n == 4 && a.img_words < fix_words<4>()) a.img_words = fix_words<4>();
     if (n == 8 && a.img_words < kFix8Words) a.img_words = kFix8Words;
 #ifdef IE_STATIC_IMG4
     a.img_words = image_words_for(4, 4, IE_STATIC_IMG4);

@@ -17,6 +17,7 @@
 // placed by a two-level scan of their lengths and ORed into the zeroed stream.
 #include <hip/hip_runtime.h>
 
+#include "ie_common.hpp"
 #include "ie_device.h"
 
 namespace ie {
@@ -39,7 +40,6 @@ __device__ __forceinline__ int bits_needed16(int v) {  // utils.hpp:226-243 for 
     return 33 - __clz(a) > 16 ? 16 : 33 - __clz(a);
 }
 
-__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
 // MSB-first bits ORed into the zeroed stream (words = stream bytes [4w, 4w + 4)).
 struct BitOr {
@@ -106,10 +106,35 @@ __device__ __forceinline__ uint32_t load4(const uint8_t* p) {
     return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
 }
 
+// Pixels no macroblock covers (the bottom strip, rows [16*mby, h), then the right strip of the
+// covered rows, columns [16*mbx, w)): their microblocks keep the frame's own pixels as "error" and
+// have no record (bits = 0, written here for 4x4 blocks), so expandDifferences doubles them
+// (Block.cpp:52-55,110-119).
+__device__ __forceinline__ void pf_strip_pixel(const PfArgs& a, int n, size_t i) {
+    const int hc = a.mby * kMB, wc = a.mbx * kMB;
+    const size_t nbot = size_t(a.h - hc) * a.w, nright = size_t(hc) * (a.w - wc);
+    if (i >= nbot + nright) return;
+    int x, y;
+    if (i < nbot) {
+        y = hc + int(i / size_t(a.w));
+        x = int(i % size_t(a.w));
+    } else {
+        const size_t j = i - nbot;
+        const int rw = a.w - wc;
+        y = int(j / size_t(rw));
+        x = wc + int(j % size_t(rw));
+    }
+    const int c = a.cur[size_t(y) * a.cs + x];
+    a.rec[size_t(y) * a.w + x] = uint8_t(min(2 * c, 255));
+    if (n == 4 && (x & 3) == 0 && (y & 3) == 0) a.bits[size_t(y / 4) * a.bx + x / 4] = 0u;
+}
+
 // One WAVE per macroblock (a 64-thread workgroup: its barriers cost nothing): lane l holds pixel row
 // l/4, columns 4(l%4)..+3 of the macroblock, whose SAD against a candidate is one v_sad_u8.
 constexpr int kMbTPB = 64;
 
+// Workgroups past the macroblocks (64 pixels each) do the uncovered strips: they touch no pixel
+// or record a macroblock does, so they share the launch.
 template <int N>
 __global__ __launch_bounds__(kMbTPB) void pf_macroblock_kernel(PfArgs a) {
     __shared__ double xs[256];
@@ -117,6 +142,12 @@ __global__ __launch_bounds__(kMbTPB) void pf_macroblock_kernel(PfArgs a) {
     __shared__ int16_t cq[256];
     const int l = threadIdx.x;
     const int mb = blockIdx.x;
+    if (mb >= a.mbx * a.mby) {
+        const size_t i = size_t(mb - a.mbx * a.mby) * kMbTPB + size_t(l);
+        const size_t npx = size_t(a.w) * a.h - size_t(a.mbx) * a.mby * kMB * kMB;
+        if (i < npx) pf_strip_pixel(a, N, i);
+        return;
+    }
     const int mx = (mb % a.mbx) * kMB, my = (mb / a.mbx) * kMB;
     const int py = l >> 2, px = (l & 3) * 4;
     const int W16 = a.w - kMB, H16 = a.h - kMB;
@@ -238,30 +269,6 @@ __global__ __launch_bounds__(kMbTPB) void pf_macroblock_kernel(PfArgs a) {
     }
 }
 
-// Pixels no macroblock covers (the bottom strip, rows [16*mby, h), then the right strip of the
-// covered rows, columns [16*mbx, w)): their microblocks keep the frame's own pixels as "error" and
-// have no record (bits = 0, written here for 4x4 blocks), so expandDifferences doubles them
-// (Block.cpp:52-55,110-119).
-__global__ __launch_bounds__(kTPB) void pf_strip_kernel(PfArgs a, int n) {
-    const size_t i = size_t(blockIdx.x) * kTPB + threadIdx.x;
-    const int hc = a.mby * kMB, wc = a.mbx * kMB;
-    const size_t nbot = size_t(a.h - hc) * a.w, nright = size_t(hc) * (a.w - wc);
-    if (i >= nbot + nright) return;
-    int x, y;
-    if (i < nbot) {
-        y = hc + int(i / size_t(a.w));
-        x = int(i % size_t(a.w));
-    } else {
-        const size_t j = i - nbot;
-        const int rw = a.w - wc;
-        y = int(j / size_t(rw));
-        x = wc + int(j % size_t(rw));
-    }
-    const int c = a.cur[size_t(y) * a.cs + x];
-    a.rec[size_t(y) * a.w + x] = uint8_t(min(2 * c, 255));
-    if (n == 4 && (x & 3) == 0 && (y & 3) == 0) a.bits[size_t(y / 4) * a.bx + x / 4] = 0u;
-}
-
 // block-wide exclusive scan of one value per thread; returns the total in *tot
 __device__ __forceinline__ uint64_t block_exscan(uint64_t v, uint64_t* sh, uint64_t* tot) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -351,6 +358,60 @@ __global__ __launch_bounds__(kTPB) void pf_emit_kernel(PfArgs a, int nb, const u
     }
 }
 
+// The scan fused into the emission: tile t of the frame's record tiles publishes its bit count,
+// finds its first bit by a decoupled look-back over its predecessors (the encoder's chain
+// protocol, ie_common.hpp: aggregate as soon as the count is known, inclusive once resolved; tiles
+// run in dispatch order) and emits -- one launch instead of tile sums, tile scan and emission.
+// The last tile writes the frame's end bit.
+__global__ __launch_bounds__(kTPB) void pf_emit_chain_kernel(PfArgs a, int nb, int ntiles, uint64_t head_bits) {
+    __shared__ uint64_t sh[kTPB / 64];
+    __shared__ uint32_t img[kPfImgWords];
+    __shared__ uint64_t sx;
+    const int t = threadIdx.x, tile = blockIdx.x;
+    const int b0 = tile * kPfTileBlocks + t * kPfPer;
+    uint64_t s = 0;
+    for (int k = 0; k < kPfPer; k++)
+        if (b0 + k < nb) s += a.bits[b0 + k];
+    uint64_t tot;
+    const uint64_t ex = block_exscan(s, sh, &tot);
+    if (t == 0) chain_publish_count(a.st, tile, tile, a.tag, uint32_t(tot));
+    if (t < 64) {
+        uint64_t excl = 0;
+        if (tile > 0) {
+            const Probe pr = probe_issue(a.st, tile, tile, 1, 0, kProbe0);
+            excl = lookback_wave(pr, a.st, tile, tile, 1, a.tag, a.err, nullptr, true);
+            if (t == 0) publish(a.st, tile, 1, a.tag, excl + tot);
+        }
+        if (t == 0) sx = excl;
+    }
+    __syncthreads();
+    const uint64_t S = *a.start + head_bits + sx;  // the tile's first bit
+    if (tile == ntiles - 1 && t == 0) *a.end = S + tot;
+    const uint32_t o0 = uint32_t(S & 31u);
+    const uint32_t nw = uint32_t((o0 + tot + 31) / 32);
+    for (uint32_t i = t; i < nw; i += kTPB) img[i] = 0u;
+    __syncthreads();
+    if (s) {
+        BitOr o(img, o0 + ex);
+        for (int k = 0; k < kPfPer && b0 + k < nb; k++) {
+            if (!a.bits[b0 + k]) continue;  // no macroblock covered it: no record (Block.cpp:373-375)
+            const int16_t* c = a.coef + size_t(b0 + k) * 16;
+            const uint32_t sz = size4(c, a.rle);
+            const int bl = int(sz & 0xFFu), lw = int(sz >> 8);
+            o.put(4, uint32_t(bl));  // Block::streamEncoded (Block.cpp:372-413)
+            if (a.rle) o.put(bl, uint32_t(lw));
+            for (int i = 0; i < lw; i++) o.put(bl, uint32_t(int32_t(c[kZz4[i]])));
+        }
+        o.flush();
+    }
+    __syncthreads();
+    uint32_t* g = a.out + (S >> 5);
+    for (uint32_t i = t; i < nw; i += kTPB) {
+        if (i == 0 || i == nw - 1) atomicOr(g + i, img[i]);
+        else g[i] = img[i];
+    }
+}
+
 // the frame's end bit when it carries no records (8x8 blocks, or no macroblock)
 __global__ void pf_end_kernel(const uint64_t* start, uint64_t* end, uint64_t head_bits) {
     if (threadIdx.x == 0) *end = *start + head_bits;
@@ -393,20 +454,21 @@ void launch_pframe(const PfArgs& a, int n, uint64_t* tsum, hipStream_t s) {
     const int nmb = a.mbx * a.mby;
     const uint64_t head = uint64_t(nmb) * 2u * uint32_t(a.mv_bits);
     const int nb = a.bx * (a.h / n);
-    if (nmb > 0) {
-        if (n == 4) {
-            hipLaunchKernelGGL(pf_macroblock_kernel<4>, dim3(nmb), dim3(kMbTPB), 0, s, a);
-        } else {
-            hipLaunchKernelGGL(pf_macroblock_kernel<8>, dim3(nmb), dim3(kMbTPB), 0, s, a);
-        }
-    }
     const size_t px = size_t(a.w) * a.h - size_t(nmb) * kMB * kMB;  // pixels no macroblock covers
-    if (px) hipLaunchKernelGGL(pf_strip_kernel, dim3(unsigned((px + kTPB - 1) / kTPB)), dim3(kTPB), 0, s, a, n);
+    const unsigned grid = unsigned(nmb) + unsigned((px + kMbTPB - 1) / kMbTPB);  // + the strips' workgroups
+    if (grid) {
+        if (n == 4) hipLaunchKernelGGL(pf_macroblock_kernel<4>, dim3(grid), dim3(kMbTPB), 0, s, a);
+        else hipLaunchKernelGGL(pf_macroblock_kernel<8>, dim3(grid), dim3(kMbTPB), 0, s, a);
+    }
     if (n == 4 && nmb > 0) {
         const int ntiles = (nb + kPfTileBlocks - 1) / kPfTileBlocks;
-        hipLaunchKernelGGL(pf_tile_sum_kernel, dim3(ntiles), dim3(kTPB), 0, s, a.bits, nb, tsum);
-        hipLaunchKernelGGL(pf_tile_scan_kernel, dim3(1), dim3(kTPB), 0, s, tsum, ntiles, head, a.start, a.end);
-        hipLaunchKernelGGL(pf_emit_kernel, dim3(ntiles), dim3(kTPB), 0, s, a, nb, tsum, head);
+        if (a.st) {  // one launch: the scan by look-back
+            hipLaunchKernelGGL(pf_emit_chain_kernel, dim3(ntiles), dim3(kTPB), 0, s, a, nb, ntiles, head);
+        } else {     // (ticket mode: tiles may not run in dispatch order) tile sums, scan, emission
+            hipLaunchKernelGGL(pf_tile_sum_kernel, dim3(ntiles), dim3(kTPB), 0, s, a.bits, nb, tsum);
+            hipLaunchKernelGGL(pf_tile_scan_kernel, dim3(1), dim3(kTPB), 0, s, tsum, ntiles, head, a.start, a.end);
+            hipLaunchKernelGGL(pf_emit_kernel, dim3(ntiles), dim3(kTPB), 0, s, a, nb, tsum, head);
+        }
     } else {
         hipLaunchKernelGGL(pf_end_kernel, dim3(1), dim3(64), 0, s, a.start, a.end, head);
     }

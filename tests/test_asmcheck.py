@@ -43,7 +43,7 @@ def test_fma_outside_any_division_fails(tmp_path):
 
 
 def _budget_asm(occ, scratch):
-    name = "_ZN2ie13encode_kernelILi8ELb0ELb0EEEvNS_7EncArgsEPKNS_9EncTablesE"
+    name = "_ZN2ie13encode_kernelILi8ELb0ELb0ELi1EEEvNS_7EncArgsEPKNS_9EncTablesE"
     return (f"{name}:\n\ts_endpgm\n; NumVgprs: 121\n; ScratchSize: {scratch}\n; Occupancy: {occ}\n")
 
 

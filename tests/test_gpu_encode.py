@@ -2,6 +2,7 @@
 CPU oracle.  Bit-exact is the only bar (integer/byte output).
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -225,3 +226,34 @@ def test_extreme_matrices_fill_the_tile_image(codec, oracle, n, qfill):
             assert end == eend and np.array_equal(fb, efb)
             nb = (end + 7) // 8
             assert out[:nb].tobytes() == exp[:nb].tobytes()
+
+
+@pytest.mark.parametrize("w,h,f", [(3840, 2160, 1), (200, 56, 3), (1928, 1080, 2), (4, 4, 1)])
+def test_small_launch_lookback_matches_batch_path(w, h, f, tmp_path):
+    """Launches whose tiles would not fill the chip issue their look-back windows at once; the
+    stream must be the one the batch path (IE_SMALL_TILES=0, fresh processes) writes -- ragged
+    widths, several frames, concatenated and segmented output."""
+    import subprocess
+    import sys
+
+    code = ("import sys, hashlib, numpy as np; sys.path.insert(0, %r)\n"
+            "import torch\n"
+            "from imageencoder_amd import Codec, read_matrix, stream_bound, synth\n"
+            "from tests import oracle_lib as O\n"
+            "w, h, f = %d, %d, %d\n"
+            "c = Codec(0, read_matrix(O.GOLDEN + '/matrix.txt', 4), 4)\n"
+            "y = torch.from_numpy(synth.frames('M', w, h, f, seed=77)).cuda()\n"
+            "out = torch.zeros(stream_bound(w, h, 4, f, 13) + 64, dtype=torch.uint8, device='cuda')\n"
+            "_, end = c.encode_frames(y, w, h, out, start_bit=13, nframes=f)\n"
+            "pitch = (stream_bound(w, h, 4, 1, 5) + 255) // 256 * 256\n"
+            "seg = torch.zeros(pitch * f, dtype=torch.uint8, device='cuda')\n"
+            "ends = c.encode_images(y, w, h, seg, out_pitch=pitch, nframes=f, start_bit=5)\n"
+            "print(end, hashlib.md5(out[:(end + 7) // 8].cpu().numpy().tobytes()).hexdigest(),\n"
+            "      hashlib.md5(seg.cpu().numpy().tobytes()).hexdigest(), list(map(int, ends)))\n") % (O.ROOT, w, h, f)
+    outs = []
+    for extra in ({"IE_SMALL_TILES": "1024"}, {"IE_SMALL_TILES": "0"}):
+        env = dict(os.environ, **extra)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env, cwd=O.ROOT)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout.strip().splitlines()[-1])
+    assert outs[0] == outs[1]

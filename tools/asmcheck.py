@@ -95,8 +95,8 @@ def static_lds(path):
 # change that makes the compiler spill or drop a wave shows up in the CPU build, not only on a GPU
 # (an unguarded profiling branch once took the 8x8 kernel from 68 to 308 B of scratch, 2x slower).
 BUDGETS = {
-    "_ZN2ie13encode_kernelILi4ELb0ELb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (5, 0),
-    "_ZN2ie13encode_kernelILi8ELb0ELb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (4, 96),
+    "_ZN2ie13encode_kernelILi4ELb0ELb0ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": (5, 0),
+    "_ZN2ie13encode_kernelILi8ELb0ELb0ELi1EEEvNS_7EncArgsEPKNS_9EncTablesE": (4, 96),
 }
 
 
@@ -110,6 +110,9 @@ def main(paths):
                 rc = 1
                 print(f"{p}: {name} allocates {size} B of static LDS (scatter_bits assumes 0)", file=sys.stderr)
         bad, kernels = scan(p)
+        if "encode" in p and not any(k in kernels for k in BUDGETS):
+            rc = 1
+            print(f"{p}: none of the budgeted encode kernels found (renamed? update BUDGETS)", file=sys.stderr)
         for name, (waves, scratch) in BUDGETS.items():
             info = kernels.get(name)
             if info and (info.get("Occupancy", 0) < waves or info.get("ScratchSize", 0) > scratch):
