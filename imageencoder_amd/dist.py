@@ -179,6 +179,14 @@ class PipelinedGather:
 
     def step(self, i: int) -> None:
         """Encode and assemble one whole batch (all chunks)."""
+        if self.E is not None:
+            # whatever the caller queued on its current stream before this step -- the frames, this
+            # object's zero-filled buffers on the first step -- comes before the encode and the
+            # transfers (the encode's end bits would otherwise race the zero fill of self.bits)
+            cur = self.torch.cuda.current_stream(self.dev)
+            self.E.wait_stream(cur)
+            if self.C is not None:
+                self.C.wait_stream(cur)
         self._base = self.hb
         if self.rank == 0 and self.hdr_last is not None:  # the header's partial byte: ORed into below
             with self._on(self.C):

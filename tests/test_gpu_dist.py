@@ -137,7 +137,7 @@ def _worker_c4(rank, world, port, F, nchunks, steps, q_out):
         G = D.PipelinedGather(dist, rank, world, F, nchunks, hdr, hb, stream_bound(w, h, n, m, 0) + 64,
                               stream_bound(w, h, n, F, hb) + 64, encode, shift, dev, comm_dev="cpu",
                               enc_stream=E, comm_stream=C)
-        res = []
+        res, counts = [], []
         for s in range(steps):
             G.step(s)
             torch.cuda.synchronize()
@@ -145,13 +145,14 @@ def _worker_c4(rank, world, port, F, nchunks, steps, q_out):
             shifter.sync()
             if rank == 0:
                 res.append((G.total, hashlib.md5(G.out[: (G.total + 7) // 8].cpu().numpy().tobytes()).hexdigest()))
+                counts.append(G.counts_host.tolist())
         del mine
         if rank == 0:
             allf = synth.uniform_device(w, h, F, seed, dev, torch)
             ref = torch.zeros(stream_bound(w, h, n, F, hb) + 64, dtype=torch.uint8, device=dev)
             ref[: hdr.size].copy_(torch.from_numpy(hdr).to(dev))
             _, end = enc.encode_frames(allf, w, h, ref, start_bit=hb, nframes=F)
-            q_out.put((res, (end, hashlib.md5(ref[: (end + 7) // 8].cpu().numpy().tobytes()).hexdigest())))
+            q_out.put((res, (end, hashlib.md5(ref[: (end + 7) // 8].cpu().numpy().tobytes()).hexdigest()), counts))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -174,9 +175,10 @@ def test_c4_shape_512_frames_8_ranks():
     for p in procs:
         p.start()
     try:
-        res, single = q.get(timeout=480)
+        res, single, counts = q.get(timeout=480)
     finally:
         for p in procs:
             p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    assert res == [single] * 2
+    # (on failure: every step's per-chunk, per-rank segment bits as rank 0 received them)
+    assert res == [single] * 2, counts

@@ -19,11 +19,11 @@ for wl in c2 c3 c4 c5; do
 done
 
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_stats -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-single-frame --no-e2e --no-decode > $O/prof_stats.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_stats -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-single-frame --no-e2e --no-decode --no-gop > $O/prof_stats.log 2>&1
 rc=$?; echo "rocprof stats rc=$rc"; stop_if_fatal $rc; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-single-frame --no-e2e --no-decode > $O/pmc_fetch.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-single-frame --no-e2e --no-decode --no-gop > $O/pmc_fetch.log 2>&1
 rc=$?; echo "pmc fetch rc=$rc"; stop_if_fatal $rc; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-single-frame --no-e2e --no-decode > $O/pmc_write.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-single-frame --no-e2e --no-decode --no-gop > $O/pmc_write.log 2>&1
 rc=$?; echo "pmc write rc=$rc"; stop_if_fatal $rc
 find $O/prof_stats $O/pmc_fetch $O/pmc_write -name "*.csv" | head -20
 python3 $R/tools/traffic.py encode_kernel $(find $O/pmc_fetch -name "*counter_collection.csv" | head -1) $(find $O/pmc_write -name "*counter_collection.csv" | head -1) $O/traffic_c2.json
