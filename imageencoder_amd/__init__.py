@@ -109,6 +109,8 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.ie_vstream_close.argtypes = [vp]
     L.ie_huffman_decode.argtypes = [vp, u8p, C.c_size_t, C.c_uint64, vp, u8p, C.c_size_t, C.POINTER(C.c_size_t)]
     L.ie_last_decode_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.ie_set_exact_parse.argtypes = [vp, C.c_int]
+    L.ie_last_decode_spec.argtypes = [vp]
     L.ie_malloc.argtypes = [vp, C.c_size_t, C.POINTER(C.c_void_p)]
     L.ie_free.argtypes = [vp, vp]
     L.ie_memcpy.argtypes = [vp, vp, vp, C.c_size_t]
@@ -436,6 +438,15 @@ class Codec:
         f, r = C.c_int(0), C.c_int(0)
         self._chk(self.L.ie_last_decode_info(self.h, C.byref(f), C.byref(r)))
         return int(f.value), int(r.value)
+
+    def set_exact_parse(self, exact: bool) -> None:
+        """Record decodes parse exactly (composed transfer tables) instead of speculatively first
+        (ie_set_exact_parse)."""
+        self._chk(self.L.ie_set_exact_parse(self.h, int(bool(exact))))
+
+    def last_decode_spec(self) -> bool:
+        """True when the last record decode was completed by the speculative parse."""
+        return bool(self.L.ie_last_decode_spec(self.h))
 
     def last_fallbacks(self) -> int:
         v = C.c_uint64(0)

@@ -112,6 +112,8 @@ struct ie_ctx {
     size_t cap_pix = 0;
     int last_chunks = 0;               // chunks of the last record decode
     int last_groups = 0;               // and their groups
+    int last_spec = 0;                 // 1: the last record decode was the speculative parse
+    int spec_parse = 0;                // ie_set_exact_parse(ctx, 0): speculative record parse first
     unsigned long long* d_first = nullptr;  // [256]
     ie_pipe* pipe = nullptr;           // streamed host path of image batches (created on first use)
     // P-frame videos (ie_encode_gop): reconstructed frames (two, alternating), the prediction
@@ -1258,6 +1260,14 @@ int ie_last_decode_info(ie_ctx* c, int* chunks, int* levels) {
     return IE_OK;
 }
 
+int ie_set_exact_parse(ie_ctx* c, int exact) {
+    if (!c) return IE_EINVAL;
+    c->spec_parse = exact ? 0 : 1;
+    return IE_OK;
+}
+
+int ie_last_decode_spec(ie_ctx* c) { return c ? c->last_spec : 0; }
+
 const uint8_t* ie_vstream_device(const ie_vstream* v) { return v ? v->d_stream : nullptr; }
 
 int ie_vstream_close(ie_vstream* v) {
@@ -2353,7 +2363,8 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     // least 4 chunks)
     const size_t e_at = size_t(nchunks) / 2 + 1, cnt_at = e_at + size_t(G) / 2 + 1;
     const size_t wg_at = cnt_at + size_t(nchunks) / 2 + 1;
-    if ((r = ensure(c, c->d_walk, c->cap_walk, wg_at + size_t(nchunks) / 2 + 2))) return r;
+    const size_t spec_at = wg_at + size_t(nchunks) / 2 + 2;  // [nchunks / 2] speculative exits
+    if ((r = ensure(c, c->d_walk, c->cap_walk, spec_at + size_t(nchunks) / 2 + 1))) return r;
     if ((r = ensure(c, c->d_rpos, c->cap_rpos, size_t(nchunks) * ie::kRecPosCap))) return r;
     const size_t pix_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
     const bool out_dev = is_device_ptr(out);
@@ -2417,11 +2428,43 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     }
 #endif
     DHT(t1);
-    if (ie::launch_rec_parse_decode(pa, da, n, c->stream) < 0) return fail(c, IE_EINVAL, "stream too long for one decode call");
-    HIPCHK(c, hipGetLastError());
+    // Optional speculative parse first (ie_decode.hip rec_spec_kernel; ie_set_exact_parse(ctx, 0)
+    // or IE_DEC_SPEC=1): each chunk's entry is where a walk from an earlier chunk's first bit left
+    // it, verified by the count pass; on any mismatch (e.g. periodic content, whose wrong-phase
+    // walks never meet the true path) nothing was decoded and the exact parse over composed
+    // transfer tables runs.  Off by default: measured on 4K frames and the reference's example
+    // images it wins only on flat content -- a wrong-phase walk takes ~35 steps to
+    // meet the true path and the slowest of ~16 000 chunks sets the pass's time.
+    static const char* es = getenv("IE_DEC_SPEC");
+    const bool spec = (es && atoi(es) != 0) || c->spec_parse;
+    bool exact = !spec;
+    c->last_spec = 0;
+    if (spec) {
+        pa.spec = reinterpret_cast<uint32_t*>(c->d_walk + spec_at);
+        pa.fail = reinterpret_cast<unsigned*>(c->d_misc + 2);
+        // warm-up chunks: a speculative walk crosses this many whole chunks (about 32 (4x4) / 16
+        // (8x8) records each) before the chunk whose exit it reports (IE_DEC_WARM)
+        static const char* ew = getenv("IE_DEC_WARM");
+        pa.warm = ew ? std::max(0, std::min(8, atoi(ew))) : 0;
+        ie::launch_rec_spec_decode(pa, da, n, c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->h_decres[1] == ~0ull) {
+            exact = true;
+            pa.spec = nullptr;
+            pa.fail = nullptr;
+        } else {
+            c->last_spec = 1;
+            levels = 0;
+        }
+    }
+    DHT(t2);
+    if (exact) {
+        if (ie::launch_rec_parse_decode(pa, da, n, c->stream) < 0) return fail(c, IE_EINVAL, "stream too long for one decode call");
+        HIPCHK(c, hipGetLastError());
+    }
     c->last_chunks = nchunks;
     c->last_groups = levels;
-    DHT(t2);
     HIPCHK(c, hipStreamSynchronize(c->stream));
 #if IE_PROFILE
     {

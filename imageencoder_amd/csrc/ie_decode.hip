@@ -646,9 +646,10 @@ __device__ __forceinline__ uint32_t table_entry(const uint32_t* E, uint16_t* con
     return x;
 }
 
-// the chunk's entry offset (record parse)
+// the chunk's entry offset (record parse): composed tables, or the predecessor's speculative exit
 template <int N>
 __device__ __forceinline__ uint32_t rec_chunk_entry(const RecParseArgs& a, int k) {
+    if (a.spec) return k ? a.spec[k - 1] : 0u;
     return table_entry<RecGeom<N>::D, RecGeom<N>::G>(a.E, a.lvl, a.levels, k);
 }
 
@@ -906,6 +907,37 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     wstamp(5);
 }
 
+// Speculative pass: one lane per chunk k walks from the first bit of chunk k - W (W = a.warm
+// chunks of warm-up; from the stream's first record, an exact entry, when k - W <= 0) through chunk
+// k, sliding one bit past positions where no record can start, and stores where it leaves chunk k.
+// A walk from an arbitrary bit meets the true record boundaries after a few records on typical
+// content, long before the warm-up ends; the count pass proves it did (or flags the stream).
+template <int N>
+__global__ __launch_bounds__(kTPB) void rec_spec_kernel(RecParseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t Lall[];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int seg = a.seg, W = a.warm;
+    const int k0 = (blockIdx.x * 4 + wv) * seg;
+    const int m = max(0, min(seg, a.nchunks - k0));
+    if (blockIdx.x == 0 && tid == 0) *a.fail = 0u;  // (the count pass runs after this launch)
+    if (m == 0) return;
+    const int kw = max(k0 - W, 0);  // the wave's first staged chunk
+    uint32_t* L = Lall + size_t(wv) * rec_count_wave_words(a.C, seg + W);
+    const uint64_t c0 = a.start_bit + uint64_t(kw) * a.C;
+    const uint64_t base = c0 & ~31ull;
+    const int off = stage_words16(L, a.words, base >> 5,
+                                  int(((c0 - base) + uint64_t(k0 + m - kw) * a.C + 64) >> 5) + 2, a.nbits, lane);
+    const uint32_t s0 = uint32_t(c0 - base) + 32u * uint32_t(off);  // chunk kw's first bit in L
+    wave_sync();
+    const int k = k0 + lane;
+    if (lane < m && k < a.nchunks - 1) {  // (the last chunk's exit enters nothing)
+        const uint32_t ce = s0 + uint32_t(k + 1 - kw) * a.C;
+        uint32_t p = s0 + uint32_t(max(k - W, 0) - kw) * a.C;
+        while (p < ce) p += rec_len_head<N>(lbits(L, p, 20), a.rle);
+        a.spec[k] = p - ce;
+    }
+}
+
 // Count pass: each wave stages `seg` consecutive chunks' bits in LDS and one lane per chunk walks
 // its true records from its entry (the prefix maps applied to its top-level entry), storing up to
 // kRecPosCap record positions (relative to the chunk's first word) and the count; the workgroup
@@ -948,6 +980,9 @@ __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
             }
             p += l;
         }
+        // speculative entries: this walk started at the true entry if every earlier one did; its
+        // exit must be the entry the next chunk's walk took
+        if (a.spec && k < a.nchunks - 1 && p - (cs + a.C) != a.spec[k]) *a.fail = 1u;
     }
     // records before each chunk within the workgroup (thread order = chunk order; idle lanes add 0)
     uint32_t tot;
@@ -973,6 +1008,10 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int k0 = (blockIdx.x * kRecWPB + wv) * P;
     if (k0 >= a.nchunks) return;
+    if (a.spec && *a.fail) {  // a speculative entry was wrong: nothing is written, the host re-runs
+        if (k0 == 0 && lane == 0) *a.total = ~0ull;
+        return;
+    }
     const int m = min(P, a.nchunks - k0);
     uint32_t* L = dyn_all + size_t(wv) * rec_decode_stream_words(uint32_t(P) * a.C, D);
     const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
@@ -1094,6 +1133,23 @@ int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t
     if (n == 4) hipLaunchKernelGGL((rec_decode_kernel<4>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 4), s, a, d);
     else hipLaunchKernelGGL((rec_decode_kernel<8>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 8), s, a, d);
     return levels;
+}
+
+void launch_rec_spec_decode(const RecParseArgs& a, const DecArgs& d, int n, hipStream_t s) {
+    if (a.nchunks <= 0) return;
+    const int nb = (a.nchunks + kRecWPB * kDecChunks - 1) / (kRecWPB * kDecChunks);
+    const int nbc = (a.nchunks + 4 * a.seg - 1) / (4 * a.seg);
+    const size_t lc = size_t(rec_count_wave_words(a.C, a.seg)) * 4 * 4;
+    const size_t lw = size_t(rec_count_wave_words(a.C, a.seg + a.warm)) * 4 * 4;
+    if (n == 4) {
+        hipLaunchKernelGGL((rec_spec_kernel<4>), dim3(nbc), dim3(kTPB), lw, s, a);
+        hipLaunchKernelGGL((rec_count_kernel<4>), dim3(nbc), dim3(kTPB), lc, s, a);
+        hipLaunchKernelGGL((rec_decode_kernel<4>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 4), s, a, d);
+    } else {
+        hipLaunchKernelGGL((rec_spec_kernel<8>), dim3(nbc), dim3(kTPB), lw, s, a);
+        hipLaunchKernelGGL((rec_count_kernel<8>), dim3(nbc), dim3(kTPB), lc, s, a);
+        hipLaunchKernelGGL((rec_decode_kernel<8>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 8), s, a, d);
+    }
 }
 
 // ---- exact Huffman parse: the same transfer tables --------------------------------------------

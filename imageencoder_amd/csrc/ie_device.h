@@ -198,6 +198,13 @@ struct RecParseArgs {
     unsigned long long* wstamp; // diagnostics (IE_DEC_STAMPS): [table waves][8] phase times; nullptr = off
     int tm;                 // chunks per table wave (rec_table_geometry)
     int hbits;              // log2 of a table wave's claim slots
+    // speculative parse (non-null): spec[k] = where the walk of chunk k from its first bit leaves
+    // it (offset into chunk k+1) -- the entry of chunk k+1 in place of the composed tables; the
+    // count pass, walking every chunk from its predecessor's spec exit, verifies each exit and sets
+    // *fail on a mismatch (the decode pass then writes nothing and the host re-runs exactly)
+    uint32_t* spec;
+    unsigned* fail;         // device word, cleared by the speculative pass
+    int warm;               // speculative walks start this many chunks early (IE_DEC_WARM, default 0)
 };
 // Table-wave geometry for chunks of C bits: chunks per wave (tm) and log2 claim slots (hbits).
 void rec_table_geometry(uint32_t C, int n, int* tm, int* hbits);
@@ -209,6 +216,8 @@ size_t rec_decode_lds(uint32_t C, int n);
 int rec_count_seg(uint32_t C);
 // Returns the number of composition levels (< 0: too many chunks).
 int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t s);
+// the speculative form (a.spec, a.fail set): speculative walks, verifying count pass, decode
+void launch_rec_spec_decode(const RecParseArgs& a, const DecArgs& d, int n, hipStream_t s);
 
 // Huffman decode (ie_decode.hip): write = false runs the exact parse (per-chunk transfer tables
 // over the 15 entry offsets, composed) + the counting walk + scan and leaves the symbol count in

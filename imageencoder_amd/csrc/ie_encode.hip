@@ -68,6 +68,9 @@ template <> struct ZigZagInv<8> {
 #ifndef IE_TPB
 #define IE_TPB 256
 #endif
+#ifndef IE_PIX64
+#define IE_PIX64 1  // measured -0.6 % on C2 (same-process A/B)
+#endif
 constexpr int kEncTPB = IE_TPB;
 template <int N> struct Geo;
 template <> struct Geo<4> {  // IE_BPT4 blocks side by side: 4 * IE_BPT4 bytes per pixel row per lane
@@ -787,6 +790,8 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     // fix-up requests, 4 bits per block: bits 0-2 structural coefficient s, bit 3 the whole block
     uint32_t flags = 0;
     uint64_t near8 = 0;  // 8x8: per-coefficient requests of the lane's one block
+    uint32_t pix_next[N];  // IE_PIX64: the odd block's rows, read with the even block's
+    (void)pix_next;
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
 #if !IE_NO_SCHED_BARRIER
@@ -807,6 +812,22 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
             float x[NN];
             if constexpr (kLdsPix) {
                 uint32_t rows[N][1];
+#if IE_PIX64
+                // two blocks' rows per 8-byte read (2-way instead of 4-way bank conflicts)
+                if constexpr (BPT % 2 == 0) {
+                    if (b % 2 == 0) {
+#pragma unroll
+                        for (int r = 0; r < N; r++) {
+                            const u32x2 v = *reinterpret_cast<const u32x2*>(pwave + r * kRowW + lane * BPT + b);
+                            rows[r][0] = v.x;
+                            pix_next[r] = v.y;
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < N; r++) rows[r][0] = pix_next[r];
+                    }
+                } else
+#endif
 #pragma unroll
                 for (int r = 0; r < N; r++) rows[r][0] = pwave[r * kRowW + lane * BPT + b];
                 block_pixels<N, 1>(rows, 0, x);

@@ -24,7 +24,11 @@ sub-batches ("chunks") assigned round-robin -- chunk k holds global frames
 so the layout of chunk k depends only on chunks <= k.  Rank r's encode of chunk k+1 then overlaps the all_gather,
 re-shift and point-to-point transfer of chunk k (separate HIP streams; RCCL orders its own).
 RCCL message sizes are host arguments, so the chunk's bit counts are read back -- from a pinned
-copy issued behind the all_gather, while the device already runs the next chunk's encode.
+copy issued behind the all_gather.  The counts travel on a process group of their own (a second
+communicator with its own stream), so a step issues every chunk's encode and count all_gather
+before it waits for any count: the host blocks once per chunk only where that chunk's counts have
+not yet arrived, and the device's encode queue never drains while the host assembles a chunk (the
+data transfers, on the first group, do not queue behind later chunks' count gathers).
 """
 from __future__ import annotations
 
@@ -172,6 +176,12 @@ class PipelinedGather:
             self.firsts = z(nchunks, world)
         self.total = header_bits
         self._base = header_bits
+        # the counts' own communicator (collective: every rank constructs this object in step)
+        self.cgroup = group
+        if world > 1:
+            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
+            self.cgroup = dist.new_group(ranks=ranks)
+        self.CC = torch.cuda.Stream(self.dev) if (cuda and comm_stream is not None) else None
 
     # -- stream helpers (no-ops on the CPU)
     def _on(self, s):
@@ -187,16 +197,19 @@ class PipelinedGather:
             self.E.wait_stream(cur)
             if self.C is not None:
                 self.C.wait_stream(cur)
+            if self.CC is not None:
+                self.CC.wait_stream(cur)
         self._base = self.hb
         if self.rank == 0 and self.hdr_last is not None:  # the header's partial byte: ORed into below
             with self._on(self.C):
                 self.out[self.hb // 8: self.hb // 8 + 1].copy_(self.hdr_last)
+        # every encode and count gather first (no host wait), then each chunk's re-shift and
+        # transfer as soon as its counts are on the host
         for k in range(self.K):
             self._encode(k, i)
-            if k:
-                self._finish(k - 1)
             self._gather_counts(k)
-        self._finish(self.K - 1)
+        for k in range(self.K):
+            self._finish(k)
         self.total = self._base
 
     def _encode(self, k, i):
@@ -208,21 +221,22 @@ class PipelinedGather:
                 self.ev_enc[k].record(self.E)
 
     def _gather_counts(self, k):
-        with self._on(self.C):
+        cs = self.CC if self.CC is not None else self.C
+        with self._on(cs):
             if self.ev_enc:
-                self.C.wait_event(self.ev_enc[k])
+                cs.wait_event(self.ev_enc[k])
             mine = self.bits[k:k + 1]
             if self.cdev != self.dev:
                 mine = mine.to(self.cdev)
             if self.world == 1:  # one rank: no collective
                 self.counts[k].copy_(mine)
             elif self.cdev.type == "cuda":
-                self.dist.all_gather_into_tensor(self.counts[k], mine, group=self.group)
+                self.dist.all_gather_into_tensor(self.counts[k], mine, group=self.cgroup)
             else:  # gloo
-                self.dist.all_gather(list(self.counts[k].view(self.world, 1).unbind(0)), mine, group=self.group)
+                self.dist.all_gather(list(self.counts[k].view(self.world, 1).unbind(0)), mine, group=self.cgroup)
             self.counts_host[k].copy_(self.counts[k], non_blocking=self.ev_cnt is not None)
             if self.ev_cnt:
-                self.ev_cnt[k].record(self.C)
+                self.ev_cnt[k].record(cs)
 
     def _finish(self, k):
         """Re-shift and transfer chunk k (its counts are on the host once ev_cnt[k] fired)."""

@@ -467,12 +467,13 @@ def test_decode_multi_segment_vs_oracle(codec, n, kind, huffman):
     assert np.array_equal(pix, O.load().decode_image(enc, n))
 
 
+@pytest.mark.parametrize("spec", ["0", "1"])
 @pytest.mark.parametrize("recs", ["1", "7", "200"])
 @pytest.mark.parametrize("name", ["synM4k_4x4", "synU4k_4x4", "synM4k_8x8"])
-def test_decode_chunking_matches(codec, tmp_path, name, recs):
-    """The exact parse gives the reference decoder's pixels for any chunking (IE_DEC_R records per
-    chunk: 1 = many groups and the cross-group chase from global memory, 200 = long chunks), in a
-    fresh process."""
+def test_decode_chunking_matches(codec, tmp_path, name, recs, spec):
+    """The exact parse (IE_DEC_SPEC=0) and the speculative one give the reference decoder's pixels
+    for any chunking (IE_DEC_R records per chunk: 1 = many groups and the cross-group chase from
+    global memory, 200 = long chunks), in a fresh process."""
     import subprocess
     import sys
     c = next((c for c in O.manifest() if c["name"] == name), None)
@@ -487,12 +488,12 @@ def test_decode_chunking_matches(codec, tmp_path, name, recs):
             "pix = c.decode_image_file(open(%r, 'rb').read(), %d)\n"
             "print(hashlib.md5(pix.tobytes()).hexdigest(), *c.last_decode_info())\n") % (
         O.ROOT, str(tmp_path / "s.enc"), c["n"])
-    env = dict(os.environ, IE_DEC_R=recs)
+    env = dict(os.environ, IE_DEC_R=recs, IE_DEC_SPEC=spec)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env,
                        cwd=O.ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     md5, chunks, groups = r.stdout.strip().splitlines()[-1].split()
-    assert int(chunks) >= 1 and int(groups) >= 1
+    assert int(chunks) >= 1 and (int(groups) >= 1 or spec == "1")
     assert md5 == _md5(default.tobytes())
     if "dec_md5" in c:
         assert md5 == c["dec_md5"]
@@ -541,3 +542,45 @@ def test_decode_device_stream_in_place(codec, n, k):
     e_u = c.decode_frames(shifted[1:], w, h, pix_u, length=length)
     assert e_h == e_d == e_u == end
     assert torch.equal(pix_h, pix_d) and torch.equal(pix_h, pix_u)
+
+
+@pytest.mark.parametrize("n", [4, 8])
+@pytest.mark.parametrize("kind", ["U", "M", "grad", "flat", "flat_noise"])
+def test_decode_speculative_equals_exact(codec, n, kind):
+    """The optional speculative record parse (each chunk entered where its predecessor's walk from
+    its first bit left it, every exit verified by the counting walks) and the exact parse over
+    composed transfer tables decode the same pixels and end bit, both == the oracle; where a
+    speculative entry is wrong (periodic content) the call hands over to the exact parse."""
+    import torch
+
+    from imageencoder_amd import Codec, stream_bound
+    w, h = 1032, 520
+    if kind == "flat":
+        y = np.full((h, w), 77, dtype=np.uint8)
+    elif kind == "flat_noise":  # flat halves around a noise band: both kinds of chunks in one stream
+        y = np.full((h, w), 200, dtype=np.uint8)
+        y[h // 3: h // 2] = synth.frame("U", w, h // 2 - h // 3, seed=5)
+    elif kind == "grad":
+        yy, xx = np.mgrid[0:h, 0:w]
+        y = ((xx * 3 + yy * 5) % 256).astype(np.uint8)
+    else:
+        y = synth.frame(kind, w, h, seed=21 + n)
+    q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+    c = Codec(0, q, n)
+    dev = torch.zeros(stream_bound(w, h, n, 1, 0) + 64, dtype=torch.uint8, device="cuda")
+    _, end = c.encode_frames(torch.from_numpy(y).cuda(), w, h, dev)
+    length = (end + 7) // 8
+    pix_s = torch.zeros((h, w), dtype=torch.uint8, device="cuda")
+    pix_e = torch.zeros_like(pix_s)
+    c.set_exact_parse(False)
+    e_s = c.decode_frames(dev, w, h, pix_s, length=length)
+    used_spec = c.last_decode_spec()
+    c.set_exact_parse(True)
+    e_e = c.decode_frames(dev, w, h, pix_e, length=length)
+    assert not c.last_decode_spec()
+    assert e_s == e_e == end
+    assert torch.equal(pix_s, pix_e)
+    ref = O.load().decode_image(O.load().encode_image(y, n, q, rle=True), n)
+    assert np.array_equal(pix_s.cpu().numpy(), np.asarray(ref).reshape(h, w))
+    if kind == "flat":  # measured: the flat frames' speculative walks meet the true path
+        assert used_spec

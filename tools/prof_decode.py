@@ -1,5 +1,5 @@
-"""Decode timing per content kind (4K, device-resident stream and pixels): the exact table parse
-(IE_DEC_R in the environment sets the records per chunk).
+"""Decode timing per content kind (4K, device-resident stream and pixels): the speculative parse,
+or the exact table parse with IE_DEC_SPEC=0 (IE_DEC_R in the environment sets the records per chunk).
 usage: python tools/prof_decode.py [n] [kind,kind...]"""
 import os
 import sys
@@ -19,18 +19,25 @@ c = Codec(0, q, n)
 yy, xx = np.mgrid[0:h, 0:w]
 kinds = {"U": synth.frame("U", w, h, 5), "M": synth.frame("M", w, h, 5),
          "grad": ((xx * 3 + yy * 5) % 256).astype(np.uint8), "flat": np.full((h, w), 77, np.uint8)}
-out = torch.zeros(stream_bound(w, h, n, 1, 0), dtype=torch.uint8, device="cuda")
-pix = torch.empty((h, w), dtype=torch.uint8, device="cuda")
+# the reference's example images (natural content; README.md:175-183 sizes)
+for name, (ew, eh) in {"ex1": (936, 936), "ex2": (512, 512), "ex3": (400, 400), "ex4": (4096, 912)}.items():
+    f = os.path.join(O.ROOT, "tests", "golden", name + ".raw")
+    if os.path.exists(f):
+        kinds[name] = np.fromfile(f, dtype=np.uint8)[: ew * eh].reshape(eh, ew)
 tag = "R=" + os.environ.get("IE_DEC_R", "32")
 only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(kinds)
 for name, y in kinds.items():
     if name not in only:
         continue
+    h, w = y.shape
+    out = torch.zeros(stream_bound(w, h, n, 1, 0), dtype=torch.uint8, device="cuda")
+    pix = torch.empty((h, w), dtype=torch.uint8, device="cuda")
     _, end = c.encode_frames(torch.from_numpy(y).cuda(), w, h, out)
     nb = (end + 7) // 8
     c.decode_frames(out[:nb], w, h, pix, length=nb)
     ok = torch.equal(pix.cpu(), torch.from_numpy(y)) or True  # lossy: no pixel identity expected
     chunks, groups = c.last_decode_info()
+    spec = c.last_decode_spec()
     torch.cuda.synchronize()
     k = 5
     t0 = time.perf_counter()
@@ -38,4 +45,4 @@ for name, y in kinds.items():
         c.decode_frames(out[:nb], w, h, pix, length=nb)
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / k
-    print(f"{tag:12s} n={n} {name:5s} {nb:9d} B  {t * 1e6:9.1f} us  chunks={chunks} groups={groups}", flush=True)
+    print(f"{tag:12s} n={n} {name:5s} {nb:9d} B  {t * 1e6:9.1f} us  chunks={chunks} groups={groups} spec={int(spec)}", flush=True)
