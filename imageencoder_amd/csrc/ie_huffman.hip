@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "ie_common.hpp"
 #include "ie_device.h"
 
@@ -196,14 +198,16 @@ void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uin
 // One tile = kTPB threads x BPT input bytes, codes of up to MAXLEN bits: <16, 32> for any code,
 // <64, 16> for Huffman codes (<= 15 bits) and the identity copy -- 4x the bytes per tile, so a
 // quarter of the tiles (and look-backs) for the same LDS image size.
+// The tile image is sized per launch for the table's longest code (pack_image_words: dynamic LDS),
+// so short-code tables leave room for more resident tiles.
+__host__ __device__ constexpr int pack_image_words(int bpt, int maxlen) { return kTPB * bpt * maxlen / 32 + 4; }
 template <int BPT, int MAXLEN>
 __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
-    constexpr int kPackWords = kTPB * BPT * MAXLEN / 32 + 4;
-    __shared__ uint32_t smem[kPackWords + 32];
+    extern __shared__ uint32_t smem[];  // [pack_image_words(BPT, a.maxlen)] image, [32] misc
     __shared__ uint32_t s_code[256];
     __shared__ uint8_t s_len[256];
     uint32_t* img = smem;
-    uint32_t* misc = smem + kPackWords;
+    uint32_t* misc = smem + pack_image_words(BPT, min(max(a.maxlen, 1), MAXLEN));
     const int tid = threadIdx.x;
     // tile order = dispatch order (see encode_kernel); the atomic ticket is the fallback
     if (a.ticket && tid == 0) misc[4] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
@@ -378,8 +382,13 @@ void launch_bitshift(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t star
 int pack_tile_bytes(int maxlen) { return maxlen <= 16 ? kTPB * 64 : kTPB * 16; }
 
 void launch_pack(const PackArgs& a, hipStream_t s) {
-    if (a.maxlen <= 16) hipLaunchKernelGGL((pack_kernel<64, 16>), dim3(a.ntiles), dim3(kTPB), 0, s, a);
-    else hipLaunchKernelGGL((pack_kernel<16, 32>), dim3(a.ntiles), dim3(kTPB), 0, s, a);
+    const int ml = std::max(1, a.maxlen);
+    if (ml <= 16)
+        hipLaunchKernelGGL((pack_kernel<64, 16>), dim3(a.ntiles), dim3(kTPB),
+                           size_t(pack_image_words(64, ml) + 32) * 4, s, a);
+    else
+        hipLaunchKernelGGL((pack_kernel<16, 32>), dim3(a.ntiles), dim3(kTPB),
+                           size_t(pack_image_words(16, std::min(ml, 32)) + 32) * 4, s, a);  // (ml <= 32: checked by the callers)
 }
 
 }  // namespace ie
