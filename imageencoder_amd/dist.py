@@ -143,12 +143,15 @@ class PipelinedGather:
                                 (bits before it zero); runs on ``comm_stream``
     comm_dev                    device of the tensors handed to torch.distributed: the encode
                                 device for RCCL, "cpu" for gloo (staged copies; rehearsal/tests)
+    count_group                 the process group of the bit-count all_gathers (default: a new group
+                                over ``group``'s ranks -- ``new_group`` is collective over the
+                                default group, so then every process constructs this object)
     Rank 0's assembled stream is ``out[: (total + 7) // 8]`` after :meth:`step`.
     """
 
     def __init__(self, dist, rank: int, world: int, nframes: int, nchunks: int, header, header_bits: int,
                  seg_cap: int, root_cap: int, encode, shift, dev, comm_dev=None, enc_stream=None,
-                 comm_stream=None, group=None):
+                 comm_stream=None, group=None, count_group=None):
         import torch
         self.torch, self.dist, self.group = torch, dist, group
         self.rank, self.world, self.F, self.K = rank, world, nframes, nchunks
@@ -177,8 +180,8 @@ class PipelinedGather:
         self.total = header_bits
         self._base = header_bits
         # the counts' own communicator (collective: every rank constructs this object in step)
-        self.cgroup = group
-        if world > 1:
+        self.cgroup = count_group if count_group is not None else group
+        if world > 1 and count_group is None:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
             self.cgroup = dist.new_group(ranks=ranks)
         self.CC = torch.cuda.Stream(self.dev) if (cuda and comm_stream is not None) else None

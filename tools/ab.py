@@ -78,6 +78,9 @@ for path in args.libs:
 
     run(sizes=True)
     torch.cuda.synchronize()
+    fb = C.c_uint64(0)
+    if hasattr(L, "ie_last_fallbacks") and L.ie_last_fallbacks(hnd, C.byref(fb)) == 0:
+        print(f"{os.path.basename(os.path.dirname(path))}: FP64 fix-up requests per launch {fb.value}", flush=True)
     variants.append({"name": os.path.basename(os.path.dirname(path)) or path, "run": run, "out": out.clone(),
                      "pitch": pitch, "eb": eb.copy(), "t": []})
 
