@@ -162,14 +162,23 @@ struct DecArgs {
 #ifndef IE_REC_M
 #define IE_REC_M 1  // measured on 4K streams: 1 beats 2, 4 and 8 (occupancy over lane packing)
 #endif
+// tables per composition group: measured on 4K frames and the reference's example images, 32
+// beats 64 and 128 (more workgroups and 32-step chases instead of 128: 4K 4x4 noise 186 -> 175-180
+// us, 400x400 88 -> 81 us per decode; 16 is no faster)
+#ifndef IE_REC_G4
+#define IE_REC_G4 32
+#endif
+#ifndef IE_REC_G8
+#define IE_REC_G8 32
+#endif
 template <int N> struct RecGeom {
     static constexpr int D = 4 + 15 * (N * N + 1);
-    static constexpr int G = (N == 4) ? 128 : 64;  // tables per group ([G][D] 16-bit exits in LDS)
+    static constexpr int G = (N == 4) ? IE_REC_G4 : IE_REC_G8;  // tables per group ([G][D] 16-bit exits in LDS)
     static constexpr int M = IE_REC_M;              // chunks per table wave
     static constexpr int HSB = (N == 4) ? 10 : 11;  // claim hash slots per chunk: 1 << HSB
     static constexpr int HS = 1 << HSB;
 };
-constexpr int kRecMaxLevels = 4;
+constexpr int kRecMaxLevels = 6;  // G^6 chunks per decode call
 constexpr int kRecPosCap = 256;  // record positions kept per chunk (more: the decode walks again)
 constexpr int kRecWPB = 4;       // chunk waves per block of the per-chunk passes
 #ifndef IE_DEC_CHUNKS
