@@ -24,7 +24,7 @@ for name, (ew, eh) in {"ex1": (936, 936), "ex2": (512, 512), "ex3": (400, 400), 
     f = os.path.join(O.ROOT, "tests", "golden", name + ".raw")
     if os.path.exists(f):
         kinds[name] = np.fromfile(f, dtype=np.uint8)[: ew * eh].reshape(eh, ew)
-tag = "R=" + os.environ.get("IE_DEC_R", "32")
+tag = "R=" + os.environ.get("IE_DEC_R", "dflt")
 only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(kinds)
 for name, y in kinds.items():
     if name not in only:
