@@ -2332,16 +2332,17 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     const uint64_t nbits = uint64_t(len) * 8;
     const uint64_t span = nbits - start_bit;
     const uint64_t nblocks = uint64_t(nframes) * (w / n) * (h / n);
-    // chunking: about R records per chunk (IE_DEC_R; default 24 for 4x4, 32 for 8x8: measured
-    // with 32-table composition groups on 4K noise / mixed / flat frames and the reference's ex4
-    // against 16, 24, 32 and 48 -- 4x4 ex4 126 -> 115 us, mixed 197 -> 191 us, noise and flat
-    // unchanged; 8x8 noise takes 2-3x as long at any R but 32) so that every chunk's walks are
-    // short; C a multiple of 32, at least
+    // chunking: about R records per chunk (IE_DEC_R; default 24 for 4x4, 28 for 8x8: measured
+    // with 32-table composition groups on 4K noise / mixed / gradient / flat frames and the
+    // reference's ex1 / ex4 -- 4x4 against 16, 24, 32, 48: ex4 126 -> 115 us, mixed 197 -> 191 us,
+    // noise and flat unchanged; 8x8 against 20-32: noise 342 -> 258 us, ex1 376 -> 269 us,
+    // gradient 209 -> 181 us, flat 101 -> 112 us; 8x8 noise alone is erratic in R, 2.6x slower at
+    // 24) so that every chunk's walks are short; C a multiple of 32, at least
     // 256 bits, at most 2^15 (16-bit record positions; a table wave's LDS -- the chunk's bits and
     // valid-header bitmap -- stays small)
     const int G = ie::rec_group_chunks(n), D = ie::rec_entry_span(n);
     static const char* rs = getenv("IE_DEC_R");
-    const uint64_t recs = rs ? std::max<uint64_t>(1, strtoull(rs, nullptr, 10)) : (n == 4 ? 24 : 32);
+    const uint64_t recs = rs ? std::max<uint64_t>(1, strtoull(rs, nullptr, 10)) : (n == 4 ? 24 : 28);
     const uint64_t want = std::max<uint64_t>((nblocks + recs - 1) / recs, 1);
     uint64_t C = (span + want - 1) / want;
     C = std::min<uint64_t>(std::max<uint64_t>((C + 31) / 32 * 32, 256), uint64_t(1) << 15);
