@@ -84,7 +84,10 @@ __global__ __launch_bounds__(kTPB) void scan_counts_kernel(const uint32_t* count
 //   LDS   the 2^kHufL1 first-level entries (codes of <= kHufL1 bits resolve there)
 constexpr int kHufL1 = 11;
 constexpr int kHufD = 15;   // entry offsets of a chunk: codes are at most 15 bits
-constexpr int kHufG = 256;  // tables per composition group
+#ifndef IE_HUF_G
+#define IE_HUF_G 256
+#endif
+constexpr int kHufG = IE_HUF_G;  // tables per composition group
 struct HufArgs {
     const uint32_t* words;
     uint64_t nbits, start_bit, chunk_bits;
