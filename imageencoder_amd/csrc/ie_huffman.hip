@@ -379,13 +379,16 @@ void launch_bitshift(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t star
                        w0, w1);
 }
 
-int pack_tile_bytes(int maxlen) { return maxlen <= 16 ? kTPB * 64 : kTPB * 16; }
+#ifndef IE_PACK_BPT
+#define IE_PACK_BPT 32  // input bytes per thread of a pack tile for codes of <= 16 bits (C5: 32 -5 % against 64 and 128)
+#endif
+int pack_tile_bytes(int maxlen) { return maxlen <= 16 ? kTPB * IE_PACK_BPT : kTPB * 16; }
 
 void launch_pack(const PackArgs& a, hipStream_t s) {
     const int ml = std::max(1, a.maxlen);
     if (ml <= 16)
-        hipLaunchKernelGGL((pack_kernel<64, 16>), dim3(a.ntiles), dim3(kTPB),
-                           size_t(pack_image_words(64, ml) + 32) * 4, s, a);
+        hipLaunchKernelGGL((pack_kernel<IE_PACK_BPT, 16>), dim3(a.ntiles), dim3(kTPB),
+                           size_t(pack_image_words(IE_PACK_BPT, ml) + 32) * 4, s, a);
     else
         hipLaunchKernelGGL((pack_kernel<16, 32>), dim3(a.ntiles), dim3(kTPB),
                            size_t(pack_image_words(16, std::min(ml, 32)) + 32) * 4, s, a);  // (ml <= 32: checked by the callers)

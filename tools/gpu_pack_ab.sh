@@ -1,7 +1,9 @@
+# C5 bench lines (Huffman pass timing) of variant libraries (VARS)
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R
-for i in 1 2; do for v in base pk; do
+for i in 1 2; do for v in ${VARS:-base}; do
 IE_LIB=imageencoder_amd/lib/var_$v/libie_hip.so timeout -k 10 200 python bench.py --workload c5 --steps 10 --warmup 2 --no-cpu --no-single-frame --no-e2e --no-decode --no-gop > /tmp/b.json 2>/tmp/b.err || { tail -5 /tmp/b.err; exit 1; }
 python3 -c "
 import json;l=[x for x in open('/tmp/b.json') if x.startswith('{')][-1];d=json.loads(l)
-print('$v', d['ms_per_step'], d.get('huffman_roofline'), d.get('check',{}).get('bit_exact'))"
+h=d.get('huffman_roofline',{})
+print('$v', d['ms_per_step'], h.get('hist_us'), h.get('pack_us'), d.get('check',{}).get('bit_exact'))"
 done; done
