@@ -24,7 +24,10 @@ namespace ie {
 namespace {
 
 constexpr int kMB = 16;
-constexpr int kPfPer = 2;                      // records per emitting thread
+#ifndef IE_PF_PER
+#define IE_PF_PER 2
+#endif
+constexpr int kPfPer = IE_PF_PER;              // records per emitting thread
 constexpr int kPfTileBlocks = kTPB * kPfPer;  // record-length tile of the scan
 __constant__ int kSx[9] = {0, 1, 1, 0, -1, -1, -1, 0, 1};  // algo.cpp:90-100
 __constant__ int kSy[9] = {0, 0, 1, 1, 1, 0, -1, -1, -1};

@@ -52,7 +52,7 @@ print(f"{w}x{h} x{F} merange={mer}: gop=1 {tI * 1e3:.3f} ms ({tI / F * 1e6:.1f} 
 
 # reference CPU baseline: its own encoder binary (OpenMP) on a 4-frame sample, whole-program time
 ref = os.path.join(ROOT, "oracle", "_ref", "encoder")
-if os.path.exists(ref):
+if os.path.exists(ref) and not os.environ.get("IE_NO_REF"):
     Fs = 4
     with tempfile.TemporaryDirectory() as d:
         open(os.path.join(d, "in.raw"), "wb").write(synth.yuv420(y[:Fs]))
