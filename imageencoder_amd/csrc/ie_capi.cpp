@@ -536,7 +536,7 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     c->last_fix_words = (L.mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
     a.tab = c->d_tab;
     a.rec_bits = c->h_tab->rec_bits;
-    a.tri = (c->n == 4 && (a.rec_bits - 4) / 17 <= 11) ? 1 : 0;  // bl_max = (rec_bits - 4) / (1 + N*N)
+    a.tri = (c->n == 4 && (a.rec_bits - 4) / 17 <= 10) ? 1 : 0;  // bl_max = (rec_bits - 4) / (1 + N*N); 3 bl <= 30
 #ifdef IE_NOTRI  // A/B aid: pairs only
     a.tri = 0;
 #endif

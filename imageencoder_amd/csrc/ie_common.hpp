@@ -192,6 +192,7 @@ constexpr int kLbAhead = IE_LB_AHEAD;
 // deep: the launch's tiles all reach their look-back at about the same time (a launch too small to
 // fill the chip), so a tile's nearest inclusive predecessor is far away: the windows after the
 // first probe are issued at once, before it is evaluated.
+template <int kLbAhead = ie::kLbAhead>
 __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
                                   unsigned* err, unsigned* rounds = nullptr, bool deep = false) {
     const int lane = lane_id();

@@ -1297,6 +1297,485 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     STAMP(9);
 }
 
+// round_block<4> with the rounding done pair by pair in zig-zag order and each packed word
+// pinned as soon as it exists: the 16 magic-added quotients never live at once (register
+// pressure of encode4w_kernel's fourth slot).  Same results bit for bit.
+__device__ __forceinline__ float round_block_lean4(const EncTables* __restrict__ tab, const float (&t)[16],
+                                                   uint32_t (&zp)[8], uint32_t* sflags) {
+    constexpr int S0 = Structural<4>::k[0], S1 = Structural<4>::k[1], S2 = Structural<4>::k[2];
+    const bool dcx = tab->dc_exact != 0;
+    float emax = 0.0f;
+    uint32_t sf = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        uint32_t yb[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int k = ZigZag<4>::idx[2 * j + h];
+            const float y = t[k] + kMagic;
+            const float e = fabsf(t[k] - (y - kMagic));
+            yb[h] = __float_as_uint(y);
+            if (k == 0) {
+                const uint32_t dc = uint32_t(int(truncf(t[0] + copysignf(0.5f, t[0]))));
+                yb[h] = dcx ? dc : yb[h];
+                emax = dcx ? emax : fmaxf(emax, e);
+            } else if (k == S0) {
+                sf |= (e >= tab->lim[S0]) ? 1u : 0u;
+            } else if (k == S1) {
+                sf |= (e >= tab->lim[S1]) ? 2u : 0u;
+            } else if (k == S2) {
+                sf |= (e >= tab->lim[S2]) ? 4u : 0u;
+            } else {
+                emax = fmaxf(emax, e);
+            }
+        }
+        zp[j] = __builtin_amdgcn_perm(yb[1], yb[0], 0x05040100u);
+        asm volatile("" : "+v"(zp[j]));
+        if (j & 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    *sflags = sf;
+    return emax;
+}
+
+// =============================================================================================
+// encode4w_kernel -- the 4x4 FAST encoder with WAVE-LOCAL emission.
+//
+// Same tile (1024 blocks, 256 threads, one chain element, the same chain granules) and the same
+// arithmetic as encode_kernel<4, false> (quot4 + round_block + the compacted FP64 fix-up, so the
+// Trk exactness argument carries over unchanged), laid out so that a wave needs its workgroup
+// only twice:
+//   * wave w owns the tile's blocks [256w, 256w + 256) (64 groups of four, raster order); lane l
+//     computes block 64b + l of that run in SLOT b = 0..3, so a slot is 64 consecutive blocks of
+//     the stream and one wave scan (DPP) places every record inside its slot;
+//   * the pixels land in the wave's own LDS region by DMA as [row][256 blocks] words (a slot
+//     reads them conflict-free, no other wave touches them); after the fix-up the same region
+//     holds two slot images in turn: slots 0 and 1 are emitted while wave 0 resolves the tile's
+//     look-back, then each slot is stored as soon as its image is complete and its buffer takes
+//     slot b + 2;
+//   * a word shared by two waves of the tile is written by the earlier wave, which ORs in the
+//     later wave's first bits (its head word, saved in LDS before the look-back barrier); a word
+//     shared with the predecessor tile is completed with that tile's tail granule as in
+//     encode_kernel.
+// LDS per tile 20.5 KB (encode_kernel<4>: ~27 KB), so up to seven tiles per CU.
+// Preconditions (launch_encode checks them): whole 16-byte groups (vec_ok, bx % 4 == 0), at
+// least 8 groups in every tile (groups_per_frame % 8 == 0: every wave segment >= 160 bits) and
+// slot images that fit half a region (rec_bits <= 252).
+// =============================================================================================
+#ifndef IE_ENC_W
+#define IE_ENC_W 1  // 0: every 4x4 FAST launch runs encode_kernel<4> (A/B builds)
+#endif
+#ifndef IE_W_DBG
+#define IE_W_DBG 0
+#endif
+#ifndef IE_W_AHEAD
+#define IE_W_AHEAD 2  // look-back windows per round trip (each holds 4 VGPRs live beside slots 2-3)
+#endif
+#ifndef IE_W_WAVES
+#define IE_W_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD): 80 VGPRs, no scratch
+#endif
+constexpr int kWReg = 1024;  // words per wave region: [4 rows][256 blocks] pixels, then two slot images
+constexpr int kWBuf = 512;   // words per slot image
+constexpr int kWTask = 128;  // words per wave: fix-up tasks [64] + results [64]
+constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9] excl, [10] ptail, [11] tail pending, [12] ticket
+constexpr int kWRows = 16 * 16 + 3 * 16;  // FP64 rows P[16][16], then S, rq, qd (doubles)
+constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc) * 4 + kWRows * 8;
+
+// Inclusive scan over the 64 lanes of a wave by DPP row shifts and row broadcasts (six VALU).
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xF, 0xF, true));   // row_shr:1
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xF, 0xF, true));   // row_shr:2
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xF, 0xF, true));   // row_shr:4
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xF, 0xF, true));   // row_shr:8
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return v;
+}
+
+// One slot image I (bit 0 at absolute stream bit X) to the output words, by one wave: words
+// [r0, nw) counted from floor(X / 32), word r = alignbit(I[r - 1], I[r], X % 32) with I[-1] =
+// prev (the 32 bits before X); the partial word nw is left to whoever writes the next bits.
+__device__ __forceinline__ void store_slot(uint32_t* __restrict__ out, const uint32_t* I, uint64_t X, uint32_t nw,
+                                           uint32_t r0, uint32_t prev, int lane) {
+    if (nw <= r0) return;
+    const uint64_t w0 = X >> 5;
+    const uint32_t s = uint32_t(X) & 31u;
+    auto word = [&](uint32_t r) -> uint32_t {
+        const uint32_t am = I[max(r, 1u) - 1u];
+        return bswap32(__builtin_amdgcn_alignbit(r ? am : prev, I[r], s));
+    };
+    const uint32_t hd = min(nw - r0, uint32_t((4u - uint32_t((w0 + r0) & 3u)) & 3u));
+    if (uint32_t(lane) < hd) out[w0 + r0 + lane] = word(r0 + lane);
+    const uint32_t rq = r0 + hd, nq = (nw - rq) >> 2;
+    for (uint32_t q = lane; q < nq; q += 64) {
+        const uint32_t r = rq + 4u * q;
+        const uint32_t am = I[max(r, 1u) - 1u];
+        const uint32_t a0 = r ? am : prev;
+        const uint32_t b0 = I[r], b1 = I[r + 1], b2 = I[r + 2], b3 = I[r + 3];
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u v = {bswap32(__builtin_amdgcn_alignbit(a0, b0, s)), bswap32(__builtin_amdgcn_alignbit(b0, b1, s)),
+                       bswap32(__builtin_amdgcn_alignbit(b1, b2, s)), bswap32(__builtin_amdgcn_alignbit(b2, b3, s))};
+        __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(out + w0 + r));
+    }
+    const uint32_t rt = rq + 4u * nq;
+    if (uint32_t(lane) < nw - rt) out[w0 + rt + lane] = word(rt + lane);
+}
+
+// The last 32 bits of the stream up to the end of a slot image of n bits, given the 32 bits
+// before it (prev).
+__device__ __forceinline__ uint32_t slot_tail32(const uint32_t* I, uint32_t n, uint32_t prev) {
+    if (n >= 32) return image_tail32(I, n);
+    return n ? ((prev << n) | (I[0] >> (32u - n))) : prev;
+}
+
+__global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, const EncTables* __restrict__ tab) {
+    constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar registers
+    uint32_t* const reg = smem + wv * kWReg;  // this wave's pixels, later its two slot images
+    uint32_t* const task = smem + 4 * kWReg + wv * kWTask;
+    uint32_t* const res = task + 64;
+    uint32_t* const misc = smem + 4 * kWReg + 4 * kWTask;
+    double* const srow = reinterpret_cast<double*>(misc + kWMisc);
+
+    int t;
+    if (a.ticket) {
+        if (tid == 0) misc[12] = uint32_t(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+        lds_barrier();
+        t = __builtin_amdgcn_readfirstlane(int(misc[12]));
+        if (t >= a.ntiles) return;
+    } else {
+        t = int(blockIdx.x);
+    }
+    // every coefficient's FP64 row and its S, rq, qd: the fix-up reads them from LDS
+    for (int i = tid; i < kWRows; i += TPB)
+        srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
+                : (i < NN * NN + 2 * NN) ? tab->rq[i - NN * NN - NN] : tab->qd[i - NN * NN - 2 * NN];
+    const TileGeo g = tile_geo<4, 4>(a, t, tid);
+    const uint64_t start_bit = a.start_dev ? *a.start_dev : a.start_bit;
+    const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
+    // groups in this tile / in this wave (>= 8 per tile: launch precondition)
+    const int ng = min(TPB, a.groups_per_frame - tif * TPB);
+    const int nbw = 4 * min(64, max(0, ng - 64 * wv));  // blocks of this wave
+    const int wlast = (ng - 1) >> 6;                    // the tile's last non-empty wave
+    if (!(IE_W_DBG & 64) && g.nblk) {
+        const uint8_t* base = a.y + size_t(frame) * a.frame_pitch + size_t(g.byi) * N * a.stride + size_t(g.bx0) * N;
+#pragma unroll
+        for (int r = 0; r < N; r++)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
+                                             (__attribute__((address_space(3))) void*)(reg + r * 256), 16, 0, 0);
+    }
+    lds_barrier();                                            // srow visible (the pixel DMA stays in flight)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
+
+    // ------------------------------------------------------------ transform + quantise, 4 slots
+    uint32_t zp[NS][NP];
+    uint32_t flags = 0;  // 4 bits per slot: structural s (bits 0-2), whole block (bit 3)
+#pragma unroll
+    for (int b = 0; b < NS; b++) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t rows[N][1];
+#pragma unroll
+        for (int r = 0; r < N; r++) rows[r][0] = reg[r * 256 + 64 * b + lane];
+        float x[NN];
+        block_pixels<N, 1>(rows, 0, x);
+        uint32_t sf;
+        float emax;
+        if (IE_W_DBG & 32) {  // profiling: no transform (quotients = pixels / 64)
+#pragma unroll
+            for (int k = 0; k < NN; k++) x[k] *= 0.015625f;
+            emax = round_block_lean4(tab, x, zp[b], &sf);
+            sf = 0;
+            emax = 0.0f;
+        } else {
+            quotients<N>(tab, x);
+            emax = round_block_lean4(tab, x, zp[b], &sf);
+        }
+        const uint32_t fb = (emax >= tab->lim_min) ? 8u : sf;
+        if (64 * b + lane < nbw) flags |= fb << (4 * b);
+        // pin the packed words here: otherwise the packing sinks to its first use and the 16
+        // unpacked quotients of every slot stay live across the slots (spills)
+#pragma unroll
+        for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
+        asm volatile("" : "+v"(flags));
+    }
+
+    // ------------------------------------------------------------ FP64 fix-up (compacted per wave)
+    auto block_px = [&](int b, int owner) {
+        BlockPx<N> px;
+#pragma unroll
+        for (int r = 0; r < N; r++) px.w[r] = reg[r * 256 + 64 * b + owner];
+        return px;
+    };
+    if (!(IE_W_DBG & 1) && __ballot(flags != 0)) {
+        const uint32_t sf = flags & 0x7777u;
+        const uint32_t cnt = __popc(sf);
+        uint32_t pre = 0, total = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {  // cnt <= 12
+            const uint64_t bm = __ballot((cnt >> k) & 1u);
+            pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+            total += uint32_t(__popcll(bm)) << k;
+        }
+        for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+            uint32_t m = sf, i = pre - r0;
+            while (m) {
+                const int bit = __ffs(m) - 1;
+                m &= m - 1;
+                if (i < 64u) task[i] = (uint32_t(lane) << 4) | uint32_t(bit);
+                i++;
+            }
+            wave_sync();
+            if (uint32_t(lane) < total - r0) {
+                const uint32_t tk = task[lane];
+                const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
+                const BlockPx<N> px = block_px(b, owner);
+                const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
+                res[lane] = uint32_t(exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                       srow[NN * NN + 2 * NN + k], px)) & 0xFFFFu;
+            }
+            wave_sync();
+            m = sf;
+            i = pre - r0;
+            while (m) {
+                const int bit = __ffs(m) - 1;
+                m &= m - 1;
+                if (i < 64u) {
+                    const uint32_t v = res[i];
+                    const int b = bit >> 2, s = bit & 3;
+#pragma unroll
+                    for (int bb = 0; bb < NS; bb++)
+#pragma unroll
+                        for (int ss = 0; ss < 3; ss++) {
+                            const int zpos = Structural<N>::zpos(ss);
+                            if (b == bb && s == ss)
+                                zp[bb][zpos >> 1] = (zpos & 1) ? ((zp[bb][zpos >> 1] & 0xFFFFu) | (v << 16))
+                                                               : ((zp[bb][zpos >> 1] & 0xFFFF0000u) | v);
+                        }
+                }
+                i++;
+            }
+            wave_sync();
+        }
+        // whole-block requests (rare): all 16 coefficients in FP64, one per lane, four blocks a round
+        const uint32_t wf = flags & 0x8888u;
+        if (__ballot(wf != 0)) {
+            const uint32_t nb = __popc(wf);
+            uint32_t pb = 0, tb = 0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {  // nb <= 4
+                const uint64_t bm = __ballot((nb >> k) & 1u);
+                pb += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+                tb += uint32_t(__popcll(bm)) << k;
+            }
+            for (uint32_t r0 = 0; r0 < tb; r0 += 4) {
+                uint32_t m = wf, j = pb - r0;
+                while (m) {
+                    const int b = (__ffs(m) - 1) >> 2;
+                    m &= m - 1;
+                    if (j < 4u) task[j] = (uint32_t(lane) << 4) | uint32_t(b);
+                    j++;
+                }
+                wave_sync();
+                if (uint32_t(lane >> 4) < tb - r0) {
+                    const uint32_t tk = task[lane >> 4];
+                    const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
+                    const BlockPx<N> px = block_px(b, owner);
+                    res[lane] = uint32_t(exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                           srow[NN * NN + 2 * NN + k], px)) & 0xFFFFu;
+                }
+                wave_sync();
+                m = wf;
+                j = pb - r0;
+                while (m) {
+                    const int b = (__ffs(m) - 1) >> 2;
+                    m &= m - 1;
+                    if (j < 4u) {
+                        const uint32_t* rr = res + 16 * j;
+#pragma unroll
+                        for (int jj = 0; jj < NP; jj++) {
+                            const uint32_t w = rr[ZigZag<N>::idx[2 * jj]] | (rr[ZigZag<N>::idx[2 * jj + 1]] << 16);
+#pragma unroll
+                            for (int bb = 0; bb < NS; bb++) zp[bb][jj] = (b == bb) ? w : zp[bb][jj];
+                        }
+                    }
+                    j++;
+                }
+                wave_sync();
+            }
+        }
+    }
+    {
+        const unsigned wsum = unsigned(wave_sum64(__popc(flags)));
+        if (lane == 0) a.wave_fix[size_t(t) * (TPB / 64) + wv] = wsum;
+    }
+
+    // ------------------------------------------------------------ sizing + the wave's offsets
+    uint32_t blw[NS], rb[NS];
+    const uint32_t k0 = uint32_t(tif * TPB + 64 * wv) * 4u;  // the wave's first block (frame raster order)
+#pragma unroll
+    for (int b = 0; b < NS; b++) {
+        const bool valid = 64 * b + lane < nbw;
+        if (!(IE_W_DBG & 4) && a.coef && valid) {
+            int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + k0 + 64 * b + lane) * NN;
+#pragma unroll
+            for (int k = 0; k < NN; k++) {
+                const int kz = ZigZagInv<N>::pos[k];
+                dst[k] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        blw[b] = size_block<N>(zp[b], a.rle, &rb[b]);
+        rb[b] = valid ? rb[b] : 0u;
+        asm volatile("" : "+v"(blw[b]), "+v"(rb[b]));
+#pragma unroll
+        for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // slot pairs packed into 16-bit halves (a slot holds <= 64 * 252 bits)
+    const uint32_t s01 = rb[0] | (rb[1] << 16), s23 = rb[2] | (rb[3] << 16);
+    const uint32_t i01 = wave_incl_scan_dpp(s01), i23 = wave_incl_scan_dpp(s23);
+    const uint32_t t01 = __builtin_amdgcn_readlane(i01, 63), t23 = __builtin_amdgcn_readlane(i23, 63);
+    const uint32_t e01 = i01 - s01, e23 = i23 - s23;  // exclusive, per half (no borrow: each half >= 0)
+    uint32_t T[NS], off[NS];
+    T[0] = t01 & 0xFFFFu;
+    T[1] = t01 >> 16;
+    T[2] = t23 & 0xFFFFu;
+    T[3] = t23 >> 16;
+    off[0] = e01 & 0xFFFFu;
+    off[1] = e01 >> 16;
+    off[2] = e23 & 0xFFFFu;
+    off[3] = e23 >> 16;
+    const uint32_t S1 = T[0], S2 = S1 + T[1], S3 = S2 + T[2], Tw = S3 + T[3];
+    if (lane == 0) misc[wv] = Tw;
+    lds_barrier();  // ---- the tile's bit count and this wave's place in it
+
+    uint32_t A = 0, W = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
+        A += v;
+        W += (w < wv) ? v : 0u;
+    }
+    if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);  // successors may resolve now
+    Probe pr{0, 0, 0};
+    if (wv == 0 && chain_pos != 0) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);  // in flight while emitting
+
+    // slot images: buffer 0 = reg[0 .. kWBuf), buffer 1 = reg[kWBuf .. 2 kWBuf); emission takes
+    // absolute LDS bit addresses (scatter_bits' ds_or addresses LDS from byte 0)
+    const uint32_t buf_bit0 = uint32_t(wv * kWReg) * 32u;
+    auto zero_buf = [&](int x, uint32_t bits) {
+        uint32_t* B = reg + x * kWBuf;
+        const uint32_t nq = (bits + 127u) >> 7;  // 16-byte groups
+        for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(B + 4 * q) = u32x4{0u, 0u, 0u, 0u};
+    };
+    auto emit_slot = [&](int b) {
+        if (!(IE_W_DBG & 8) && rb[b]) {
+            const uint32_t p = buf_bit0 + uint32_t(b & 1) * (kWBuf * 32u) + off[b];
+            if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
+            else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
+        }
+    };
+    zero_buf(0, T[0]);
+    zero_buf(1, T[1]);
+    wave_sync();
+    emit_slot(0);
+    emit_slot(1);
+    wave_sync();
+    if (lane == 0 && Tw) misc[4 + wv] = reg[0];  // the wave's first 32 bits
+
+    // ------------------------------------------------------------ look-back (wave 0)
+    const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
+    uint32_t* const out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
+    if (wv == 0) {
+        uint64_t excl = 0;
+        uint32_t ptail = 0, pend = 0;
+        if (chain_pos == 0) {
+            // chain start: the bits before start_bit belong to the caller (header)
+            const uint32_t s = uint32_t(start_bit & 31);
+            ptail = s ? (bswap32(out[start_bit >> 5]) >> (32 - s)) : 0u;
+        } else if (IE_W_DBG & 16) {  // profiling: no look-back (every tile at a made-up offset)
+            excl = uint64_t(tif) * 110000u;
+            if (lane == 0) publish(a.st, t, 1, a.tag, excl + A);
+        } else {
+            excl = lookback_wave<IE_W_AHEAD>(pr, a.st, t, chain_pos, step, a.tag, a.err, nullptr, a.deep_lb != 0);
+            const bool have = uint32_t(pr.gt >> 56) == a.tag;  // (lane 0's probe read the tail)
+            const bool split = ((start_bit + excl) & 31) != 0;
+            ptail = have ? uint32_t(pr.gt) : 0u;
+            pend = (!have && split) ? 1u : 0u;
+        }
+        if (lane == 0) {
+            if (chain_pos != 0) publish(a.st, t, 1, a.tag, excl + A);
+            misc[8] = uint32_t(excl);
+            misc[9] = uint32_t(excl >> 32);
+            misc[10] = ptail;
+            misc[11] = pend;
+            const uint64_t P = start_bit + excl;
+            if (tif == 0) a.frame_start[frame] = P;
+            if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
+        }
+    }
+    lds_barrier();  // ---- the tile's position
+
+    // ------------------------------------------------------------ store, slot by slot
+    if (!(IE_W_DBG & 2) && Tw) {
+        const uint64_t excl = uint64_t(__builtin_amdgcn_readfirstlane(misc[8])) |
+                              (uint64_t(__builtin_amdgcn_readfirstlane(misc[9])) << 32);
+        const uint64_t Xw = start_bit + excl + W;
+        const bool pend = __builtin_amdgcn_readfirstlane(misc[11]) != 0u;
+        // the wave's first word is written by the previous wave (or, pending, later by this one)
+        const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
+        uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[10]) : 0u;
+        // slot b is stored from buffer b & 1 as soon as it is complete; slot b + 2 is then emitted
+        // into the same buffer (one wave's LDS operations complete in order)
+        auto store_b = [&](int b, uint32_t Sb) {
+            if (!T[b]) return;
+            const uint64_t Xb = Xw + Sb;
+            const uint32_t nw = uint32_t(((Xb + T[b]) >> 5) - (Xb >> 5));
+            const uint32_t* I = reg + (b & 1) * kWBuf;
+            store_slot(out, I, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
+            prev = slot_tail32(I, T[b], prev);
+        };
+        auto refill = [&](int b) {
+            if (!T[b]) return;
+            wave_sync();
+            zero_buf(b & 1, T[b]);
+            wave_sync();
+            emit_slot(b);
+            wave_sync();
+        };
+        store_b(0, 0u);
+        __builtin_amdgcn_sched_barrier(0);
+        refill(2);
+        __builtin_amdgcn_sched_barrier(0);
+        store_b(1, S1);
+        __builtin_amdgcn_sched_barrier(0);
+        refill(3);
+        __builtin_amdgcn_sched_barrier(0);
+        store_b(2, S2);
+        __builtin_amdgcn_sched_barrier(0);
+        store_b(3, S3);
+        const uint64_t E = Xw + Tw;
+        const uint32_t e = uint32_t(E) & 31u;
+        if (lane == 0) {
+            if (e) {  // the wave's last, partial word
+                if (wv < wlast) out[E >> 5] = bswap32((prev << (32u - e)) | (misc[4 + wv + 1] >> e));
+                else if (chain_last) out[E >> 5] = bswap32(prev << (32u - e));
+            }
+            if (wv == wlast) publish(a.st, t, 2, a.tag, prev);  // the tile's last 32 bits
+            if (wv == 0 && pend) {  // the first word, with the predecessor's tail
+                const uint32_t pt = wait_tail(a.st, t - step, a.tag, a.err);
+                const uint32_t s = uint32_t(Xw) & 31u;
+                out[Xw >> 5] = bswap32((pt << (32u - s)) | (misc[4] >> s));
+            }
+        }
+    }
+}
+
+void launch_encode4w(const EncArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(encode4w_kernel, dim3(a.ntiles), dim3(256), kWLdsBytes, s, a, a.tab);
+}
+
 // The streamed host path's per-image header words: word i (read from page-locked host memory
 // the device maps, one PCIe read per image) to dst[i * pitch_words] -- instead of an SDMA copy
 // that would queue behind the chunk's pixel upload on the copy engine.
@@ -1322,8 +1801,16 @@ int encode_small_tiles() {
 
 int encode_threads_per_tile() { return kEncTPB; }
 
+void launch_encode4w(const EncArgs& a, hipStream_t s);
+
 void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt) {
     EncArgs a = a0;
+    // 4x4 FAST over whole 16-byte groups: the wave-local encoder (encode4w_kernel)
+    if (IE_ENC_W && n == 4 && !exact && !a.hist && bpt == 4 && a.vec_ok && a.bx % 4 == 0 &&
+        a.groups_per_frame % 8 == 0 && a.rec_bits <= 252 && !a.ablate && !a.stamps) {
+        launch_encode4w(a, s);
+        return;
+    }
     a.img_words = image_words_for(n, bpt, a.rec_bits);
     if (n == 4 && a.img_words < fix_words<4>()) a.img_words = fix_words<4>();
     if (n == 8 && a.img_words < kFix8Words) a.img_words = kFix8Words;
