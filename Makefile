@@ -18,7 +18,7 @@ all: lib host oracle
 
 lib: $(LIBDIR)/libie_hip.so
 
-$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp $(CSRC)/ie_dct.h include/ie_hip.h
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp $(CSRC)/ie_dct.h $(CSRC)/ie_recbits.h include/ie_hip.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -61,7 +61,7 @@ ref:
 # Check the exact FP64 paths really are unfused: dump the gfx950 ISA of the
 # encode, decode and P-frame kernels and scan it (tools/asmcheck.py; also reports VGPRs / scratch).
 ASMS := $(OBJDIR)/asm/ie_encode.s $(OBJDIR)/asm/ie_decode.s $(OBJDIR)/asm/ie_pframe.s
-$(OBJDIR)/asm/%.s: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp $(CSRC)/ie_dct.h
+$(OBJDIR)/asm/%.s: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp $(CSRC)/ie_dct.h $(CSRC)/ie_recbits.h
 	@mkdir -p $(OBJDIR)/asm
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o $@
 asmcheck: $(ASMS)

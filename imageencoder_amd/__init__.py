@@ -439,10 +439,11 @@ class Codec:
         self._chk(self.L.ie_last_decode_info(self.h, C.byref(f), C.byref(r)))
         return int(f.value), int(r.value)
 
-    def set_exact_parse(self, exact: bool) -> None:
+    def set_exact_parse(self, exact: bool, warm: int = 0) -> None:
         """Record decodes parse exactly (composed transfer tables) instead of speculatively first
-        (ie_set_exact_parse)."""
-        self._chk(self.L.ie_set_exact_parse(self.h, int(bool(exact))))
+        (ie_set_exact_parse); a speculative parse may start each chunk's walk ``warm`` (<= 8)
+        chunks early."""
+        self._chk(self.L.ie_set_exact_parse(self.h, 1 if exact else -min(8, max(0, int(warm)))))
 
     def last_decode_spec(self) -> bool:
         """True when the last record decode was completed by the speculative parse."""

@@ -113,7 +113,8 @@ struct ie_ctx {
     int last_chunks = 0;               // chunks of the last record decode
     int last_groups = 0;               // and their groups
     int last_spec = 0;                 // 1: the last record decode was the speculative parse
-    int spec_parse = 0;                // ie_set_exact_parse(ctx, 0): speculative record parse first
+    int spec_parse = 0;                // ie_set_exact_parse(ctx, <= 0): speculative record parse first
+    int spec_warm = 0;                 // ie_set_exact_parse(ctx, -w): w warm-up chunks (<= 8)
     unsigned long long* d_first = nullptr;  // [256]
     ie_pipe* pipe = nullptr;           // streamed host path of image batches (created on first use)
     // P-frame videos (ie_encode_gop): reconstructed frames (two, alternating), the prediction
@@ -1262,7 +1263,8 @@ int ie_last_decode_info(ie_ctx* c, int* chunks, int* levels) {
 
 int ie_set_exact_parse(ie_ctx* c, int exact) {
     if (!c) return IE_EINVAL;
-    c->spec_parse = exact ? 0 : 1;
+    c->spec_parse = exact > 0 ? 0 : 1;
+    c->spec_warm = exact < 0 ? std::min(8, -exact) : 0;
     return IE_OK;
 }
 
@@ -1389,9 +1391,7 @@ int pack(ie_ctx* c, const uint8_t* bytes, size_t n, const uint32_t* code, const 
         a.chain_end = c->d_chain_end;
         a.err = c->d_err;
         a.maxlen = int(maxlen);
-        if ((r = stage_mark(c, 2))) return r;
-        ie::launch_pack(a, c->stream);
-        if ((r = stage_mark(c, 3))) return r;
+        ie::launch_pack(a, c->stream);  // (no stage events: ie_last_stage_ms reports the batched calls)
         HIPCHK(c, hipGetLastError());
         if (c->use_ticket) c->ticket_base += uint64_t(ntiles);
         if (!end_bit && out_dev) {
@@ -2319,11 +2319,12 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     if (start_bit > uint64_t(len) * 8) return fail(c, IE_EINVAL, "start_bit beyond the stream");
     HIPCHK(c, hipSetDevice(c->device));
     const int n = c->n;
-    // stream: a 4-byte aligned device stream is read in place (the kernels read whole aligned words
-    // up to the one holding the last byte -- never past its page -- and clear the bits past the
-    // stream themselves); anything else is staged (device copy or H2D) with zero padding
+    // stream: a 16-byte aligned device stream is read in place (the kernels read it with 16-byte
+    // vector loads of whole aligned words up to the one holding the last byte -- never past its
+    // page -- and clear the bits past the stream themselves); anything else is staged (device
+    // copy or H2D) with zero padding
     const uint8_t* words = in;
-    if (!is_device_ptr(in) || (reinterpret_cast<uintptr_t>(in) & 3u)) {
+    if (!is_device_ptr(in) || (reinterpret_cast<uintptr_t>(in) & 15u)) {
         const size_t padded = (len + 3) / 4 * 4 + 16;
         if ((r = ensure(c, c->d_dec, c->cap_dec, padded))) return r;
         HIPCHK(c, hipMemsetAsync(c->d_dec + (len / 4) * 4, 0, padded - (len / 4) * 4, c->stream));
@@ -2451,7 +2452,10 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
         // warm-up chunks: a speculative walk crosses this many whole chunks (about 32 (4x4) / 16
         // (8x8) records each) before the chunk whose exit it reports (IE_DEC_WARM)
         static const char* ew = getenv("IE_DEC_WARM");
-        pa.warm = ew ? std::max(0, std::min(8, atoi(ew))) : 0;
+        const int warm = c->spec_warm ? c->spec_warm : (ew ? std::max(0, std::min(8, atoi(ew))) : 0);
+        // rec_spec_kernel stages seg + warm chunks per wave in LDS: keep a wave within 12 KB
+        const int room = int((uint64_t(12 * 1024) * 8 - 256) / uint64_t(pa.C)) - pa.seg;
+        pa.warm = std::max(0, std::min(warm, room));
         ie::launch_rec_spec_decode(pa, da, n, c->stream);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipStreamSynchronize(c->stream));

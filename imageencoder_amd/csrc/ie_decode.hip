@@ -183,9 +183,9 @@ __global__ void huf_total_kernel(const uint64_t* base, const uint32_t* count, in
 // (T_{k+1} o T_k), and the true entry of every chunk follows from the stream's start by composing
 // tables: exact for any content, with no speculation to converge (periodic streams, which lock
 // speculative walks into a wrong phase, cost nothing extra).
-//   rec_table_kernel   one wave per chunk: the D walks share their work through claims in LDS --
-//                      the first walk to reach a position owns it, a later walk that lands there
-//                      stops and takes the owner's exit -- so about one walk per chunk survives.
+//   rec_table2_kernel  the D walks of a chunk share their work through claims in LDS -- the first
+//                      walk to reach a position owns it, a later walk that lands there stops and
+//                      takes the owner's exit -- so about one walk per chunk survives.
 //   rec_compose_kernel one workgroup per group of G tables: the group's tables in LDS, every entry
 //                      chased through them; the chase writes the group-relative prefix map P_j
 //                      over each table (group entry -> entry of table j) and the group's
@@ -331,192 +331,6 @@ __device__ __forceinline__ uint32_t decode_record(const uint32_t* L, uint32_t p,
         }
     }
     return p + uint32_t(length * bl);
-}
-
-// One wave tabulates M consecutive chunks.  All M*D walks run in one loop (entry e = lane,
-// lane + 64, ...; a lane starts its next walk as soon as one ends), interleaved over the chunks,
-// so the long walks of the M chunks run side by side in different lanes.  A walk steps between
-// valid record headers (a precomputed bitmap: an invalid header slides a walk to the next valid
-// one) and claims every position it visits -- the first walk to reach a position owns it; a walk
-// landing on an owned position stops and takes the owner's exit.  Claims live in a small
-// open-addressing hash table per chunk ((position << 16 | owner) words set by compare-and-swap):
-// a chunk's walks visit a few hundred positions, not all C.  Claims only save work -- a walk that
-// finds the table full just walks on -- so the tables are exact whatever the content.  Wrong-phase
-// walks step a few bits at a time and meet each other often, so a chunk keeps about one of them
-// alive besides its true path.
-template <int N>
-__global__ __launch_bounds__(64) void rec_table_kernel(RecParseArgs a) {
-    constexpr int D = RecGeom<N>::D, M = RecGeom<N>::M, E = M * D, HS = RecGeom<N>::HS;
-    constexpr int PER = (E + 63) / 64;
-    // dynamic LDS: the M chunks' bits (+ 64 for the last header) and their valid-header bitmap
-    extern __shared__ uint32_t L[];
-    __shared__ uint32_t H[M][HS];
-    __shared__ uint16_t res[E];
-    __shared__ uint16_t tgt[E];
-    const int lane = threadIdx.x, k0 = blockIdx.x * M;
-    const int m = min(M, a.nchunks - k0);           // chunks of this wave
-#if IE_PROFILE  // per-wave phase times (IE_DEC_STAMPS): realtime (100 MHz) and cycle counters
-    unsigned long long* ws = a.wstamp ? a.wstamp + size_t(blockIdx.x) * 8 : nullptr;
-    auto wstamp = [&](int i) {
-        if (ws && lane == 0) ws[i] = __builtin_amdgcn_s_memrealtime();
-    };
-    wstamp(0);
-#else
-    auto wstamp = [](int) {};
-#endif
-    const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
-    const uint64_t base = c0 & ~31ull;
-    const uint32_t s0 = uint32_t(c0 - base), C = a.C, CW = C >> 5;
-    const uint64_t lim64 = a.nbits - base;          // stream end relative to L: no record starts there or later
-    const uint32_t lim = uint32_t(min<uint64_t>(lim64, uint64_t(s0) + uint64_t(m) * C));
-    uint32_t* VB = L + rec_table_stream_words(uint32_t(M) * C);
-    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, lane, 64);
-    for (int i = lane; i < M * HS; i += 64) (&H[0][0])[i] = 0xFFFFFFFFu;
-    __syncthreads();
-    wstamp(1);
-    // 1. valid headers of every position (the 32 headers of a word from one 64-bit window)
-    for (uint32_t i = lane; i < uint32_t(m) * CW; i += 64) {
-        const uint32_t p0 = s0 + (i << 5);
-        uint32_t msk = 0;
-        if (p0 < lim) {
-            const uint32_t w0 = p0 >> 5, sb = p0 & 31u;
-            const uint64_t v = (((uint64_t(L[w0]) << 32) | L[w0 + 1]) << sb) |
-                               (sb ? (uint64_t(L[w0 + 2]) >> (32 - sb)) : 0ull);
-#pragma unroll
-            for (uint32_t q = 0; q < 32; q++)
-                msk |= (rec_len_head<N>(uint32_t((v << q) >> 44), a.rle) > 1u ? 1u : 0u) << q;
-            const uint32_t cut = lim - p0;  // no record starts at or past the stream's end
-            if (cut < 32u) msk &= (1u << cut) - 1u;
-        }
-        VB[i] = msk;
-    }
-    __syncthreads();
-    wstamp(2);
-    // 2. the walks
-    {
-        // entry e is offset e / M of chunk e % M: the first offsets of all M chunks -- where
-        // their surviving walks start -- run together in the first pass
-        uint32_t e = lane, p = 0, cs = 0, ce = 0, j = 0, id = 0;
-        uint32_t nsteps = 0, nwin = 0, nbey = 0;
-        bool fresh = true;
-        while (e < uint32_t(M * D)) {
-            nsteps++;
-            if (fresh) {
-                j = e % M;
-                const uint32_t d = e / M;
-                if (j >= uint32_t(m)) {  // no such chunk
-                    e += 64;
-                    continue;
-                }
-                id = j * D + d;  // index of the entry in res / tgt
-                cs = j * C;      // chunk-relative positions below are offsets from s0 + cs
-                ce = cs + C;
-                p = cs + d;
-                fresh = false;
-            }
-            bool done = false;
-            uint32_t t = kNoOwner;
-            if (p < ce) {
-                // next valid position of the chunk (or its end)
-                uint32_t wi = p >> 5, msk = VB[wi] & (0xFFFFFFFFu << (p & 31u));
-                const uint32_t wend = ce >> 5;
-                while (!msk && ++wi < wend) msk = VB[wi];
-                p = msk ? (wi << 5) + uint32_t(__builtin_ctz(msk)) : ce;
-            }
-            if (p >= ce) {
-                done = true;
-            } else {
-                const uint32_t head = lbits(L, s0 + p, 20);
-                const uint32_t key = (p - cs) << 16;  // chunk-relative position
-                uint32_t h = ((p - cs) * 2654435761u) >> (32 - RecGeom<N>::HSB);
-                for (int probe = 0; probe < HS; probe++) {
-                    const uint32_t o = atomicCAS(&H[j][h], 0xFFFFFFFFu, key | id);
-                    if (o == 0xFFFFFFFFu) break;                  // claimed
-                    if ((o & 0xFFFF0000u) == key) {               // owned: merge
-                        t = o & 0xFFFFu;
-                        done = true;
-                        break;
-                    }
-                    h = (h + 1) & uint32_t(HS - 1);               // another position: probe on
-                }
-                if (!done) p += rec_len_head<N>(head, a.rle);
-            }
-            if (done) {
-                if (t == kNoOwner) nwin++;
-                tgt[id] = uint16_t(t);
-                if (t == kNoOwner) res[id] = uint16_t(p - ce);
-                e += 64;
-                fresh = true;
-            }
-        }
-        (void)nsteps;
-        (void)nwin;
-        (void)nbey;
-#if IE_PROFILE
-        if (ws) {
-            const uint32_t mx = __reduce_max_sync(~0ull, nsteps);
-            const uint32_t sm = __reduce_add_sync(~0ull, nsteps);
-            if (lane == 0) {
-                ws[6] = (uint64_t(mx) << 32) | sm;
-                uint32_t hw;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-                ws[7] = hw;
-            }
-        }
-#endif
-#if IE_PROFILE  // walk statistics (IE_DEC_STATS in a profiling build)
-        if (a.stats) {
-            const uint32_t mx = __reduce_max_sync(~0ull, nsteps);
-            atomicAdd(&a.stats[0], uint64_t(nsteps));
-            atomicAdd(&a.stats[1], uint64_t(nbey));
-            atomicAdd(&a.stats[2], uint64_t(nwin));
-            if (lane == 0) { atomicAdd(&a.stats[3], uint64_t(mx)); atomicMax(&a.stats[4], uint64_t(mx)); }
-        }
-#endif
-    }
-    __syncthreads();
-    wstamp(3);
-    // 3. an entry takes its owner's exit once the owner is resolved; else it jumps to its owner's
-    //    owner (owner chains climb to strictly later positions, so they end; pointer jumping
-    //    halves them every round)
-    for (;;) {
-        uint32_t nr[PER], nt[PER];
-        bool pend = false;
-#pragma unroll
-        for (int i = 0; i < PER; i++) {
-            const int e = lane + 64 * i;
-            nr[i] = kNoOwner;
-            nt[i] = kNoOwner;
-            if (e < m * D) {  // (entries of chunks past the stream's last never ran)
-                const uint32_t o = tgt[e];
-                if (o != kNoOwner) {
-                    const uint32_t oo = tgt[o];
-                    if (oo == kNoOwner) {
-                        nr[i] = res[o];
-                    } else {
-                        nt[i] = oo;
-                        pend = true;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < PER; i++) {
-            const int e = lane + 64 * i;
-            if (nr[i] != kNoOwner) {
-                res[e] = uint16_t(nr[i]);
-                tgt[e] = uint16_t(kNoOwner);
-            } else if (nt[i] != kNoOwner) {
-                tgt[e] = uint16_t(nt[i]);
-            }
-        }
-        if (!__syncthreads_or(pend)) break;
-    }
-    wstamp(4);
-    uint16_t* T = a.tab + size_t(k0) * D;
-    for (int e = lane; e < m * D; e += 64) T[e] = res[e];
-    wstamp(5);
 }
 
 // One composition level over n tables ([n][D], 16-bit exits): prefix maps written over the
@@ -1024,7 +838,7 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
     const int off = stage_words16(L, a.words, base >> 5, int((uint32_t(c0 - base) + uint32_t(m) * a.C + D + 64) >> 5) + 2,
                                   a.nbits, lane);
     const uint32_t ob = 32u * uint32_t(off);
-    const uint32_t s0 = uint32_t(c0 - base) + ob, end = s0 + uint32_t(m) * a.C;
+    const uint32_t s0 = uint32_t(c0 - base) + ob;
     const uint64_t lbase0 = base - ob;  // stream bit of L's bit 0
     // first block index: the totals of the count pass's workgroups before chunk k0's, plus the
     // records before it in its own (no separate scan launch); the next chunks follow on
@@ -1088,7 +902,6 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
 
 int rec_group_chunks(int n) { return n == 4 ? RecGeom<4>::G : RecGeom<8>::G; }
 int rec_entry_span(int n) { return n == 4 ? RecGeom<4>::D : RecGeom<8>::D; }
-int rec_table_chunks(int n) { return n == 4 ? RecGeom<4>::M : RecGeom<8>::M; }
 // chunks per table wave and claim slots: tm chunks' positions fit the 16-bit claim keys.  The
 // claim table is small on purpose (lossy, direct-mapped): measured on 4K streams, the occupancy a
 // small LDS footprint buys beats the merges a larger table finds (IE_REC_TM / IE_REC_HB override)
@@ -1102,10 +915,6 @@ void rec_table_geometry(uint32_t C, int n, int* tm, int* hbits) {
     *tm = t;
     *hbits = std::min(14, std::max(6, hb));
 }
-size_t rec_table_lds(uint32_t C, int n) {
-    const int M = n == 4 ? RecGeom<4>::M : RecGeom<8>::M;
-    return size_t(rec_table_stream_words(uint32_t(M) * C) + M * (C >> 5)) * 4;
-}
 size_t rec_decode_lds(uint32_t C, int n) {
     return size_t(rec_decode_stream_words(uint32_t(kDecChunks) * C, rec_entry_span(n))) * 4 * kRecWPB;
 }
@@ -1114,17 +923,12 @@ int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t
     if (a.nchunks <= 0) return 0;
     const int nb = (a.nchunks + kRecWPB * kDecChunks - 1) / (kRecWPB * kDecChunks);  // decode blocks
     const int nt = (a.nchunks + RecGeom<4>::M - 1) / RecGeom<4>::M;  // table waves (M chunks each)
-#if IE_REC_V1
-    if (n == 4) hipLaunchKernelGGL((rec_table_kernel<4>), dim3(nt), dim3(64), rec_table_lds(a.C, 4), s, a);
-    else hipLaunchKernelGGL((rec_table_kernel<8>), dim3(nt), dim3(64), rec_table_lds(a.C, 8), s, a);
-#else
     (void)nt;
     rec_table_geometry(a.C, n, &a.tm, &a.hbits);
     const int nt2 = (a.nchunks + a.tm - 1) / a.tm;
     const size_t l2 = size_t(rec_table2_words(a.C, rec_entry_span(n), a.tm, a.hbits)) * 4;
     if (n == 4) hipLaunchKernelGGL((rec_table2_kernel<4>), dim3(nt2), dim3(64), l2, s, a);
     else hipLaunchKernelGGL((rec_table2_kernel<8>), dim3(nt2), dim3(64), l2, s, a);
-#endif
     const int levels = (n == 4) ? launch_compose<RecGeom<4>::D, RecGeom<4>::G>(a.tab, a.nchunks, a.E, a.ticket + 1, a.lvl, s)
                                 : launch_compose<RecGeom<8>::D, RecGeom<8>::G>(a.tab, a.nchunks, a.E, a.ticket + 1, a.lvl, s);
     if (levels < 0) return -1;

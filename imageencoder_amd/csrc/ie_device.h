@@ -219,8 +219,6 @@ struct RecParseArgs {
 void rec_table_geometry(uint32_t C, int n, int* tm, int* hbits);
 int rec_group_chunks(int n);
 int rec_entry_span(int n);
-int rec_table_chunks(int n);  // chunks per table wave
-size_t rec_table_lds(uint32_t C, int n);
 size_t rec_decode_lds(uint32_t C, int n);
 int rec_count_seg(uint32_t C);
 // Returns the number of composition levels (< 0: too many chunks).

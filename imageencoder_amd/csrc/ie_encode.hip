@@ -432,7 +432,7 @@ __device__ __forceinline__ uint32_t size_block(uint32_t (&zp)[N * N / 2], int rl
 #define IE_ASM_OR 1
 #endif
 __device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t v, uint32_t len) {
-    const uint32_t w = p >> 5, s = p & 31u;
+    const uint32_t s = p & 31u;
     const uint64_t x = uint64_t(v) << (64u - len - s);
 #if IE_ASM_OR
     // The image is the dynamic LDS area at LDS byte address 0 (the encode kernels allocate no static
@@ -443,8 +443,8 @@ __device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t
     asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a), "v"(uint32_t(x >> 32)), "v"(uint32_t(x))
                  : "memory");
 #else
-    atomicOr(&img[w], uint32_t(x >> 32));
-    atomicOr(&img[w + 1], uint32_t(x));
+    atomicOr(&img[p >> 5], uint32_t(x >> 32));
+    atomicOr(&img[(p >> 5) + 1], uint32_t(x));
 #endif
 }
 

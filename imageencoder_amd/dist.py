@@ -181,10 +181,21 @@ class PipelinedGather:
         self._base = header_bits
         # the counts' own communicator (collective: every rank constructs this object in step)
         self.cgroup = count_group if count_group is not None else group
+        self._own_cgroup = False
         if world > 1 and count_group is None:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
-            self.cgroup = dist.new_group(ranks=ranks)
+            # the counts travel on the transfers' backend: a gloo group under an NCCL default
+            # group keeps its counts (CPU tensors) on gloo
+            self.cgroup = dist.new_group(ranks=ranks, backend=dist.get_backend(group))
+            self._own_cgroup = True
         self.CC = torch.cuda.Stream(self.dev) if (cuda and comm_stream is not None) else None
+
+    def close(self) -> None:
+        """Destroy the count communicator this object created (collective, like the constructor)."""
+        if self._own_cgroup and self.cgroup is not None:
+            self.dist.destroy_process_group(self.cgroup)
+        self.cgroup = None
+        self._own_cgroup = False
 
     # -- stream helpers (no-ops on the CPU)
     def _on(self, s):

@@ -10,7 +10,10 @@
  *   dc::ImageDecoder::process      ImageDecoder.cpp:55-122  (parse + IDCT + clamp; ie_decode_*)
  *
  * A per-block C call would cross the host/device boundary 518 400 times per 4K frame, so the
- * boundary is frame-batch level; dc::Block<> keeps its API in the host library (include/ie_host.hpp).
+ * boundary is frame-batch level.  dc::Block<> has no counterpart here or in the host library
+ * (include/ie_host.hpp, which mirrors ImageProcessor / MatrixReader / the encoders and decoders):
+ * only the reference's own Block.o, linked into the drop-in builds of integration/, keeps that API
+ * ("Why there is no dc::Block<N>").
  *
  * Conventions
  *   - Every function returns IE_OK (0) or a negative IE_E* code; ie_last_error() describes it.
@@ -231,7 +234,9 @@ int ie_huffman_pack_batch(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const
 
 /* Device time of the last batched Huffman stage on the context's stream (HIP events around its
  * launches): stage 0 = the histogram / first-occurrence kernels of ie_huffman_hist_batch_ends_async,
- * stage 1 = the pack kernel of ie_huffman_pack_batch.  Waits for the stage to finish. */
+ * stage 1 = the pack kernel of ie_huffman_pack_batch.  Only those two batched calls record the
+ * events (two hipEventRecord each); the single-string ie_huffman_hist / ie_huffman_pack do not.
+ * Waits for the stage to finish. */
 int ie_last_stage_ms(ie_ctx* ctx, int stage, float* ms);
 
 /* Copy n bytes into out starting at bit start_bit, i.e. shifted by start_bit % 8 (the "no gain"
@@ -285,7 +290,9 @@ int ie_last_decode_info(ie_ctx* ctx, int* chunks, int* levels);
  * entry is where a walk from its predecessor's first bit left it, and the counting walks, each from
  * its predecessor's speculative exit, verify every exit; on any mismatch (periodic content, e.g.
  * gradients) nothing is written and the exact parse runs.  Faster only on flat content (DESIGN.md
- * §7).  ie_last_decode_spec returns 1 when the last record decode was completed by the speculative
+ * §7).  exact < 0: speculative with -exact (<= 8) warm-up chunks -- a chunk's walk starts that
+ * many chunks earlier (the count pass's LDS bounds it further for long chunks).
+ * ie_last_decode_spec returns 1 when the last record decode was completed by the speculative
  * parse, 0 when by the exact one. */
 int ie_set_exact_parse(ie_ctx* ctx, int exact);
 int ie_last_decode_spec(ie_ctx* ctx);

@@ -109,8 +109,10 @@ def test_numpy_shift(start):
     assert np.array_equal(bits[start:start + 37 * 8], np.unpackbits(src))
 
 
-def _pipe_worker(rank, world, port, w, h, F, nchunks, gen, steps, result_q):
-    """PipelinedGather on CPU/gloo: round-robin chunks, the oracle as each rank's encoder."""
+def _pipe_worker(rank, world, port, w, h, F, nchunks, gen, steps, result_q, subgroup=False):
+    """PipelinedGather on CPU/gloo: round-robin chunks, the oracle as each rank's encoder.
+    subgroup: the transfers run on an explicit gloo group (the count communicator PipelinedGather
+    creates takes that group's backend) and the object is closed and rebuilt once (no leak)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -139,20 +141,26 @@ def _pipe_worker(rank, world, port, w, h, F, nchunks, gen, steps, result_q):
             v = torch.from_numpy(D.numpy_shift(src.numpy(), nbytes, start))
             dst[: v.numel()].copy_(v)
 
-        g = D.PipelinedGather(dist, rank, world, F, nchunks, hdr, hb, seg_cap, cap, encode, shift, "cpu")
+        grp = dist.new_group(ranks=list(range(world)), backend="gloo") if subgroup else None
+        if subgroup:  # a throw-away gather: its count communicator is destroyed by close()
+            D.PipelinedGather(dist, rank, world, F, nchunks, hdr, hb, seg_cap, cap, encode, shift, "cpu",
+                              group=grp).close()
+        g = D.PipelinedGather(dist, rank, world, F, nchunks, hdr, hb, seg_cap, cap, encode, shift, "cpu", group=grp)
         outs = []
         for step in range(steps):
             g.step(step)
             if rank == 0:
                 outs.append((g.total, g.out[: (g.total + 7) // 8].numpy().tobytes()))
+        g.close()
         if rank == 0:
             result_q.put(outs)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,F,nchunks,gen", [(2, 8, 2, "U"), (3, 9, 3, "M"), (2, 5, 2, "M"), (3, 2, 1, "U")])
-def test_pipelined_gather_matches_reference(world, F, nchunks, gen):
+@pytest.mark.parametrize("world,F,nchunks,gen,subgroup",
+                         [(2, 8, 2, "U", False), (3, 9, 3, "M", False), (2, 5, 2, "M", True), (3, 2, 1, "U", False)])
+def test_pipelined_gather_matches_reference(world, F, nchunks, gen, subgroup):
     """Round-robin chunks assembled by PipelinedGather equal the single-process gop=1 stream of
     the same frames in global order, for two consecutive steps over different frames (the root
     buffer is reused: stale bytes must not leak into the next stream)."""
@@ -160,7 +168,7 @@ def test_pipelined_gather_matches_reference(world, F, nchunks, gen):
     ctx = mp.get_context("spawn")
     qres = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, w, h, F, nchunks, gen, steps, qres))
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, w, h, F, nchunks, gen, steps, qres, subgroup))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -537,11 +537,16 @@ def test_decode_device_stream_in_place(codec, n, k):
     pix_u = torch.zeros_like(pix_h)
     e_h = c.decode_frames(host, w, h, pix_h, length=length)
     e_d = c.decode_frames(dev, w, h, pix_d, length=length)
-    shifted = torch.full((length + 17,), 0xFF, dtype=torch.uint8, device="cuda")
-    shifted[1:length + 1] = dev[:length]
-    e_u = c.decode_frames(shifted[1:], w, h, pix_u, length=length)
-    assert e_h == e_d == e_u == end
-    assert torch.equal(pix_h, pix_d) and torch.equal(pix_h, pix_u)
+    assert e_h == e_d == end
+    assert torch.equal(pix_h, pix_d)
+    # device views at every offset of a 16-byte line: only 16-byte aligned ones are read in place
+    for off in (1, 4, 8, 12, 16):
+        shifted = torch.full((length + 33,), 0xFF, dtype=torch.uint8, device="cuda")
+        shifted[off:length + off] = dev[:length]
+        pix_u.zero_()
+        e_u = c.decode_frames(shifted[off:], w, h, pix_u, length=length)
+        assert e_u == end, off
+        assert torch.equal(pix_h, pix_u), off
 
 
 @pytest.mark.parametrize("n", [4, 8])
@@ -584,3 +589,29 @@ def test_decode_speculative_equals_exact(codec, n, kind):
     assert np.array_equal(pix_s.cpu().numpy(), np.asarray(ref).reshape(h, w))
     if kind == "flat":  # measured: the flat frames' speculative walks meet the true path
         assert used_spec
+
+
+@pytest.mark.parametrize("n", [4, 8])
+@pytest.mark.parametrize("warm", [1, 8])
+def test_decode_speculative_warm(codec, n, warm):
+    """Speculative parse with warm-up chunks (ie_set_exact_parse(ctx, -warm)): noise frames make
+    the longest chunks (8x8: C = 8192 bits), where warm = 8 would exceed the count pass's LDS
+    unless the host clamps it; the pixels equal the exact parse's either way."""
+    import torch
+
+    from imageencoder_amd import Codec, stream_bound
+    w, h = 1024, 256
+    y = synth.frame("U", w, h, seed=31 + n)
+    q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
+    c = Codec(0, q, n)
+    dev = torch.zeros(stream_bound(w, h, n, 1, 0) + 64, dtype=torch.uint8, device="cuda")
+    _, end = c.encode_frames(torch.from_numpy(y).cuda(), w, h, dev)
+    length = (end + 7) // 8
+    pix_s = torch.zeros((h, w), dtype=torch.uint8, device="cuda")
+    pix_e = torch.zeros_like(pix_s)
+    c.set_exact_parse(False, warm=warm)
+    e_s = c.decode_frames(dev, w, h, pix_s, length=length)
+    c.set_exact_parse(True)
+    e_e = c.decode_frames(dev, w, h, pix_e, length=length)
+    assert e_s == e_e == end
+    assert torch.equal(pix_s, pix_e)
