@@ -143,7 +143,7 @@ __device__ __forceinline__ int exact_coef_inl(const EncTables* __restrict__ tab,
     double acc = 0.0;
 #pragma unroll
     for (int ij = 0; ij < NN; ij++) {
-        const double x = double(int((px.w[ij >> 2] >> (8 * (ij & 3))) & 0xFFu)) + (-128.0);
+        const double x = double(int((px.w[ij >> 2] >> (8 * (ij & 3))) & 0xFFu) - 128);  // == double(p) + (-128.0), exactly
         acc = acc + P[ij] * x;
     }
     const double D = acc * tab->S[k];
@@ -163,7 +163,7 @@ __device__ __forceinline__ int exact_coef_row(const double* P, double S, double 
     double acc = 0.0;
 #pragma unroll IE_FIX_UNROLL
     for (int ij = 0; ij < NN; ij++) {
-        const double x = double(int((px.w[ij >> 2] >> (8 * (ij & 3))) & 0xFFu)) + (-128.0);
+        const double x = double(int((px.w[ij >> 2] >> (8 * (ij & 3))) & 0xFFu) - 128);  // == double(p) + (-128.0), exactly
         acc = acc + P[ij] * x;
     }
     const double D = acc * S;
@@ -188,7 +188,30 @@ __device__ __forceinline__ int exact_coef_task(const double* P, double S, double
         for (int e = 0; e < 4; e++) pr[e] = P[4 * w + e];
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-            const double x = double(int((px4 >> (8 * e)) & 0xFFu)) + (-128.0);
+            const double x = double(int((px4 >> (8 * e)) & 0xFFu) - 128);
+            acc = acc + pr[e] * x;
+        }
+    }
+    const double D = acc * S;
+    const double t = (rq != 0.0) ? D * rq : D / qd;
+    double r = trunc(t);
+    if (fabs(t - r) >= 0.5) r += copysign(1.0, t);
+    return int(r);
+}
+
+// exact_coef_task for a 4x4 block whose pixel rows are 256 words apart (encode4w_kernel's LDS
+// layout), one row per step of a loop left rolled: few registers live beside the caller's.
+__device__ __forceinline__ int exact_coef_rows4(const double* P, double S, double rq, double qd, const uint32_t* pw) {
+    double acc = 0.0;
+#pragma unroll 1
+    for (int w = 0; w < 4; w++) {
+        const uint32_t px4 = pw[w * 256];
+        double pr[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) pr[e] = P[4 * w + e];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const double x = double(int((px4 >> (8 * e)) & 0xFFu) - 128);  // == double(p) + (-128.0), exactly
             acc = acc + pr[e] * x;
         }
     }
@@ -1367,14 +1390,16 @@ __device__ __forceinline__ float round_block_lean4(const EncTables* __restrict__
 #ifndef IE_W_DBG
 #define IE_W_DBG 0
 #endif
+#ifndef IE_W_POOL
+#define IE_W_POOL 1  // one FP64 task list per tile (0: per wave)
+#endif
 #ifndef IE_W_AHEAD
 #define IE_W_AHEAD 2  // look-back windows per round trip (each holds 4 VGPRs live beside slots 2-3)
 #endif
 #ifndef IE_W_WAVES
-#define IE_W_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD): 80 VGPRs, no scratch
+#define IE_W_WAVES 7  // __launch_bounds__ occupancy hint (waves per SIMD): <= 72 VGPRs
 #endif
-constexpr int kWReg = 1024;  // words per wave region: [4 rows][256 blocks] pixels, then two slot images
-constexpr int kWBuf = 512;   // words per slot image
+constexpr int kWReg = 1024;  // words per wave region: [4 rows][256 blocks] pixels, then the two slot-pair images in turn
 constexpr int kWTask = 128;  // words per wave: fix-up tasks [64] + results [64]
 constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9] excl, [10] ptail, [11] tail pending, [12] ticket
 constexpr int kWRows = 16 * 16 + 3 * 16;  // FP64 rows P[16][16], then S, rq, qd (doubles)
@@ -1447,6 +1472,10 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     } else {
         t = int(blockIdx.x);
     }
+    if (tid == 0) {  // the tile's FP64 task counters (IE_W_POOL): structural, whole-block
+        misc[16] = 0u;
+        misc[17] = 0u;
+    }
     // every coefficient's FP64 row and its S, rq, qd: the fix-up reads them from LDS
     for (int i = tid; i < kWRows; i += TPB)
         srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
@@ -1500,14 +1529,121 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         asm volatile("" : "+v"(flags));
     }
 
-    // ------------------------------------------------------------ FP64 fix-up (compacted per wave)
+    // ------------------------------------------------------------ FP64 fix-up
+    if constexpr (IE_W_POOL) {
+        // One task list for the whole tile (IE_W_POOL): every flagged coefficient -- structural s
+        // of slot b, or all 16 of a whole-block request -- takes a slot from an LDS counter, and
+        // the tile's waves evaluate 64 tasks per wave-round: about two FP64 rounds per tile
+        // instead of one or two per wave.  Task word: wave << 12 | lane << 6 | slot << 4 | k; the
+        // evaluating lane overwrites it with the result.  Passes of kWPoolCap tasks (the per-wave
+        // task areas, pooled) keep any count bounded.
+        constexpr uint32_t kWPoolCap = 4 * kWTask;
+        uint32_t* const pool = smem + 4 * kWReg;
+        // structural tasks first (one counter), then whole-block requests in groups of 16 from a
+        // 16-aligned start (another counter), so that no group straddles a window
+        const uint32_t sfl = flags & 0x7777u, wfl = flags & 0x8888u;
+        const uint32_t ns = uint32_t(__popc(sfl)), nwb = uint32_t(__popc(wfl));
+        uint32_t sbase = 0, wbase = 0;
+        if (ns) sbase = atomicAdd(&misc[16], ns);  // (LDS atomics with return)
+        if (nwb) wbase = atomicAdd(&misc[17], nwb);
+        lds_barrier();
+        const uint32_t nstruct = __builtin_amdgcn_readfirstlane(misc[16]);
+        const uint32_t wb0 = (nstruct + 15u) & ~15u;
+        const uint32_t total = wb0 + 16u * __builtin_amdgcn_readfirstlane(misc[17]);
+        for (uint32_t w0 = 0; w0 < total; w0 += kWPoolCap) {  // (uniform)
+            // this lane's tasks in the window [w0, w0 + cap): same order as the patch below
+            // (unsigned offsets: a task before the window wraps to a huge i, and counting on wraps
+            // it back to the right place in a later window)
+            if (flags) {
+                uint32_t i = sbase - w0, j = wb0 + 16u * wbase - w0;
+                uint32_t own = (uint32_t(wv) << 12) | (uint32_t(lane) << 6);
+                asm volatile("" : "+v"(own));  // (opaque per window: keeps the task words from being hoisted)
+#pragma unroll
+                for (int b = 0; b < NS; b++) {
+                    const uint32_t tb = own | (uint32_t(b) << 4);
+#pragma unroll
+                    for (int ss = 0; ss < 3; ss++)
+                        if ((sfl >> (4 * b + ss)) & 1u) {
+                            if (i < kWPoolCap) pool[i] = tb | uint32_t(Structural<N>::k[ss]);
+                            i++;
+                        }
+                    if ((wfl >> (4 * b + 3)) & 1u) {
+                        if (j < kWPoolCap)
+                            for (uint32_t k = 0; k < 16u; k++) pool[j + k] = tb | k | 0x4000u;
+                        j += 16u;
+                    }
+                }
+            }
+            lds_barrier();  // tasks written; every wave's pixels are in LDS (each waited for its DMA)
+            const uint32_t nwin = min(kWPoolCap, total - w0);
+            for (uint32_t r = uint32_t(wv) * 64u; r < nwin; r += 256u) {  // (uniform per wave)
+                if (r + uint32_t(lane) < nwin) {
+                    const uint32_t tk = pool[r + lane];
+                    const int k = int(tk & 15u), b = int((tk >> 4) & 3u), ol = int((tk >> 6) & 63u);
+                    const int ow = int((tk >> 12) & 3u);
+                    const uint32_t* opx = smem + ow * kWReg + 64 * b + ol;  // the owner's pixel rows, 256 words apart
+                    const uint32_t v = (IE_W_DBG & 128) ? (opx[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
+                                     : uint32_t(exact_coef_rows4(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                                 srow[NN * NN + 2 * NN + k], opx)) & 0xFFFFu;
+                    if (tk & 0x4000u) {
+                        // whole-block group (16-aligned, inside this wave's round, every task word
+                        // read above): the result as int16 at its zig-zag place of the group's
+                        // first 32 bytes -- the owner reads its block back as 8 packed words
+                        constexpr uint64_t kPos = 0xFEA9DB83C7426510ull;  // ZigZagInv<4>::pos, a nibble each
+                        const uint32_t zpos = uint32_t(kPos >> (4 * k)) & 15u;
+                        reinterpret_cast<uint16_t*>(pool + ((r + lane) & ~15u))[zpos] = uint16_t(v);
+                    } else {
+                        pool[r + lane] = v;
+                    }
+                }
+            }
+            lds_barrier();  // results in place
+            if (sfl) {
+                uint32_t i = sbase - w0;
+#pragma unroll
+                for (int b = 0; b < NS; b++) {
+#pragma unroll
+                    for (int ss = 0; ss < 3; ss++)
+                        if ((sfl >> (4 * b + ss)) & 1u) {
+                            const int zw = Structural<N>::zpos(ss) >> 1;  // (high halves, see below)
+                            if (i < kWPoolCap) zp[b][zw] = __builtin_amdgcn_perm(pool[i], zp[b][zw], 0x05040100u);
+                            i++;
+                        }
+                }
+            }
+            if (__ballot(wfl != 0)) {
+                // whole blocks: the 8 packed words the evaluators assembled, taken by selects (a
+                // conditional overwrite of the packed registers costs spills at this occupancy)
+                uint32_t j = wb0 + 16u * wbase - w0;
+#pragma unroll
+                for (int b = 0; b < NS; b++) {
+                    const bool hit = ((wfl >> (4 * b + 3)) & 1u) && j < kWPoolCap;
+                    const uint32_t* src = pool + (hit ? j : 0u);
+                    const u32x4 v0 = *reinterpret_cast<const u32x4*>(src);
+                    const u32x4 v1 = *reinterpret_cast<const u32x4*>(src + 4);
+                    zp[b][0] = hit ? v0.x : zp[b][0];
+                    zp[b][1] = hit ? v0.y : zp[b][1];
+                    zp[b][2] = hit ? v0.z : zp[b][2];
+                    zp[b][3] = hit ? v0.w : zp[b][3];
+                    zp[b][4] = hit ? v1.x : zp[b][4];
+                    zp[b][5] = hit ? v1.y : zp[b][5];
+                    zp[b][6] = hit ? v1.z : zp[b][6];
+                    zp[b][7] = hit ? v1.w : zp[b][7];
+                    j += ((wfl >> (4 * b + 3)) & 1u) ? 16u : 0u;
+                }
+            }
+            if (w0 + kWPoolCap < total) lds_barrier();  // the next window rewrites the list
+        }
+    }
+    static_assert(Structural<4>::zpos(0) & Structural<4>::zpos(1) & Structural<4>::zpos(2) & 1,
+                  "4x4 structural coefficients sit in high halves of the packed words");
     auto block_px = [&](int b, int owner) {
         BlockPx<N> px;
 #pragma unroll
         for (int r = 0; r < N; r++) px.w[r] = reg[r * 256 + 64 * b + owner];
         return px;
     };
-    if (!(IE_W_DBG & 1) && __ballot(flags != 0)) {
+    if (!IE_W_POOL && !(IE_W_DBG & 1) && __ballot(flags != 0)) {
         const uint32_t sf = flags & 0x7777u;
         const uint32_t cnt = __popc(sf);
         uint32_t pre = 0, total = 0;
@@ -1531,30 +1667,27 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                 const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
                 const BlockPx<N> px = block_px(b, owner);
                 const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
-                res[lane] = uint32_t(exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                       srow[NN * NN + 2 * NN + k], px)) & 0xFFFFu;
+                res[lane] = (IE_W_DBG & 128) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
+                                             : uint32_t(exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                                          srow[NN * NN + 2 * NN + k], px)) & 0xFFFFu;
             }
             wave_sync();
-            m = sf;
+            // the owners take their results back: the flagged positions in bit order, each a
+            // constant register (the three structural coefficients are high halves of packed
+            // words), so no per-request select over every slot and coefficient
             i = pre - r0;
-            while (m) {
-                const int bit = __ffs(m) - 1;
-                m &= m - 1;
-                if (i < 64u) {
-                    const uint32_t v = res[i];
-                    const int b = bit >> 2, s = bit & 3;
 #pragma unroll
-                    for (int bb = 0; bb < NS; bb++)
+            for (int b = 0; b < NS; b++)
 #pragma unroll
-                        for (int ss = 0; ss < 3; ss++) {
-                            const int zpos = Structural<N>::zpos(ss);
-                            if (b == bb && s == ss)
-                                zp[bb][zpos >> 1] = (zpos & 1) ? ((zp[bb][zpos >> 1] & 0xFFFFu) | (v << 16))
-                                                               : ((zp[bb][zpos >> 1] & 0xFFFF0000u) | v);
-                        }
+                for (int ss = 0; ss < 3; ss++) {
+                    if ((sf >> (4 * b + ss)) & 1u) {
+                        const int zw = Structural<N>::zpos(ss) >> 1;
+                        static_assert(Structural<4>::zpos(0) & Structural<4>::zpos(1) & Structural<4>::zpos(2) & 1,
+                                      "4x4 structural coefficients sit in high halves");
+                        if (i < 64u) zp[b][zw] = __builtin_amdgcn_perm(res[i], zp[b][zw], 0x05040100u);  // res low -> high half
+                        i++;
+                    }
                 }
-                i++;
-            }
             wave_sync();
         }
         // whole-block requests (rare): all 16 coefficients in FP64, one per lane, four blocks a round
@@ -1605,8 +1738,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
             }
         }
     }
-    {
-        const unsigned wsum = unsigned(wave_sum64(__popc(flags)));
+    {  // statistics: FP64 requests of this wave (one store)
+        const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan_dpp(uint32_t(__popc(flags))), 63);
         if (lane == 0) a.wave_fix[size_t(t) * (TPB / 64) + wv] = wsum;
     }
 
@@ -1661,23 +1794,23 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     Probe pr{0, 0, 0};
     if (wv == 0 && chain_pos != 0) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);  // in flight while emitting
 
-    // slot images: buffer 0 = reg[0 .. kWBuf), buffer 1 = reg[kWBuf .. 2 kWBuf); emission takes
+    // slot-pair images: slots 0 and 1, then slots 2 and 3, each pair as ONE bit image from word 0
+    // of the wave's region (a pair holds <= 2 * 64 * 252 bits = 1008 words); emission takes
     // absolute LDS bit addresses (scatter_bits' ds_or addresses LDS from byte 0)
-    const uint32_t buf_bit0 = uint32_t(wv * kWReg) * 32u;
-    auto zero_buf = [&](int x, uint32_t bits) {
-        uint32_t* B = reg + x * kWBuf;
+    const uint32_t reg_bit0 = uint32_t(wv * kWReg) * 32u;
+    const uint32_t Sb[NS] = {0u, S1, S2, S3};
+    auto zero_img = [&](uint32_t bits) {
         const uint32_t nq = (bits + 127u) >> 7;  // 16-byte groups
-        for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(B + 4 * q) = u32x4{0u, 0u, 0u, 0u};
+        for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(reg + 4 * q) = u32x4{0u, 0u, 0u, 0u};
     };
-    auto emit_slot = [&](int b) {
+    auto emit_slot = [&](int b) {  // slot b at its place in its pair's image
         if (!(IE_W_DBG & 8) && rb[b]) {
-            const uint32_t p = buf_bit0 + uint32_t(b & 1) * (kWBuf * 32u) + off[b];
+            const uint32_t p = reg_bit0 + (Sb[b] - Sb[b & 2]) + off[b];
             if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
             else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
         }
     };
-    zero_buf(0, T[0]);
-    zero_buf(1, T[1]);
+    zero_img(S2);
     wave_sync();
     emit_slot(0);
     emit_slot(1);
@@ -1726,35 +1859,25 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         // the wave's first word is written by the previous wave (or, pending, later by this one)
         const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
         uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[10]) : 0u;
-        // slot b is stored from buffer b & 1 as soon as it is complete; slot b + 2 is then emitted
-        // into the same buffer (one wave's LDS operations complete in order)
-        auto store_b = [&](int b, uint32_t Sb) {
-            if (!T[b]) return;
-            const uint64_t Xb = Xw + Sb;
-            const uint32_t nw = uint32_t(((Xb + T[b]) >> 5) - (Xb >> 5));
-            const uint32_t* I = reg + (b & 1) * kWBuf;
-            store_slot(out, I, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
-            prev = slot_tail32(I, T[b], prev);
+        // pair 0 is stored as soon as the tile's position is known; the region then takes pair 1
+        // (one wave's LDS operations complete in order)
+        auto store_pair = [&](uint32_t S0, uint32_t n) {
+            if (!n) return;
+            const uint64_t Xb = Xw + S0;
+            const uint32_t nw = uint32_t(((Xb + n) >> 5) - (Xb >> 5));
+            store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
+            prev = slot_tail32(reg, n, prev);
         };
-        auto refill = [&](int b) {
-            if (!T[b]) return;
+        store_pair(0u, S2);
+        if (Tw > S2) {
+            wave_sync();  // pair 0's image has been read
+            zero_img(Tw - S2);
             wave_sync();
-            zero_buf(b & 1, T[b]);
+            emit_slot(2);
+            emit_slot(3);
             wave_sync();
-            emit_slot(b);
-            wave_sync();
-        };
-        store_b(0, 0u);
-        __builtin_amdgcn_sched_barrier(0);
-        refill(2);
-        __builtin_amdgcn_sched_barrier(0);
-        store_b(1, S1);
-        __builtin_amdgcn_sched_barrier(0);
-        refill(3);
-        __builtin_amdgcn_sched_barrier(0);
-        store_b(2, S2);
-        __builtin_amdgcn_sched_barrier(0);
-        store_b(3, S3);
+            store_pair(S2, Tw - S2);
+        }
         const uint64_t E = Xw + Tw;
         const uint32_t e = uint32_t(E) & 31u;
         if (lane == 0) {
