@@ -47,6 +47,10 @@ sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")  # data files (matrices, manifest of md5s)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ROUND = "r04"  # profiles/<ROUND>_traffic_<workload>.json: this round's counter passes (tools/gpu_traffic.sh)
+# the dominant kernel of each workload's timed launch (launch_encode: 4x4 FAST over whole 16-byte
+# groups runs encode4w_kernel; 8x8 runs encode_kernel<8>)
+KERNEL = {"c2": "encode4w_kernel", "c3": "encode_kernel<8,false>", "c4": "encode4w_kernel", "c5": "encode4w_kernel"}
 
 WORKLOADS = {
     "c2": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=False,
@@ -353,6 +357,16 @@ def main():
                 nout += sum(int(x) for x in hs)
             t_h, t_p = float(np.median(th)) / 1e3, float(np.median(tp)) / 1e3
             hbytes = (nin + nout) / 5
+            # the counting encoder the step really runs (encode_kernel<4,HIST>: it also counts the
+            # bytes it stores), timed alone on the same stream
+            def enc_counted(i):
+                slot = i % nslots
+                codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, outs[i % len(outs)], out_pitch=pitch,
+                                    nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False, count_bytes=True)
+            _, g3 = timer.run(enc_counted, 1, args.steps)
+            t_cnt = g3 / args.steps
+            extra["counted_encode"] = {"kernel": "encode_kernel<4,false,HIST>", "launch_us": round(t_cnt * 1e6, 2),
+                                       "frac": round((B * w * h + out_bytes_per_launch) / t_cnt / 1e9 / HBM_PEAK_GBS, 4)}
             extra["huffman_roofline"] = {
                 "bound": "hbm", "achieved": round(hbytes / (t_h + t_p) / 1e9, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(hbytes / (t_h + t_p) / 1e9 / HBM_PEAK_GBS, 4),
@@ -360,6 +374,31 @@ def main():
                 "hist_us": round(t_h * 1e6, 2), "pack_us": round(t_p * 1e6, 2),
                 "note": "payload bytes read by the pack + Huffman bytes written, per 16-image batch; the byte "
                         "counts are taken by the encoder as it stores (its launch is the line's roofline)"}
+            # the inverse of the Huffman pass: image 0's Huffman stream decoded back
+            # to payload bytes, device-resident (ie_huffman_decode: table walk + composition + count +
+            # emit kernels), wall time per call incl. its host syncs
+            hs0 = codec.huffman_encode_after_encode(outs[0], pitch, B, houts, hpitch)
+            henc = houts[: hs0[0]].cpu().numpy().tobytes()
+            tab = codec.huffman_table(henc)
+            if tab is not None:
+                lut, hsb = tab
+                dlut = torch.from_numpy(lut.view(np.int16).copy()).to(dev)
+                denc = houts[: hs0[0]]
+                dsym = torch.zeros(8 * len(henc) + 64, dtype=torch.uint8, device=dev)
+                nsym = codec.huffman_decode_device(denc, len(henc), dlut, hsb, dsym)
+                torch.cuda.synchronize(dev)
+                kh = 10
+                t0 = time.perf_counter()
+                for _ in range(kh):
+                    codec.huffman_decode_device(denc, len(henc), dlut, hsb, dsym)
+                torch.cuda.synchronize(dev)
+                thd = (time.perf_counter() - t0) / kh
+                hb_dec = len(henc) + nsym
+                extra["huffman_decode"] = {"us": round(thd * 1e6, 1), "symbols": nsym, "stream_bytes": len(henc),
+                                           "achieved_GBps": round(hb_dec / thd / 1e9, 1),
+                                           "frac": round(hb_dec / thd / 1e9 / HBM_PEAK_GBS, 4),
+                                           "note": "Huffman stream read + symbols written per call, wall time incl. "
+                                                   "the host syncs (symbol count, then the decode)"}
         if args.single_frame:  # one 4K frame per launch: the latency of the single-image configuration
             one = outs[0][:pitch]
 
@@ -434,7 +473,10 @@ def main():
             torch.cuda.synchronize(dev)
             td = (time.perf_counter() - t0) / kd
             chunks, groups = codec.last_decode_info()
+            dec_bytes = nb0 + w * h  # the stream read + the pixels written
             extra["decode_one_image"] = {"us": round(td * 1e6, 1), "Mpx_s": round(w * h / td / 1e6, 1),
+                                         "achieved_GBps": round(dec_bytes / td / 1e9, 1),
+                                         "frac": round(dec_bytes / td / 1e9 / HBM_PEAK_GBS, 4),
                                          "path": f"exact parse: {chunks} chunk transfer tables composed in "
                                                  f"{groups} level(s), then count and decode launches; "
                                                  "one host sync at the end (device-resident stream and pixels)"}
@@ -573,7 +615,7 @@ def main():
 
     if rank == 0:
         traffic = None
-        tf = os.path.join(ROOT, "profiles", f"traffic_{wl}.json")
+        tf = os.path.join(ROOT, "profiles", f"{ROUND}_traffic_{wl}.json")  # this round's passes only
         if os.path.exists(tf):
             traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
         line = {
@@ -598,7 +640,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "encode_kernel",
+                "traffic_file": os.path.relpath(tf, ROOT) if traffic is not None else None,
+                "kernel": KERNEL[wl],
                 "alg_bytes_per_launch": int(alg_bytes),
                 "launch_us": round(enc_s * 1e6, 2),
                 "read_only_frac": round(in_bytes_per_launch / enc_s / 1e9 / HBM_PEAK_GBS, 4),

@@ -53,6 +53,9 @@ template <> struct ZigZagInv<8> {
 #ifndef IE_PROFILE
 #define IE_PROFILE 0
 #endif
+#ifndef IE_K8_PROF
+#define IE_K8_PROF 0  // 1: encode_kernel<8> reads the profiling fields in every build (round 3's spill workaround)
+#endif
 #ifndef IE_BPT4
 #define IE_BPT4 4
 #endif
@@ -222,6 +225,30 @@ __device__ __forceinline__ int exact_coef_rows4(const double* P, double S, doubl
     return int(r);
 }
 
+// exact_coef_task for an 8x8 block in encode_kernel<8>'s LDS pixel layout (row r = words
+// r*128, r*128 + 1 from pw): the pixel words come from LDS one at a time (a register copy of the
+// block indexed by the loop counter would live in scratch memory).
+__device__ __forceinline__ int exact_coef_rows8(const double* P, double S, double rq, double qd, const uint32_t* pw) {
+    double acc = 0.0;
+#pragma unroll 2
+    for (int w = 0; w < 16; w++) {
+        const uint32_t px4 = pw[(w >> 1) * 128 + (w & 1)];
+        double pr[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) pr[e] = P[4 * w + e];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const double x = double(int((px4 >> (8 * e)) & 0xFFu) - 128);  // == double(p) + (-128.0), exactly
+            acc = acc + pr[e] * x;
+        }
+    }
+    const double D = acc * S;
+    const double t = (rq != 0.0) ? D * rq : D / qd;
+    double r = trunc(t);
+    if (fabs(t - r) >= 0.5) r += copysign(1.0, t);
+    return int(r);
+}
+
 // Out-of-line copy for the EXACT mode's per-coefficient loop.
 template <int N>
 __device__ __noinline__ int exact_coef(const EncTables* __restrict__ tab, int k, BlockPx<N> px) {
@@ -342,6 +369,34 @@ __device__ __forceinline__ uint64_t round_block_mask(const EncTables* __restrict
 #pragma unroll
     for (int j = 0; j < NN / 2; j++)
         zp[j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
+    return near;
+}
+
+// round_block_mask for 8x8 with each zig-zag pair rounded and packed (and pinned) in turn: never
+// 64 magic-added quotients live beside the 64 quotients.  Same results bit for bit.
+__device__ __forceinline__ uint64_t round_block_mask_lean8(const EncTables* __restrict__ tab, const float (&t)[64],
+                                                         uint32_t (&zp)[32]) {
+    uint64_t near = 0;
+    const bool dcx = tab->dc_exact != 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+        uint32_t yb[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int k = ZigZag<8>::idx[2 * j + h];
+            const float y = t[k] + kMagic;
+            const float e = fabsf(t[k] - (y - kMagic));
+            yb[h] = __float_as_uint(y);
+            if (k == 0) {
+                yb[h] = dcx ? uint32_t(int(truncf(t[0] + copysignf(0.5f, t[0])))) : yb[h];
+                near |= (!dcx && e >= tab->lim[0]) ? 1ull : 0ull;
+            } else {
+                near |= uint64_t(e >= tab->lim[k]) << k;
+            }
+        }
+        zp[j] = __builtin_amdgcn_perm(yb[1], yb[0], 0x05040100u);
+        asm volatile("" : "+v"(zp[j]));
+    }
     return near;
 }
 
@@ -713,10 +768,10 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
 
     const int tid = threadIdx.x;
     // Profiling hooks (IE_ABLATE / IE_STAMPS) exist only in IE_PROFILE builds (tools/variants.sh):
-    // in the product build they are constants, so they hold no scalar registers.
-    // (The 8x8 kernel reads the two fields in every build: its register allocation spills 252 B
-    // without them live.  Only IE_PROFILE hosts set them; the product host passes 0 / nullptr.)
-    constexpr bool kProf = IE_PROFILE || N == 8;
+    // in the product build they are constants, so they hold no scalar registers.  (Round 3 kept them
+    // live in the 8x8 kernel to dodge a spill; with its pixels in LDS and the fix-up reading them
+    // from there the 8x8 kernel has no scratch without that: IE_K8_PROF=1 restores it for A/B.)
+    constexpr bool kProf = IE_PROFILE || (N == 8 && IE_K8_PROF);
     const int ablate = kProf ? a.ablate : 0;
     uint64_t* const stamps = kProf ? a.stamps : nullptr;
     // Tile order = dispatch order.  Workgroups are dispatched in increasing blockIdx, so every
@@ -753,12 +808,41 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
     constexpr bool kLdsPix = IE_LDS_PIX && N == 4 && !EXACT;
+    // 8x8 FAST: the pixels in LDS too, [8 rows][64 lanes][2 words] per wave (block row r of lane l
+    // = words r*128 + 2l, 2l+1): no pixel registers live through the transform and the fix-up
+    constexpr bool kLdsPix8 = IE_LDS_PIX && N == 8 && !EXACT;
     // kLdsPix: this wave's [4 rows][64 lanes][BPT] words; block b of a lane = word b of each row
-    constexpr int kRowW = 64 * BPT;
+    constexpr int kRowW = (N == 8) ? 128 : 64 * BPT;
     uint32_t* const pwave = img + kFixPix + (tid >> 6) * (N * kRowW);
     const int lane = tid & 63;
     uint32_t seg[N][WPR];
-    if constexpr (kLdsPix) {
+    if constexpr (kLdsPix8) {
+        // DMA when the wave's blocks pair up within rows (even bx): lanes 0-31 fetch row r, lanes
+        // 32-63 row r+1, 16 bytes = the row pieces of blocks 2c, 2c+1 (c = lane & 31) each
+        const int wfirst = tif * TPB + (tid & ~63);                          // the wave's first block
+        const int nwb = min(64, max(0, a.groups_per_frame - wfirst));        // its blocks in this frame
+        if (a.vec_ok && !(a.bx & 1) && nwb > 0) {
+            const int c = lane & 31, half = lane >> 5;
+            const int bi = wfirst + 2 * c;                                    // block of this lane's piece
+            const bool live = 2 * c < nwb;
+            const int by_ = bi / a.bx, bx_ = bi - by_ * a.bx;
+            const uint8_t* src = a.y + size_t(frame) * a.frame_pitch + size_t(by_) * N * a.stride + size_t(bx_) * N;
+#pragma unroll
+            for (int r = 0; r < N; r += 2)
+                if (live)
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + size_t(r + half) * a.stride),
+                                                     (__attribute__((address_space(3))) void*)(pwave + r * kRowW), 16, 0, 0);
+        } else {  // odd bx / unaligned rows: through registers
+            load_tile<N, WPR, BPT>(a, g, seg);
+#pragma unroll
+            for (int r = 0; r < N; r++) {
+                u32x2 v;
+                v.x = seg[r][0];
+                v.y = seg[r][1];
+                *reinterpret_cast<u32x2*>(pwave + r * kRowW + 2 * lane) = v;
+            }
+        }
+    } else if constexpr (kLdsPix) {
         static_assert((BPT == 4 || BPT == 1) && WPR == BPT && TPB % 64 == 0, "LDS pixel layout: 4 * BPT bytes per lane per row");
         if (IE_PROFILE && (ablate & 4096)) {
             // profiling: no pixel loads at all (the LDS holds whatever the previous tile left)
@@ -795,7 +879,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         load_tile<N, WPR, BPT>(a, g, seg);
     }
     if constexpr (!EXACT) lds_barrier();  // srow visible (the pixel loads stay in flight)
-    if constexpr (kLdsPix) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
+    if constexpr (kLdsPix || kLdsPix8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
 
     asm volatile("; PHASE load_done" ::: "memory");
     if (IE_PROFILE && (ablate & 512)) return;  // profiling: instruction count of the prologue + load alone
@@ -833,7 +917,16 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                 zp[b][j] = __builtin_amdgcn_perm(yb[ZigZag<N>::idx[2 * j + 1]], yb[ZigZag<N>::idx[2 * j]], 0x05040100u);
         } else {
             float x[NN];
-            if constexpr (kLdsPix) {
+            if constexpr (kLdsPix8) {
+                uint32_t rows[N][2];
+#pragma unroll
+                for (int r = 0; r < N; r++) {
+                    const u32x2 v = *reinterpret_cast<const u32x2*>(pwave + r * kRowW + 2 * lane);
+                    rows[r][0] = v.x;
+                    rows[r][1] = v.y;
+                }
+                block_pixels<N, 2>(rows, 0, x);
+            } else if constexpr (kLdsPix) {
                 uint32_t rows[N][1];
 #if IE_PIX64
                 // two blocks' rows per 8-byte read (2-way instead of 4-way bank conflicts)
@@ -862,6 +955,8 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                 static_assert(BPT == 1, "8x8: one block per lane");
                 near8 = round_block_mask<N>(tab, x, zp[b]);
                 if (b >= nblk || (ablate & 1)) near8 = 0;
+#pragma unroll
+                for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));  // packed here, not at first use
                 continue;
             }
             uint32_t sf;
@@ -896,12 +991,14 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         // and the owners patch their results in.
         const unsigned nfix = unsigned(__popcll(near8));
         if (__ballot(near8 != 0)) {
-            uint32_t* pxl = img;  // [TPB] x kFix8Stride words
+            uint32_t* pxl = img;  // (!kLdsPix8) [TPB] x kFix8Stride words
+            if constexpr (!kLdsPix8) {
 #pragma unroll
-            for (int q4 = 0; q4 < 4; q4++) {
-                u32x4 v;
-                v.x = seg[2 * q4][0]; v.y = seg[2 * q4][1]; v.z = seg[2 * q4 + 1][0]; v.w = seg[2 * q4 + 1][1];
-                *reinterpret_cast<u32x4*>(pxl + kFix8Stride * tid + 4 * q4) = v;
+                for (int q4 = 0; q4 < 4; q4++) {
+                    u32x4 v;
+                    v.x = seg[2 * q4][0]; v.y = seg[2 * q4][1]; v.z = seg[2 * q4 + 1][0]; v.w = seg[2 * q4 + 1][1];
+                    *reinterpret_cast<u32x4*>(pxl + kFix8Stride * tid + 4 * q4) = v;
+                }
             }
             const uint32_t cnt = nfix;
             uint32_t pre = 0, total = 0;
@@ -945,17 +1042,21 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                     }
                     wave_sync();
                     if (!done && (s >= 0 || slot >= 0)) {
-                        BlockPx<N> px;
-#pragma unroll
-                        for (int q4 = 0; q4 < 4; q4++) {
-                            const u32x4 w4 = *reinterpret_cast<const u32x4*>(pxl + kFix8Stride * owner + 4 * q4);
-                            px.w[4 * q4] = w4.x; px.w[4 * q4 + 1] = w4.y; px.w[4 * q4 + 2] = w4.z; px.w[4 * q4 + 3] = w4.w;
-                        }
                         const double* P = (s >= 0) ? srow + s * NN : stage + slot * NN;
                         const double S = (s >= 0) ? srow[3 * NN + s] : tab->S[k];
                         const double rq = (s >= 0) ? srow[3 * NN + 3 + s] : tab->rq[k];
                         const double qd = (s >= 0) ? srow[3 * NN + 6 + s] : tab->qd[k];
-                        res[lane] = uint32_t(exact_coef_row<N>(P, S, rq, qd, px)) & 0xFFFFu;
+                        if constexpr (kLdsPix8) {
+                            res[lane] = uint32_t(exact_coef_rows8(P, S, rq, qd, pwave + 2 * (owner & 63))) & 0xFFFFu;
+                        } else {
+                            BlockPx<N> px;
+#pragma unroll
+                            for (int q4 = 0; q4 < 4; q4++) {
+                                const u32x4 w4 = *reinterpret_cast<const u32x4*>(pxl + kFix8Stride * owner + 4 * q4);
+                                px.w[4 * q4] = w4.x; px.w[4 * q4 + 1] = w4.y; px.w[4 * q4 + 2] = w4.z; px.w[4 * q4 + 3] = w4.w;
+                            }
+                            res[lane] = uint32_t(exact_coef_row<N>(P, S, rq, qd, px)) & 0xFFFFu;
+                        }
                         done = true;
                     }
                     wave_sync();  // the next pass rewrites the staged rows

@@ -96,7 +96,8 @@ def static_lds(path):
 # (an unguarded profiling branch once took the 8x8 kernel from 68 to 308 B of scratch, 2x slower).
 BUDGETS = {
     "_ZN2ie13encode_kernelILi4ELb0ELb0ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": (5, 0),
-    "_ZN2ie13encode_kernelILi8ELb0ELb0ELi1EEEvNS_7EncArgsEPKNS_9EncTablesE": (4, 96),
+    "_ZN2ie13encode_kernelILi8ELb0ELb0ELi1EEEvNS_7EncArgsEPKNS_9EncTablesE": (4, 0),
+    "_ZN2ie15encode4w_kernelENS_7EncArgsEPKNS_9EncTablesE": (7, 0),
 }
 
 
@@ -106,7 +107,7 @@ def main(paths):
         # the encoder's bit image is addressed from LDS byte 0 (scatter_bits' inline ds_or): its
         # kernels must allocate no static LDS, so the dynamic area starts there
         for name, size in static_lds(p).items():
-            if "encode_kernel" in name and size != 0:
+            if ("encode_kernel" in name or "encode4w_kernel" in name) and size != 0:
                 rc = 1
                 print(f"{p}: {name} allocates {size} B of static LDS (scatter_bits assumes 0)", file=sys.stderr)
         bad, kernels = scan(p)

@@ -25,16 +25,18 @@ for name, (ew, eh) in {"ex1": (936, 936), "ex2": (512, 512), "ex3": (400, 400), 
     if os.path.exists(f):
         kinds[name] = np.fromfile(f, dtype=np.uint8)[: ew * eh].reshape(eh, ew)
 tag = "R=" + os.environ.get("IE_DEC_R", "dflt")
+hdr = int(os.environ.get("IE_HDR_BITS", "0"))  # a settings header of this many bits before the records (bench.py: 165 / 549)
+tag += f" hdr={hdr}"
 only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(kinds)
 for name, y in kinds.items():
     if name not in only:
         continue
     h, w = y.shape
-    out = torch.zeros(stream_bound(w, h, n, 1, 0), dtype=torch.uint8, device="cuda")
+    out = torch.zeros(stream_bound(w, h, n, 1, hdr), dtype=torch.uint8, device="cuda")
     pix = torch.empty((h, w), dtype=torch.uint8, device="cuda")
-    _, end = c.encode_frames(torch.from_numpy(y).cuda(), w, h, out)
+    _, end = c.encode_frames(torch.from_numpy(y).cuda(), w, h, out, start_bit=hdr)
     nb = (end + 7) // 8
-    c.decode_frames(out[:nb], w, h, pix, length=nb)
+    c.decode_frames(out[:nb], w, h, pix, length=nb, start_bit=hdr)
     ok = torch.equal(pix.cpu(), torch.from_numpy(y)) or True  # lossy: no pixel identity expected
     chunks, groups = c.last_decode_info()
     spec = c.last_decode_spec()
@@ -42,7 +44,7 @@ for name, y in kinds.items():
     k = 5
     t0 = time.perf_counter()
     for _ in range(k):
-        c.decode_frames(out[:nb], w, h, pix, length=nb)
+        c.decode_frames(out[:nb], w, h, pix, length=nb, start_bit=hdr)
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / k
     print(f"{tag:12s} n={n} {name:5s} {nb:9d} B  {t * 1e6:9.1f} us  chunks={chunks} groups={groups} spec={int(spec)}", flush=True)

@@ -5,16 +5,20 @@ FETCH_SIZE / WRITE_SIZE are reported in KiB.  MI355X_MICROARCH.md (HBM [CDNA4]):
 FETCH_SIZE counts exactly half the bytes of wide (16 B/lane) coalesced streaming reads -- the
 encoder's pixel loads are 16 B/lane (4x4 blocks) -- so it is doubled; WRITE_SIZE is exact for
 16 B/lane stores.  Usage:
-    python tools/traffic.py KERNEL_SUBSTR fetch_counter_collection.csv write_counter_collection.csv OUT.json
+    python tools/traffic.py KERNEL_SUBSTR fetch_counter_collection.csv write_counter_collection.csv OUT.json [GRID]
+GRID (optional): only dispatches of that Grid_Size (threads), e.g. the 16-frame sub-batch launches of
+c4 beside its 64-frame ones.
 """
 import csv
 import json
 import sys
 
 
-def mean_counter(path, kernel, counter):
+def mean_counter(path, kernel, counter, grid=None):
     vals = {}
     for r in csv.DictReader(open(path)):
+        if grid is not None and int(float(r.get("Grid_Size", 0))) != grid:
+            continue
         if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
             key = r.get("Dispatch_Id") or r.get("Correlation_Id") or str(len(vals))
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
@@ -28,8 +32,9 @@ def mean_counter(path, kernel, counter):
 
 def main():
     kernel, fcsv, wcsv, out = sys.argv[1:5]
-    f_kib, nf = mean_counter(fcsv, kernel, "FETCH_SIZE")
-    w_kib, nw = mean_counter(wcsv, kernel, "WRITE_SIZE")
+    grid = int(sys.argv[5]) if len(sys.argv) > 5 else None
+    f_kib, nf = mean_counter(fcsv, kernel, "FETCH_SIZE", grid)
+    w_kib, nw = mean_counter(wcsv, kernel, "WRITE_SIZE", grid)
     fetch = 2.0 * f_kib * 1024.0
     write = w_kib * 1024.0
     res = {
@@ -40,6 +45,7 @@ def main():
         "hbm_write_bytes_per_launch": int(write),
         "hbm_bytes_per_launch": int(fetch + write),
         "launches_averaged": [nf, nw],
+        "grid_size": grid,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (--kernel-trace only); "
                   "FETCH_SIZE x2 per the gfx950 correction for 16 B/lane streaming reads",
     }
