@@ -93,7 +93,7 @@ struct EncArgs {
     uint32_t* hist;
 };
 
-constexpr int kStamps = 16;
+constexpr int kStamps = 64;  // encode_kernel: [0, 16) by thread 0; encode4w_kernel: [4 waves][16] by each wave's lane 0
 // chain-state words per tile (the host allocates; ie_common.hpp kGran must not exceed it)
 constexpr int kStateWordsPerTile = 16;
 // bpt: blocks per thread, encode_blocks_per_thread(n, ntiles at the default) for the launch

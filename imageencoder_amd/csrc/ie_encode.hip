@@ -1492,19 +1492,20 @@ __device__ __forceinline__ float round_block_lean4(const EncTables* __restrict__
 #define IE_W_DBG 0
 #endif
 #ifndef IE_W_POOL
-#define IE_W_POOL 1  // one FP64 task list per tile (0: per wave)
+#define IE_W_POOL 0  // 0: FP64 tasks compacted per wave; 2: one list per tile, structural results as 2-bit deltas
 #endif
 #ifndef IE_W_AHEAD
 #define IE_W_AHEAD 2  // look-back windows per round trip (each holds 4 VGPRs live beside slots 2-3)
 #endif
 #ifndef IE_W_WAVES
-#define IE_W_WAVES 7  // __launch_bounds__ occupancy hint (waves per SIMD): <= 72 VGPRs
+#define IE_W_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD): 76 VGPRs, no scratch (7 spills with IE_W_POOL 0)
 #endif
 constexpr int kWReg = 1024;  // words per wave region: [4 rows][256 blocks] pixels, then the two slot-pair images in turn
 constexpr int kWTask = 128;  // words per wave: fix-up tasks [64] + results [64]
 constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9] excl, [10] ptail, [11] tail pending, [12] ticket
 constexpr int kWRows = 16 * 16 + 3 * 16;  // FP64 rows P[16][16], then S, rq, qd (doubles)
-constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc) * 4 + kWRows * 8;
+constexpr int kWDelta = 256;  // IE_W_POOL 2: one word per lane of the tile, the FP64 fix-up's structural deltas
+constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc + kWDelta) * 4 + kWRows * 8;
 
 // Inclusive scan over the 64 lanes of a wave by DPP row shifts and row broadcasts (six VALU).
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
@@ -1553,6 +1554,13 @@ __device__ __forceinline__ uint32_t slot_tail32(const uint32_t* I, uint32_t n, u
     return n ? ((prev << n) | (I[0] >> (32u - n))) : prev;
 }
 
+// profiling builds (IE_PROFILE, IE_STAMPS set): lane 0 of each wave stamps s_memtime at its phase
+// boundaries, [tile][wave][12] (tools/stamps_w.py)
+#define WSTAMP(i)                                                                                                   \
+    do {                                                                                                            \
+        if (IE_PROFILE && a.stamps && lane == 0) a.stamps[size_t(t) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
 __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -1562,7 +1570,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     uint32_t* const task = smem + 4 * kWReg + wv * kWTask;
     uint32_t* const res = task + 64;
     uint32_t* const misc = smem + 4 * kWReg + 4 * kWTask;
-    double* const srow = reinterpret_cast<double*>(misc + kWMisc);
+    uint32_t* const sdelta = misc + kWMisc;  // [4 waves][64 lanes]
+    double* const srow = reinterpret_cast<double*>(sdelta + kWDelta);
 
     int t;
     if (a.ticket) {
@@ -1573,6 +1582,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     } else {
         t = int(blockIdx.x);
     }
+    WSTAMP(0);
+    asm volatile("; PHASE w0" ::: "memory");
     if (tid == 0) {  // the tile's FP64 task counters (IE_W_POOL): structural, whole-block
         misc[16] = 0u;
         misc[17] = 0u;
@@ -1597,6 +1608,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     }
     lds_barrier();                                            // srow visible (the pixel DMA stays in flight)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
+    WSTAMP(1);
+    asm volatile("; PHASE w1" ::: "memory");
 
     // ------------------------------------------------------------ transform + quantise, 4 slots
     uint32_t zp[NS][NP];
@@ -1630,6 +1643,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         asm volatile("" : "+v"(flags));
     }
 
+    WSTAMP(2);
+    asm volatile("; PHASE w2" ::: "memory");
     // ------------------------------------------------------------ FP64 fix-up
     if constexpr (IE_W_POOL) {
         // One task list for the whole tile (IE_W_POOL): every flagged coefficient -- structural s
@@ -1647,6 +1662,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         uint32_t sbase = 0, wbase = 0;
         if (ns) sbase = atomicAdd(&misc[16], ns);  // (LDS atomics with return)
         if (nwb) wbase = atomicAdd(&misc[17], nwb);
+        if constexpr (IE_W_POOL == 2) sdelta[wv * 64 + lane] = 0u;
         lds_barrier();
         const uint32_t nstruct = __builtin_amdgcn_readfirstlane(misc[16]);
         const uint32_t wb0 = (nstruct + 15u) & ~15u;
@@ -1665,7 +1681,13 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
 #pragma unroll
                     for (int ss = 0; ss < 3; ss++)
                         if ((sfl >> (4 * b + ss)) & 1u) {
-                            if (i < kWPoolCap) pool[i] = tb | uint32_t(Structural<N>::k[ss]);
+                            if (i < kWPoolCap) {
+                                if constexpr (IE_W_POOL == 2)  // wave, lane, slot, s, and the FP32 value (high half)
+                                    pool[i] = (own >> 2) | (uint32_t(b) << 2) | uint32_t(ss) |
+                                              (zp[b][Structural<N>::zpos(ss) >> 1] & 0xFFFF0000u);
+                                else
+                                    pool[i] = tb | uint32_t(Structural<N>::k[ss]);
+                            }
                             i++;
                         }
                     if ((wfl >> (4 * b + 3)) & 1u) {
@@ -1676,9 +1698,27 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                 }
             }
             lds_barrier();  // tasks written; every wave's pixels are in LDS (each waited for its DMA)
+            if (w0 == 0) WSTAMP(11);
             const uint32_t nwin = min(kWPoolCap, total - w0);
             for (uint32_t r = uint32_t(wv) * 64u; r < nwin; r += 256u) {  // (uniform per wave)
-                if (r + uint32_t(lane) < nwin) {
+                const uint32_t gi = w0 + r + uint32_t(lane);  // the task's index in the tile's list
+                if (r + uint32_t(lane) >= nwin || (gi >= nstruct && gi < wb0)) {
+                    // past the window, or the padding before the 16-aligned whole-block groups: no task
+                } else if (IE_W_POOL == 2 && gi < nstruct) {
+                    // structural task: the FP64 value's difference from the owner's FP32 rounding
+                    // (-1, 0 or +1: both round a value within the FP32 bound of a tie) goes into the
+                    // owner's delta word as 2 bits at 6 * slot + 2 * s
+                    const uint32_t tk = pool[r + lane];
+                    const int ss = int(tk & 3u), b = int((tk >> 2) & 3u), ol = int((tk >> 4) & 63u);
+                    const int ow = int((tk >> 10) & 3u);
+                    const int k = Structural<N>::k[0] * (ss == 0) + Structural<N>::k[1] * (ss == 1) + Structural<N>::k[2] * (ss == 2);
+                    const uint32_t* opx = smem + ow * kWReg + 64 * b + ol;
+                    const int y1 = (IE_W_DBG & 128) ? int(int16_t(tk >> 16)) + int(opx[0] & 1u)  // profiling: no FP64
+                                                    : exact_coef_rows4(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                                       srow[NN * NN + 2 * NN + k], opx);
+                    const uint32_t d = uint32_t(y1 - int(int16_t(tk >> 16))) & 3u;
+                    if (d) atomicOr(&sdelta[ow * 64 + ol], d << (6 * b + 2 * ss));
+                } else {
                     const uint32_t tk = pool[r + lane];
                     const int k = int(tk & 15u), b = int((tk >> 4) & 3u), ol = int((tk >> 6) & 63u);
                     const int ow = int((tk >> 12) & 3u);
@@ -1698,8 +1738,24 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                     }
                 }
             }
+            if (w0 == 0) WSTAMP(12);
             lds_barrier();  // results in place
-            if (sfl) {
+            if (w0 == 0) WSTAMP(13);
+            if constexpr (IE_W_POOL == 2) {
+                if (__ballot(sfl != 0) && w0 + kWPoolCap >= total) {  // (after the last window)
+                    // branch-free: every structural coefficient += its 2-bit delta (0 unless the
+                    // FP64 evaluation rounded it otherwise), as int16 in the high half of its word
+                    const uint32_t dw = sdelta[wv * 64 + lane];
+#pragma unroll
+                    for (int b = 0; b < NS; b++)
+#pragma unroll
+                        for (int ss = 0; ss < 3; ss++) {
+                            const int zw = Structural<N>::zpos(ss) >> 1;  // (high halves, see below)
+                            const int d = __builtin_amdgcn_sbfe(int(dw), 6 * b + 2 * ss, 2);
+                            zp[b][zw] = uint32_t(d << 16) + zp[b][zw];
+                        }
+                }
+            } else if (sfl) {
                 uint32_t i = sbase - w0;
 #pragma unroll
                 for (int b = 0; b < NS; b++) {
@@ -1844,6 +1900,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         if (lane == 0) a.wave_fix[size_t(t) * (TPB / 64) + wv] = wsum;
     }
 
+    WSTAMP(3);
+    asm volatile("; PHASE w3" ::: "memory");
     // ------------------------------------------------------------ sizing + the wave's offsets
     uint32_t blw[NS], rb[NS];
     const uint32_t k0 = uint32_t(tif * TPB + 64 * wv) * 4u;  // the wave's first block (frame raster order)
@@ -1882,7 +1940,11 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     off[3] = e23 >> 16;
     const uint32_t S1 = T[0], S2 = S1 + T[1], S3 = S2 + T[2], Tw = S3 + T[3];
     if (lane == 0) misc[wv] = Tw;
+    WSTAMP(4);
+    asm volatile("; PHASE w4" ::: "memory");
     lds_barrier();  // ---- the tile's bit count and this wave's place in it
+    WSTAMP(5);
+    asm volatile("; PHASE w5" ::: "memory");
 
     uint32_t A = 0, W = 0;
 #pragma unroll
@@ -1916,6 +1978,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     emit_slot(0);
     emit_slot(1);
     wave_sync();
+    WSTAMP(6);
+    asm volatile("; PHASE w6" ::: "memory");
     if (lane == 0 && Tw) misc[4 + wv] = reg[0];  // the wave's first 32 bits
 
     // ------------------------------------------------------------ look-back (wave 0)
@@ -1949,7 +2013,11 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
             if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
         }
     }
+    WSTAMP(7);
+    asm volatile("; PHASE w7" ::: "memory");
     lds_barrier();  // ---- the tile's position
+    WSTAMP(8);
+    asm volatile("; PHASE w8" ::: "memory");
 
     // ------------------------------------------------------------ store, slot by slot
     if (!(IE_W_DBG & 2) && Tw) {
@@ -1970,6 +2038,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
             prev = slot_tail32(reg, n, prev);
         };
         store_pair(0u, S2);
+        WSTAMP(9);
+    asm volatile("; PHASE w9" ::: "memory");
         if (Tw > S2) {
             wave_sync();  // pair 0's image has been read
             zero_img(Tw - S2);
@@ -1993,6 +2063,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                 out[Xw >> 5] = bswap32((pt << (32u - s)) | (misc[4] >> s));
             }
         }
+        WSTAMP(10);
+    asm volatile("; PHASE w10" ::: "memory");
     }
 }
 
@@ -2031,7 +2103,7 @@ void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt)
     EncArgs a = a0;
     // 4x4 FAST over whole 16-byte groups: the wave-local encoder (encode4w_kernel)
     if (IE_ENC_W && n == 4 && !exact && !a.hist && bpt == 4 && a.vec_ok && a.bx % 4 == 0 &&
-        a.groups_per_frame % 8 == 0 && a.rec_bits <= 252 && !a.ablate && !a.stamps) {
+        a.groups_per_frame % 8 == 0 && a.rec_bits <= 252 && !a.ablate) {
         launch_encode4w(a, s);
         return;
     }

@@ -49,7 +49,7 @@ def _budget_asm(occ, scratch):
 
 def test_register_budget_holds(tmp_path):
     p = tmp_path / "k.s"
-    p.write_text(_budget_asm(4, 68))
+    p.write_text(_budget_asm(4, 0))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asmcheck.py"), str(p)],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
@@ -57,7 +57,7 @@ def test_register_budget_holds(tmp_path):
 
 def test_spilling_kernel_over_budget_fails(tmp_path):
     p = tmp_path / "k.s"
-    p.write_text(_budget_asm(4, 308))  # the spill an unguarded profiling branch once caused
+    p.write_text(_budget_asm(4, 68))  # the scratch the per-lane pixel rows once cost the 8x8 kernel
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asmcheck.py"), str(p)],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "over budget" in r.stderr

@@ -1,0 +1,20 @@
+"""One C2-shaped launch (16 4K uniform-noise frames) with IE_STAMPS set (run with IE_LIB = an
+IE_PROFILE build): writes the per-tile stamps file named by IE_STAMPS."""
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+from imageencoder_amd import Codec, stream_bound, synth  # noqa: E402
+from tests import oracle_lib as O  # noqa: E402
+
+w, h, nf = 3840, 2160, 16
+c = Codec(0, O.read_matrix("matrix.txt", 4), 4)
+y = synth.uniform_device(w, h, nf, 3, "cuda", torch)
+pitch = (stream_bound(w, h, 4, 1, 165) + 255) // 256 * 256
+out = torch.zeros(pitch * nf, dtype=torch.uint8, device="cuda")
+for _ in range(3):
+    c.encode_images(y, w, h, out, out_pitch=pitch, nframes=nf, start_bit=165)
+torch.cuda.synchronize()
+print("stamps written to", os.environ.get("IE_STAMPS"))

@@ -1,0 +1,31 @@
+"""Summarise encode4w_kernel's per-wave phase stamps (IE_PROFILE build, IE_STAMPS=file: s_memtime at
+each phase boundary by every wave's lane 0, [tile][4 waves][12]) of one launch.
+usage: python tools/stamps_w.py stamps.bin [clock_ghz]"""
+import sys
+
+import numpy as np
+
+names = ["load", "transform", "fix-up", "size+scan", "barrier(count)", "emit pair 0", "look-back",
+         "barrier(position)", "store pair 0", "refill+store pair 1"]
+raw = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 64).astype(np.int64)
+ghz = float(sys.argv[2]) if len(sys.argv) > 2 else 2.3
+w16 = raw.reshape(-1, 4, 16)
+w = w16[:, :, :11]
+rows = w.reshape(-1, 11)
+wave = np.tile(np.arange(4), len(w))
+ok = (rows > 0).all(axis=1)
+rows, wave = rows[ok], wave[ok]
+d = np.diff(rows, axis=1) / ghz / 1e3
+print(f"waves {len(rows)}")
+print("phase                 all_mean  wave0  waves1-3   p90")
+for i, nm in enumerate(names):
+    print(f"{nm:20s} {d[:, i].mean():8.3f} {d[wave == 0, i].mean():7.3f} {d[wave > 0, i].mean():8.3f} "
+          f"{np.percentile(d[:, i], 90):7.3f}")
+life = (rows[:, -1] - rows[:, 0]) / ghz / 1e3
+print(f"wave lifetime mean {life.mean():.2f} us  p50 {np.median(life):.2f}")
+fx = w16.reshape(-1, 16)[:, [2, 11, 12, 13, 3]]
+fx = fx[(fx > 0).all(axis=1)]
+if len(fx):
+    dd = np.diff(fx, axis=1) / ghz / 1e3
+    print(f"fix-up split ({len(fx)} waves): tasks+barrier {dd[:, 0].mean():.3f}  eval {dd[:, 1].mean():.3f}  "
+          f"barrier {dd[:, 2].mean():.3f}  patch {dd[:, 3].mean():.3f} us")
