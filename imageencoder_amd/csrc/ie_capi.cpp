@@ -2290,6 +2290,66 @@ int finish_decode(ie_ctx* c, uint8_t* out, const uint8_t* dpix, bool out_dev, in
     return IE_OK;
 }
 
+// Chunk plan of a record span (span bits from the first record, nblocks records) and the
+// parse buffers it needs: fills a's chunking fields and scratch pointers, *levels = composition
+// levels.  The record stream's own fields (words, nbits, start_bit, dstart, total, end_out) are
+// the caller's.
+int plan_records(ie_ctx* c, uint64_t span, uint64_t nblocks, ie::RecParseArgs& a, size_t* spec_at_out, int* levels_out) {
+    const int n = c->n;
+    int r;
+    // chunking: about R records per chunk (IE_DEC_R; default 24 for 4x4, 28 for 8x8: measured
+    // with 32-table composition groups on 4K noise / mixed / gradient / flat frames and the
+    // reference's ex1 / ex4 -- 4x4 against 16, 24, 32, 48: ex4 126 -> 115 us, mixed 197 -> 191 us,
+    // noise and flat unchanged; 8x8 against 20-32: noise 342 -> 258 us, ex1 376 -> 269 us,
+    // gradient 209 -> 181 us, flat 101 -> 112 us; 8x8 noise alone is erratic in R, 2.6x slower at
+    // 24) so that every chunk's walks are short; C a multiple of 32, at least
+    // 256 bits, at most 2^15 (16-bit record positions; a table wave's LDS -- the chunk's bits and
+    // valid-header bitmap -- stays small)
+    const int G = ie::rec_group_chunks(n), D = ie::rec_entry_span(n);
+    static const char* rs = getenv("IE_DEC_R");
+    const uint64_t recs = rs ? std::max<uint64_t>(1, strtoull(rs, nullptr, 10)) : (n == 4 ? 24 : 28);
+    const uint64_t want = std::max<uint64_t>((nblocks + recs - 1) / recs, 1);
+    uint64_t C = (span + want - 1) / want;
+    C = std::min<uint64_t>(std::max<uint64_t>((C + 31) / 32 * 32, 256), uint64_t(1) << 15);
+    const uint64_t nch = std::max<uint64_t>((span + C - 1) / C, 1);
+    // levels: ceil(n / G) composites per level until at most G remain (G^4 chunks at most)
+    size_t tab_rows = 0;
+    int levels = 0;
+    for (uint64_t cur = nch;; cur = (cur + G - 1) / G) {
+        tab_rows += cur;
+        levels++;
+        if ((cur + G - 1) / G <= uint64_t(G)) {
+            tab_rows += (cur + G - 1) / G;
+            break;
+        }
+    }
+    if (levels > ie::kRecMaxLevels || nch > uint64_t(INT32_MAX))
+        return fail(c, IE_EINVAL, "stream too long for one decode call");
+    const int nchunks = int(nch);
+    if ((r = ensure(c, c->d_rtab, c->cap_rtab, tab_rows * D))) return r;
+    // d_walk (8-byte words): [nchunks / 2] in-workgroup record bases, [G / 2] top-level entries,
+    // [nchunks / 2] chunk counts, [nchunks / 2] count-pass workgroup totals (a workgroup covers at
+    // least 4 chunks)
+    const size_t e_at = size_t(nchunks) / 2 + 1, cnt_at = e_at + size_t(G) / 2 + 1;
+    const size_t wg_at = cnt_at + size_t(nchunks) / 2 + 1;
+    const size_t spec_at = wg_at + size_t(nchunks) / 2 + 2;  // [nchunks / 2] speculative exits
+    if ((r = ensure(c, c->d_walk, c->cap_walk, spec_at + size_t(nchunks) / 2 + 1))) return r;
+    if ((r = ensure(c, c->d_rpos, c->cap_rpos, size_t(nchunks) * ie::kRecPosCap))) return r;
+    a.C = uint32_t(C);
+    a.nchunks = nchunks;
+    a.tab = c->d_rtab;
+    a.seg = ie::rec_count_seg(uint32_t(C));
+    a.lbase = reinterpret_cast<uint32_t*>(c->d_walk);
+    a.wgsum = reinterpret_cast<uint32_t*>(c->d_walk + wg_at);
+    a.E = reinterpret_cast<uint32_t*>(c->d_walk + e_at);
+    a.cnt = reinterpret_cast<uint32_t*>(c->d_walk + cnt_at);
+    a.pos = c->d_rpos;
+    a.ticket = reinterpret_cast<unsigned*>(c->d_misc + 1);
+    if (spec_at_out) *spec_at_out = spec_at;
+    *levels_out = levels;
+    return IE_OK;
+}
+
 // add_base: P-frame error -- the decoded error is added to the pixels already in `out`
 #if IE_PROFILE  // host-side phase times of the record decode (IE_DEC_HOST=1): entry, launches, sync
 struct DecHostTimes {
@@ -2335,44 +2395,11 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     const uint64_t nbits = uint64_t(len) * 8;
     const uint64_t span = nbits - start_bit;
     const uint64_t nblocks = uint64_t(nframes) * (w / n) * (h / n);
-    // chunking: about R records per chunk (IE_DEC_R; default 24 for 4x4, 28 for 8x8: measured
-    // with 32-table composition groups on 4K noise / mixed / gradient / flat frames and the
-    // reference's ex1 / ex4 -- 4x4 against 16, 24, 32, 48: ex4 126 -> 115 us, mixed 197 -> 191 us,
-    // noise and flat unchanged; 8x8 against 20-32: noise 342 -> 258 us, ex1 376 -> 269 us,
-    // gradient 209 -> 181 us, flat 101 -> 112 us; 8x8 noise alone is erratic in R, 2.6x slower at
-    // 24) so that every chunk's walks are short; C a multiple of 32, at least
-    // 256 bits, at most 2^15 (16-bit record positions; a table wave's LDS -- the chunk's bits and
-    // valid-header bitmap -- stays small)
-    const int G = ie::rec_group_chunks(n), D = ie::rec_entry_span(n);
-    static const char* rs = getenv("IE_DEC_R");
-    const uint64_t recs = rs ? std::max<uint64_t>(1, strtoull(rs, nullptr, 10)) : (n == 4 ? 24 : 28);
-    const uint64_t want = std::max<uint64_t>((nblocks + recs - 1) / recs, 1);
-    uint64_t C = (span + want - 1) / want;
-    C = std::min<uint64_t>(std::max<uint64_t>((C + 31) / 32 * 32, 256), uint64_t(1) << 15);
-    const uint64_t nch = std::max<uint64_t>((span + C - 1) / C, 1);
-    // levels: ceil(n / G) composites per level until at most G remain (G^4 chunks at most)
-    size_t tab_rows = 0;
+    ie::RecParseArgs pa{};
+    size_t spec_at = 0;
     int levels = 0;
-    for (uint64_t cur = nch;; cur = (cur + G - 1) / G) {
-        tab_rows += cur;
-        levels++;
-        if ((cur + G - 1) / G <= uint64_t(G)) {
-            tab_rows += (cur + G - 1) / G;
-            break;
-        }
-    }
-    if (levels > ie::kRecMaxLevels || nch > uint64_t(INT32_MAX))
-        return fail(c, IE_EINVAL, "stream too long for one decode call");
-    const int nchunks = int(nch);
-    if ((r = ensure(c, c->d_rtab, c->cap_rtab, tab_rows * D))) return r;
-    // d_walk (8-byte words): [nchunks / 2] in-workgroup record bases, [G / 2] top-level entries,
-    // [nchunks / 2] chunk counts, [nchunks / 2] count-pass workgroup totals (a workgroup covers at
-    // least 4 chunks)
-    const size_t e_at = size_t(nchunks) / 2 + 1, cnt_at = e_at + size_t(G) / 2 + 1;
-    const size_t wg_at = cnt_at + size_t(nchunks) / 2 + 1;
-    const size_t spec_at = wg_at + size_t(nchunks) / 2 + 2;  // [nchunks / 2] speculative exits
-    if ((r = ensure(c, c->d_walk, c->cap_walk, spec_at + size_t(nchunks) / 2 + 1))) return r;
-    if ((r = ensure(c, c->d_rpos, c->cap_rpos, size_t(nchunks) * ie::kRecPosCap))) return r;
+    if ((r = plan_records(c, span, nblocks, pa, &spec_at, &levels))) return r;
+    const int nchunks = pa.nchunks;
     const size_t pix_bytes = size_t(nframes - 1) * frame_pitch + stride * size_t(h - 1) + size_t(w);
     const bool out_dev = is_device_ptr(out);
     uint8_t* dpix = out;
@@ -2390,20 +2417,10 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     da.stride = stride;
     da.frame_pitch = frame_pitch;
     da.tab = c->d_tab;
-    ie::RecParseArgs pa{};
     pa.words = reinterpret_cast<const uint32_t*>(words);
     pa.nbits = nbits;
     pa.start_bit = start_bit;
-    pa.C = uint32_t(C);
-    pa.nchunks = nchunks;
     pa.rle = da.rle;
-    pa.tab = c->d_rtab;
-    pa.seg = ie::rec_count_seg(uint32_t(C));
-    pa.lbase = reinterpret_cast<uint32_t*>(c->d_walk);
-    pa.wgsum = reinterpret_cast<uint32_t*>(c->d_walk + wg_at);
-    pa.E = reinterpret_cast<uint32_t*>(c->d_walk + e_at);
-    pa.cnt = reinterpret_cast<uint32_t*>(c->d_walk + cnt_at);
-    pa.pos = c->d_rpos;
     if (!c->h_decres) {
         void* hp = nullptr;
         HIPCHK(c, hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -2412,7 +2429,6 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
         HIPCHK(c, hipHostGetDevicePointer(&dp, hp, 0));
         c->d_decres = static_cast<uint64_t*>(dp);
     }
-    pa.ticket = reinterpret_cast<unsigned*>(c->d_misc + 1);
     pa.total = c->d_decres + 1;
     pa.end_out = c->d_decres;
     // (d_misc needs no clearing: the last chunk's decode wave always writes the record total, and
@@ -2426,7 +2442,7 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
     static const char* dstamps = getenv("IE_DEC_STAMPS");  // file: [table waves][8] u64 per call
     uint64_t* d_ws = nullptr;
     int tm_ = 1, hb_ = 0;
-    ie::rec_table_geometry(uint32_t(C), n, &tm_, &hb_);
+    ie::rec_table_geometry(pa.C, n, &tm_, &hb_);
     const size_t nws = size_t(nchunks + tm_ - 1) / size_t(tm_) * 8;
     if (dstamps) {
         HIPCHK(c, hipMalloc(&d_ws, nws * 8));
@@ -2491,7 +2507,7 @@ int decode_frames_impl(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_
         uint64_t st[5];
         HIPCHK(c, hipMemcpy(st, c->d_misc + 3, sizeof(st), hipMemcpyDeviceToHost));
         fprintf(stderr, "[dec] chunks %d C %u: lane-steps %.1f/chunk, beyond-window %.1f/chunk, unmerged walks %.2f/chunk, "
-                "wave max steps avg %.1f max %llu\n", nchunks, unsigned(C), double(st[0]) / nchunks, double(st[1]) / nchunks,
+                "wave max steps avg %.1f max %llu\n", nchunks, unsigned(pa.C), double(st[0]) / nchunks, double(st[1]) / nchunks,
                 double(st[2]) / nchunks, double(st[3]) / nchunks, (unsigned long long)st[4]);
         HIPCHK(c, hipMemsetAsync(c->d_misc + 3, 0, sizeof(uint64_t), c->stream));
     }
@@ -2521,6 +2537,10 @@ int ie_decode_frames(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bi
 // Video decode with P-frames (VideoDecoder.cpp:28-58, Frame.cpp:47-127): frame by frame, each
 // starting at the previous frame's end; a P-frame's motion vectors and reference-block copies
 // (pf_mvcopy_kernel), then its records (every microblock's) decoded onto the copied pixels.
+// Device-chained: every frame's launches read its first bit from the device word the previous
+// frame's decode wrote (pos[f], RecParseArgs::dstart), with chunks planned from the frame's bound
+// rather than its span, so the whole call is enqueued at once and the host waits once, at the end,
+// for the end bits and record totals it checks.
 int ie_decode_gop(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, int w, int h, int nframes, int gop,
                   int merange, int use_rle, int motioncomp, uint8_t* out, size_t stride, size_t frame_pitch,
                   uint64_t* end_bit) {
@@ -2537,11 +2557,11 @@ int ie_decode_gop(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, 
                                   "misplaced otherwise and its uncovered microblocks read records never written");
     if (start_bit > uint64_t(len) * 8) return fail(c, IE_EINVAL, "start_bit beyond the stream");
     HIPCHK(c, hipSetDevice(c->device));
-    // the stream once on the device (zero padding for the vector reads), the frames decoded into
-    // a device buffer (P-frames read their predecessor there)
-    const size_t padded = len + 16;
+    // the stream once on the device (16-byte aligned, zero padding for the vector reads), the
+    // frames decoded into a device buffer (P-frames read their predecessor there)
+    const size_t padded = (len + 3) / 4 * 4 + 16;
     if ((r = ensure(c, c->d_in, c->cap_in, padded))) return r;
-    HIPCHK(c, hipMemsetAsync(c->d_in + len, 0, 16, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_in + (len / 4) * 4, 0, padded - (len / 4) * 4, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_in, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                              c->stream));
     const bool out_dev = is_device_ptr(out);
@@ -2552,38 +2572,74 @@ int ie_decode_gop(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, 
         dpix = c->d_gop_rec;
     }
     const int n = c->n, mv = mvec_bits(merange);
-    const uint64_t nmb = uint64_t(w / 16) * (h / 16);
-    const uint64_t rec_bound = uint64_t(w / n) * (h / n) * bound_bits_per_block(n);
-    uint64_t pos = start_bit;
+    const uint64_t nbits = uint64_t(len) * 8;
+    const uint64_t nmb = uint64_t(w / 16) * (h / 16), mvb = nmb * 2u * uint64_t(mv);
+    const uint64_t nblocks = uint64_t(w / n) * (h / n);
+    const uint64_t rec_bound = nblocks * bound_bits_per_block(n);
+    // per-frame device words: pos[0..nframes] first bits (pos[f + 1] = frame f's end), tot[f]
+    // records on frame f's true path; then the host copy of both
+    const size_t nw = 2 * size_t(nframes) + 1;
+    if ((r = ensure(c, c->d_gop_pos, c->cap_gop_pos, nw))) return r;
+    uint64_t* pos = c->d_gop_pos;
+    uint64_t* tot = pos + nframes + 1;
+    ie::launch_gop_init(pos, tot, nframes, start_bit, c->stream);
+    HIPCHK(c, hipGetLastError());
+    // one chunk plan for every frame: its bound (plus a P-frame's vectors), so the grids and
+    // scratch do not depend on where a frame ends
+    ie::RecParseArgs pa{};
+    int levels = 0;
+    if ((r = plan_records(c, rec_bound, nblocks, pa, nullptr, &levels))) return r;
+    pa.words = reinterpret_cast<const uint32_t*>(c->d_in);
+    pa.nbits = nbits;
+    pa.rle = use_rle ? 1 : 0;
+    pa.span = rec_bound;
+    if (gop > 1 && nframes > 1 && !motioncomp)
+        if ((r = ensure(c, c->d_gop_coef, c->cap_gop_coef, (stride * size_t(h) + 1) / 2))) return r;
     for (int f = 0; f < nframes; f++) {
         uint8_t* fo = dpix + size_t(f) * frame_pitch;
         const bool iframe = (f % gop) == 0;
         if (!iframe) {
-            if (pos + nmb * 2u * uint64_t(mv) > uint64_t(len) * 8) return fail(c, IE_EFORMAT, "stream ends in the motion vectors");
-            ie::launch_pframe_mvcopy(c->d_in, pos, mv, fo - frame_pitch, stride, fo, stride, w, h, c->stream);
+            ie::launch_pframe_mvcopy(c->d_in, 0, pos + f, nbits, mv, fo - frame_pitch, stride, fo, stride, w, h, c->stream);
             HIPCHK(c, hipGetLastError());
-            pos += nmb * 2u * uint64_t(mv);
         }
-        // the records from the byte holding pos, at most this frame's bound of the stream
-        const size_t b0 = size_t(pos / 8);
-        const size_t flen = size_t(std::min<uint64_t>(uint64_t(len) - b0, (pos % 8 + rec_bound + 7) / 8 + 8));
-        uint64_t e = 0;
+        ie::DecArgs da{};
+        da.nframes = 1;
+        da.bx = w / n;
+        da.by = h / n;
+        da.rle = pa.rle;
+        da.tab = c->d_tab;
         if (!iframe && !motioncomp) {
             // the error is read (the stream must be consumed) but not applied: decode into scratch
-            if ((r = ensure(c, c->d_gop_coef, c->cap_gop_coef, (stride * size_t(h) + 1) / 2))) return r;
-            r = decode_frames_impl(c, c->d_in + b0, flen, pos % 8, w, h, 1, use_rle,
-                                   reinterpret_cast<uint8_t*>(c->d_gop_coef), stride, 0, &e, 0);
+            da.out = reinterpret_cast<uint8_t*>(c->d_gop_coef);
+            da.add_base = 0;
         } else {
-            r = decode_frames_impl(c, c->d_in + b0, flen, pos % 8, w, h, 1, use_rle, fo, stride, 0, &e, iframe ? 0 : 1);
+            da.out = fo;
+            da.add_base = iframe ? 0 : 1;
         }
-        if (r) return r;
-        pos = uint64_t(b0) * 8 + e;
+        da.stride = stride;
+        da.frame_pitch = 0;
+        pa.dstart = pos + f;
+        pa.start_add = iframe ? 0 : mvb;
+        pa.total = tot + f;
+        pa.end_out = pos + f + 1;
+        if (ie::launch_rec_parse_decode(pa, da, n, c->stream) < 0) return fail(c, IE_EINVAL, "stream too long for one decode call");
+        HIPCHK(c, hipGetLastError());
+    }
+    std::vector<uint64_t> hp(nw);
+    HIPCHK(c, hipMemcpyAsync(hp.data(), pos, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->last_chunks = pa.nchunks;
+    c->last_groups = levels;
+    c->last_spec = 0;
+    for (int f = 0; f < nframes; f++) {
+        if ((f % gop) != 0 && hp[f] + mvb > nbits) return fail(c, IE_EFORMAT, "stream ends in the motion vectors");
+        if (hp[nframes + 1 + f] < nblocks || hp[f + 1] > nbits) return fail(c, IE_EFORMAT, "stream ends before the last block");
     }
     if (!out_dev)
         for (int f = 0; f < nframes; f++)
             HIPCHK(c, hipMemcpy2D(out + size_t(f) * frame_pitch, stride, dpix + size_t(f) * frame_pitch, stride,
                                   size_t(w), size_t(h), hipMemcpyDeviceToHost));
-    if (end_bit) *end_bit = pos;
+    if (end_bit) *end_bit = hp[nframes];
     return IE_OK;
 }
 

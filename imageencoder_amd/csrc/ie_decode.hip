@@ -470,6 +470,19 @@ __device__ __forceinline__ uint32_t rec_chunk_entry(const RecParseArgs& a, int k
     return table_entry<RecGeom<N>::D, RecGeom<N>::G>(a.E, a.lvl, a.levels, k);
 }
 
+// The record span of a launch: [start, nbits) -- the host's, or, device-chained (a.dstart), from
+// an earlier launch's end bit (clamped to the stream; ~0 = that launch found no end) for at most
+// a.span bits.  Chunks past the span's end see no stream bits and hold no record.
+struct RecSpan {
+    uint64_t start, nbits;
+};
+__device__ __forceinline__ RecSpan rec_span(const RecParseArgs& a) {
+    if (!a.dstart) return {a.start_bit, a.nbits};
+    const uint64_t st = min(min(*a.dstart, a.nbits) + a.start_add, a.nbits);
+    return {st, min(a.nbits, st + a.span)};
+}
+__device__ __forceinline__ uint64_t sat_sub(uint64_t x, uint64_t y) { return x > y ? x - y : 0ull; }
+
 // L[i] = bswap(W[w0 + i]) for i < nw (zeros past nwords) by one wave with 16-byte loads, four
 // per lane in flight; L must be 16-byte aligned.  The copy starts at the aligned word w0 & ~3:
 // returns the offset of word w0 in L (0..3).
@@ -560,13 +573,14 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     uint16_t* res = reinterpret_cast<uint16_t*>(H + HM + 1);
     uint16_t* tgt = res + tm * D1;
     uint32_t* wl = H + HM + 1 + tm * D1;  // after res + tgt (tm * D1 words together)
-    const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
+    const RecSpan sp = rec_span(a);
+    const uint64_t c0 = sp.start + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
     const int off = stage_words16(L, a.words, base >> 5, int(((c0 - base) + uint64_t(m) * C + 64) >> 5) + 2,
-                                  a.nbits, lane);
+                                  sp.nbits, lane);
     const uint32_t s0 = uint32_t(c0 - base) + 32u * uint32_t(off);  // the wave's first bit in L
     // positions below are relative to s0; no record starts at or past the stream's end
-    const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - c0, uint64_t(m) * C));
+    const uint32_t lim = uint32_t(min<uint64_t>(sat_sub(sp.nbits, c0), uint64_t(m) * C));
     for (uint32_t i = lane; i <= HM; i += 64) H[i] = 0xFFFFFFFFu;
     __syncthreads();
     wstamp(1);
@@ -740,10 +754,11 @@ __global__ __launch_bounds__(kTPB) void rec_spec_kernel(RecParseArgs a) {
     if (m == 0) return;
     const int kw = max(k0 - W, 0);  // the wave's first staged chunk
     uint32_t* L = Lall + size_t(wv) * rec_count_wave_words(a.C, seg + W);
-    const uint64_t c0 = a.start_bit + uint64_t(kw) * a.C;
+    const RecSpan sp = rec_span(a);
+    const uint64_t c0 = sp.start + uint64_t(kw) * a.C;
     const uint64_t base = c0 & ~31ull;
     const int off = stage_words16(L, a.words, base >> 5,
-                                  int(((c0 - base) + uint64_t(k0 + m - kw) * a.C + 64) >> 5) + 2, a.nbits, lane);
+                                  int(((c0 - base) + uint64_t(k0 + m - kw) * a.C + 64) >> 5) + 2, sp.nbits, lane);
     const uint32_t s0 = uint32_t(c0 - base) + 32u * uint32_t(off);  // chunk kw's first bit in L
     wave_sync();
     const int k = k0 + lane;
@@ -769,11 +784,12 @@ __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
     const int m = max(0, min(seg, a.nchunks - k0));
     uint32_t* L = Lall + size_t(wv) * rec_count_wave_words(a.C, seg);
     uint32_t s0 = 0;
+    const RecSpan sp = rec_span(a);
     if (m > 0) {
-        const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
+        const uint64_t c0 = sp.start + uint64_t(k0) * a.C;
         const uint64_t base = c0 & ~31ull;
         const int off = stage_words16(L, a.words, base >> 5, int(((c0 - base) + uint64_t(m) * a.C + 64) >> 5) + 2,
-                                      a.nbits, lane);
+                                      sp.nbits, lane);
         s0 = uint32_t(c0 - base) + 32u * uint32_t(off);  // the wave's first bit, relative to L
     }
     const int k = k0 + lane;
@@ -782,8 +798,8 @@ __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
     wave_sync();
     uint32_t R = 0;
     if (mine) {
-        const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;  // = bit s0 of L
-        const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - c0 + s0, uint64_t(s0) + uint64_t(m) * a.C));
+        const uint64_t c0 = sp.start + uint64_t(k0) * a.C;  // = bit s0 of L
+        const uint32_t lim = uint32_t(min<uint64_t>(sat_sub(sp.nbits, c0) + s0, uint64_t(s0) + uint64_t(m) * a.C));
         const uint32_t cs = s0 + uint32_t(lane) * a.C;
         const uint32_t cb = cs & ~31u;  // the chunk's first word
         const uint32_t ce = min(cs + a.C, lim);  // no record starts at or past the stream's end
@@ -831,12 +847,13 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
     }
     const int m = min(P, a.nchunks - k0);
     uint32_t* L = dyn_all + size_t(wv) * rec_decode_stream_words(uint32_t(P) * a.C, D);
-    const uint64_t c0 = a.start_bit + uint64_t(k0) * a.C;
+    const RecSpan sp = rec_span(a);
+    const uint64_t c0 = sp.start + uint64_t(k0) * a.C;
     const uint64_t base = c0 & ~31ull;
     // the chunks' bits first (16-byte loads in flight while the indices below are read); bit
     // positions in L are relative to word `off` of L, which holds the first chunk's first word
     const int off = stage_words16(L, a.words, base >> 5, int((uint32_t(c0 - base) + uint32_t(m) * a.C + D + 64) >> 5) + 2,
-                                  a.nbits, lane);
+                                  sp.nbits, lane);
     const uint32_t ob = 32u * uint32_t(off);
     const uint32_t s0 = uint32_t(c0 - base) + ob;
     const uint64_t lbase0 = base - ob;  // stream bit of L's bit 0
@@ -877,7 +894,7 @@ __global__ __launch_bounds__(64 * kRecWPB) void rec_decode_kernel(RecParseArgs a
     uint64_t gi = first;
     for (int j = 0; j < m; j++) {
         uint32_t p = s0 + uint32_t(j) * a.C + rec_chunk_entry<N>(a, k0 + j);
-        const uint32_t wend = uint32_t(min<uint64_t>(s0 + uint64_t(j + 1) * a.C, a.nbits - lbase0));
+        const uint32_t wend = uint32_t(min<uint64_t>(s0 + uint64_t(j + 1) * a.C, sat_sub(sp.nbits, lbase0)));
         while (p < wend && gi < nblocks) {
             uint32_t mine = 0, n = 0;
             while (n < 64u && p < wend) {
@@ -940,6 +957,16 @@ int launch_rec_parse_decode(RecParseArgs a, const DecArgs& d, int n, hipStream_t
     if (n == 4) hipLaunchKernelGGL((rec_decode_kernel<4>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 4), s, a, d);
     else hipLaunchKernelGGL((rec_decode_kernel<8>), dim3(nb), dim3(64 * kRecWPB), rec_decode_lds(a.C, 8), s, a, d);
     return levels;
+}
+
+__global__ void gop_init_kernel(uint64_t* pos, uint64_t* tot, int n, uint64_t start) {
+    for (int i = threadIdx.x; i <= n; i += blockDim.x) {
+        pos[i] = i ? ~0ull : start;
+        if (i < n) tot[i] = 0;
+    }
+}
+void launch_gop_init(uint64_t* pos, uint64_t* tot, int n, uint64_t start, hipStream_t s) {
+    hipLaunchKernelGGL(gop_init_kernel, dim3(1), dim3(256), 0, s, pos, tot, n, start);
 }
 
 void launch_rec_spec_decode(const RecParseArgs& a, const DecArgs& d, int n, hipStream_t s) {

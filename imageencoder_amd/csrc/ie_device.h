@@ -214,6 +214,11 @@ struct RecParseArgs {
     uint32_t* spec;
     unsigned* fail;         // device word, cleared by the speculative pass
     int warm;               // speculative walks start this many chunks early (IE_DEC_WARM, default 0)
+    // device-chained span (ie_decode_gop): when non-null the first record is at
+    // min(*dstart + start_add, nbits) -- an earlier launch's end bit -- and the span ends at most
+    // `span` bits after it (start_bit is then unused); chunks past the span's end hold no record
+    const uint64_t* dstart;
+    uint64_t start_add, span;
 };
 // Table-wave geometry for chunks of C bits: chunks per wave (tm) and log2 claim slots (hbits).
 void rec_table_geometry(uint32_t C, int n, int* tm, int* hbits);
@@ -260,8 +265,12 @@ void launch_pframe(const PfArgs& a, int n, uint64_t* tile_scratch, hipStream_t s
 // P-frame decode, first half (Block.cpp:481-496): every macroblock's motion vector read from the
 // stream words (big-endian bytes) at start_bit, the previous decoded frame's block at the clamped
 // vector copied into place
-void launch_pframe_mvcopy(const uint8_t* stream, uint64_t start_bit, int mv_bits, const uint8_t* ref, uint64_t rs,
-                          uint8_t* out, uint64_t os, int w, int h, hipStream_t s);
+// gop decode: pos[0] = start, pos[1..n] = ~0 (no end yet), tot[0..n) = 0
+void launch_gop_init(uint64_t* pos, uint64_t* tot, int n, uint64_t start, hipStream_t s);
+// dstart non-null: the vectors start at *dstart (device, an earlier launch's end bit) in place of
+// start_bit; a macroblock whose vector lies past nbits copies nothing (the caller reports it)
+void launch_pframe_mvcopy(const uint8_t* stream, uint64_t start_bit, const uint64_t* dstart, uint64_t nbits, int mv_bits,
+                          const uint8_t* ref, uint64_t rs, uint8_t* out, uint64_t os, int w, int h, hipStream_t s);
 int pframe_tiles(int nb);    // tile_scratch entries
 
 }  // namespace ie

@@ -1560,6 +1560,11 @@ __device__ __forceinline__ uint32_t slot_tail32(const uint32_t* I, uint32_t n, u
     do {                                                                                                            \
         if (IE_PROFILE && a.stamps && lane == 0) a.stamps[size_t(t) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+// the chip-wide 100 MHz clock (comparable across CUs and XCDs) at the wave's start (14) and end (15)
+#define WRTSTAMP(i)                                                                                                 \
+    do {                                                                                                            \
+        if (IE_PROFILE && a.stamps && lane == 0) a.stamps[size_t(t) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
 __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
@@ -1583,6 +1588,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         t = int(blockIdx.x);
     }
     WSTAMP(0);
+    WRTSTAMP(14);
     asm volatile("; PHASE w0" ::: "memory");
     if (tid == 0) {  // the tile's FP64 task counters (IE_W_POOL): structural, whole-block
         misc[16] = 0u;
@@ -2021,8 +2027,10 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
 
     // ------------------------------------------------------------ store, slot by slot
     if (!(IE_W_DBG & 2) && Tw) {
-        const uint64_t excl = uint64_t(__builtin_amdgcn_readfirstlane(misc[8])) |
-                              (uint64_t(__builtin_amdgcn_readfirstlane(misc[9])) << 32);
+        // (readfirstlane returns int: zero-extend each half, or a prefix of 2^31 bits or more
+        // would sign-extend into the high word)
+        const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[8]))) |
+                              (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[9]))) << 32);
         const uint64_t Xw = start_bit + excl + W;
         const bool pend = __builtin_amdgcn_readfirstlane(misc[11]) != 0u;
         // the wave's first word is written by the previous wave (or, pending, later by this one)
@@ -2064,6 +2072,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
             }
         }
         WSTAMP(10);
+        WRTSTAMP(15);
     asm volatile("; PHASE w10" ::: "memory");
     }
 }

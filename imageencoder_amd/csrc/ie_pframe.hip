@@ -421,12 +421,14 @@ __global__ void pf_end_kernel(const uint64_t* start, uint64_t* end, uint64_t hea
 }
 
 // P-frame decode, first half: lane l copies row l/4, pixels 4(l%4)..+3 of the reference block
-__global__ __launch_bounds__(kMbTPB) void pf_mvcopy_kernel(const uint8_t* in, uint64_t start_bit, int mv,
-                                                           const uint8_t* ref, uint64_t rs, uint8_t* out, uint64_t os,
-                                                           int w, int h, int mbx) {
+__global__ __launch_bounds__(kMbTPB) void pf_mvcopy_kernel(const uint8_t* in, uint64_t start_bit, const uint64_t* dstart,
+                                                           uint64_t nbits, int mv, const uint8_t* ref, uint64_t rs,
+                                                           uint8_t* out, uint64_t os, int w, int h, int mbx) {
     const int l = threadIdx.x, mb = blockIdx.x;
     const int mx = (mb % mbx) * kMB, my = (mb / mbx) * kMB;
+    if (dstart) start_bit = min(*dstart, nbits);
     const uint64_t p = start_bit + uint64_t(mb) * 2u * uint32_t(mv);
+    if (p + 2u * uint32_t(mv) > nbits) return;  // (a truncated stream: the host reports it)
     uint64_t win = 0;  // 64 stream bits from byte p/8 (2*mv <= 32 bits + 7 bits of offset)
 #pragma unroll
     for (int k = 0; k < 8; k++) win = (win << 8) | in[(p >> 3) + k];
@@ -445,12 +447,12 @@ __global__ __launch_bounds__(kMbTPB) void pf_mvcopy_kernel(const uint8_t* in, ui
 
 }  // namespace
 
-void launch_pframe_mvcopy(const uint8_t* stream, uint64_t start_bit, int mv_bits, const uint8_t* ref, uint64_t rs,
-                          uint8_t* out, uint64_t os, int w, int h, hipStream_t s) {
+void launch_pframe_mvcopy(const uint8_t* stream, uint64_t start_bit, const uint64_t* dstart, uint64_t nbits, int mv_bits,
+                          const uint8_t* ref, uint64_t rs, uint8_t* out, uint64_t os, int w, int h, hipStream_t s) {
     const int nmb = (w / kMB) * (h / kMB);
     if (nmb > 0)
-        hipLaunchKernelGGL(pf_mvcopy_kernel, dim3(nmb), dim3(kMbTPB), 0, s, stream, start_bit, mv_bits, ref, rs, out, os,
-                           w, h, w / kMB);
+        hipLaunchKernelGGL(pf_mvcopy_kernel, dim3(nmb), dim3(kMbTPB), 0, s, stream, start_bit, dstart, nbits, mv_bits, ref,
+                           rs, out, os, w, h, w / kMB);
 }
 
 void launch_pframe(const PfArgs& a, int n, uint64_t* tsum, hipStream_t s) {

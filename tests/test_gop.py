@@ -187,6 +187,34 @@ def test_gpu_decode_gop_payload(codec, name, mc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("keep", [0.2, 0.5, 0.9, 0.999])
+def test_gpu_decode_gop_truncated(codec, keep):
+    """A truncated video payload fails with IE_EFORMAT (device-chained decode: the frames after the
+    cut read an end bit no frame wrote and stay within the stream), and the context decodes the
+    whole payload correctly afterwards."""
+    import torch
+    from imageencoder_amd import IEError
+    c = next(c for c in DEC if c["name"] == "gopP64x48x5_g3_m8")
+    q = O.read_matrix(c["matrix"], 4)
+    codec.set_quant(q, 4)
+    w, h = c["w"], c["h"]
+    f = c["dec1_size"] // (w * h * 3 // 2)
+    _, hb = O.load().header(4, q, c["rle"], w, h, video=True, frames=f, gop=c["gop"], merange=c["merange"])
+    enc = np.frombuffer(O.case_expected(c), dtype=np.uint8)
+    pitch = w * h * 3 // 2
+    cut = hb // 8 + int((enc.size - hb // 8) * keep)
+    out = torch.full((f * pitch,), 0x80, dtype=torch.uint8, device="cuda")
+    with pytest.raises(IEError, match="stream ends"):
+        codec.decode_gop(torch.from_numpy(enc[:cut].copy()).cuda(), w, h, out, c["gop"], c["merange"], f,
+                         start_bit=hb, frame_pitch=pitch, rle=bool(c["rle"]), motioncomp=True)
+    out.fill_(0x80)
+    end = codec.decode_gop(torch.from_numpy(enc.copy()).cuda(), w, h, out, c["gop"], c["merange"], f, start_bit=hb,
+                           frame_pitch=pitch, rle=bool(c["rle"]), motioncomp=True)
+    assert (end + 7) // 8 == enc.size
+    assert hashlib.md5(out.cpu().numpy().tobytes()).hexdigest() == c["dec1_md5"]
+
+
+@pytest.mark.gpu
 def test_gpu_gop_roundtrip_1080_multiple_of_16(codec):
     """Encode a 1920x1088 panning video with P-frames on the GPU, decode it on the GPU: the oracle's
     decode of the same file (parity pinned by the goldens above at small sizes)."""

@@ -186,6 +186,33 @@ def test_fast_equals_exact_large(codec, n, matrix):
         assert torch.equal(a[: (ea + 7) // 8], b[: (eb + 7) // 8])
 
 
+def test_chain_prefix_beyond_2_31_bits(codec):
+    """One concatenated launch whose tiles sit more than 2^31 and 2^32 bits into the stream: 96
+    4K noise frames (~5.4e9 bits) in ONE ie_encode_frames launch == the same frames in four
+    launches of 24 chained by start_bit (each chain's own prefix below 2^31 bits).  A tile's
+    64-bit position once passed through a sign-extending 32-bit half (readfirstlane returns int):
+    a prefix of 2^31 bits or more turned into an address past the device's aperture."""
+    import torch
+    from imageencoder_amd import stream_bound
+    q = O.read_matrix("matrix.txt", 4)
+    codec.set_quant(q, 4)
+    w, h, f, k = 3840, 2160, 96, 24
+    y = synth.uniform_device(w, h, f, synth.DEFAULT_SEED + 31, "cuda", torch)
+    cap = stream_bound(w, h, 4, f, 165)
+    a = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    fa, ea = codec.encode_frames(y, w, h, a, start_bit=165, nframes=f)
+    assert ea > (1 << 32)
+    b = torch.zeros_like(a)
+    e, fb = 165, []
+    for i in range(0, f, k):
+        fi, ei = codec.encode_frames(y[i:i + k], w, h, b, start_bit=e, nframes=k)
+        assert ei - e < (1 << 31)
+        fb.append(fi)
+        e = ei
+    assert ea == e and np.array_equal(fa, np.concatenate(fb))
+    assert torch.equal(a[: (ea + 7) // 8], b[: (e + 7) // 8])
+
+
 def test_random_noise_stress(codec, oracle):
     """Uniform random bytes from numpy's generator (not the splitmix frames) against the oracle."""
     from imageencoder_amd import stream_bound

@@ -1,4 +1,4 @@
-"""One C2-shaped launch (16 4K uniform-noise frames) with IE_STAMPS set (run with IE_LIB = an
+"""One C2-shaped launch (NF 4K uniform-noise frames, default 16) with IE_STAMPS set (run with IE_LIB = an
 IE_PROFILE build): writes the per-tile stamps file named by IE_STAMPS."""
 import os
 import sys
@@ -9,7 +9,7 @@ import torch  # noqa: E402
 from imageencoder_amd import Codec, stream_bound, synth  # noqa: E402
 from tests import oracle_lib as O  # noqa: E402
 
-w, h, nf = 3840, 2160, 16
+w, h, nf = 3840, 2160, int(os.environ.get("NF", "16"))
 c = Codec(0, O.read_matrix("matrix.txt", 4), 4)
 y = synth.uniform_device(w, h, nf, 3, "cuda", torch)
 pitch = (stream_bound(w, h, 4, 1, 165) + 255) // 256 * 256

@@ -23,6 +23,13 @@ for i, nm in enumerate(names):
           f"{np.percentile(d[:, i], 90):7.3f}")
 life = (rows[:, -1] - rows[:, 0]) / ghz / 1e3
 print(f"wave lifetime mean {life.mean():.2f} us  p50 {np.median(life):.2f}")
+rt = w16.reshape(-1, 16)[:, 14:16]
+rt = rt[(rt > 0).all(axis=1)]
+if len(rt):  # chip-wide 100 MHz clock: starts and ends across the launch
+    st = (rt[:, 0] - rt[:, 0].min()) / 100.0
+    en = (rt[:, 1] - rt[:, 0].min()) / 100.0
+    print(f"launch span {en.max():.2f} us: wave starts p50 {np.median(st):.2f} p90 {np.percentile(st, 90):.2f} "
+          f"max {st.max():.2f}; ends p50 {np.median(en):.2f} p90 {np.percentile(en, 90):.2f}")
 fx = w16.reshape(-1, 16)[:, [2, 11, 12, 13, 3]]
 fx = fx[(fx > 0).all(axis=1)]
 if len(fx):
