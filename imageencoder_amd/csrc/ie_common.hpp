@@ -253,6 +253,38 @@ __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_
     }
 }
 
+// One probe window's share of a look-back (predecessors d0 .. d0 + width - 1 of the tile, as probe
+// p read them): found -- the nearest inclusive prefix (or the chain start) lies in the window;
+// sum -- the values up to and including it (the whole window's aggregates when not found);
+// ready -- every value summed was published.  Every lane gets the result.
+struct WinSum {
+    uint64_t sum;
+    bool found, ready;
+};
+__device__ __forceinline__ WinSum window_sum(const Probe& p, int chain_pos, int d0, int width, uint32_t tag) {
+    const int lane = lane_id(), d = d0 + lane;
+    int status = 2;  // before the chain start: a virtual inclusive prefix of 0
+    uint64_t val = 0;
+    if (lane >= width) {
+        status = 3;
+    } else if (chain_pos - 1 - d >= 0) {
+        if (uint32_t(p.gi >> 56) == tag) {
+            val = p.gi & kMask56;
+        } else {
+            status = (uint32_t(p.ga >> 56) == tag) ? 1 : 0;
+            val = p.ga & kMask56;
+        }
+    }
+    const uint64_t incl = __ballot(status == 2);
+    const int dP = incl ? (__ffsll((unsigned long long)incl) - 1) : width;
+    const uint64_t upto = (dP < 64) ? ((2ull << dP) - 1ull) : ~0ull;  // lanes 0 .. dP
+    WinSum r;
+    r.ready = !(__ballot(status == 0) & upto);
+    r.sum = wave_sum64((lane <= dP && lane < width) ? val : 0ull);
+    r.found = dP < width;
+    return r;
+}
+
 // The tail granule of tile idx (one thread).
 __device__ __forceinline__ uint32_t wait_tail(const uint64_t* st, int idx, uint32_t tag, unsigned* err,
                                               unsigned* polls = nullptr) {

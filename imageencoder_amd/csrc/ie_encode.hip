@@ -1502,7 +1502,8 @@ __device__ __forceinline__ float round_block_lean4(const EncTables* __restrict__
 #endif
 constexpr int kWReg = 1024;  // words per wave region: [4 rows][256 blocks] pixels, then the two slot-pair images in turn
 constexpr int kWTask = 128;  // words per wave: fix-up tasks [64] + results [64]
-constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9] excl, [10] ptail, [11] tail pending, [12] ticket
+constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9] excl, [10] ptail, [11] tail pending, [12] ticket,
+                             // [16..17] FP64 task counters, [18..25] small-launch window sums, [26..29] their found flags
 constexpr int kWRows = 16 * 16 + 3 * 16;  // FP64 rows P[16][16], then S, rq, qd (doubles)
 constexpr int kWDelta = 256;  // IE_W_POOL 2: one word per lane of the tile, the FP64 fix-up's structural deltas
 constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc + kWDelta) * 4 + kWRows * 8;
@@ -1960,8 +1961,20 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         W += (w < wv) ? v : 0u;
     }
     if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);  // successors may resolve now
-    Probe pr{0, 0, 0};
-    if (wv == 0 && chain_pos != 0) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);  // in flight while emitting
+    // look-back probes, in flight while emitting.  A launch too small to fill the chip (deep_lb:
+    // its tiles reach their look-back together, so a tile's nearest inclusive prefix is far away):
+    // the four waves read predecessors [128 wv, 128 wv + 128) in two windows each -- 512 in one
+    // round trip; otherwise wave 0 reads the nearest kProbe0.
+    const bool deep = a.deep_lb != 0;
+    Probe pr{0, 0, 0}, pr2{0, 0, 0};
+    if (chain_pos != 0) {
+        if (deep) {
+            pr = probe_issue(a.st, t, chain_pos, step, 128 * wv, 64);
+            pr2 = probe_issue(a.st, t, chain_pos, step, 128 * wv + 64, 64);
+        } else if (wv == 0) {
+            pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
+        }
+    }
 
     // slot-pair images: slots 0 and 1, then slots 2 and 3, each pair as ONE bit image from word 0
     // of the wave's region (a pair holds <= 2 * 64 * 252 bits = 1008 words); emission takes
@@ -1991,6 +2004,31 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     // ------------------------------------------------------------ look-back (wave 0)
     const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
     uint32_t* const out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
+    if (deep && chain_pos != 0 && !(IE_W_DBG & 16)) {
+        // every wave sums its two windows (read again until every value it needs is published;
+        // its predecessors never wait on this tile) for wave 0 to combine
+        WinSum r0, r1;
+        unsigned spins = 0;
+        for (;;) {
+            r0 = window_sum(pr, chain_pos, 128 * wv, 64, a.tag);
+            r1 = window_sum(pr2, chain_pos, 128 * wv + 64, 64, a.tag);
+            if (r0.ready && (r0.found || r1.ready)) break;
+            if (++spins > kSpinLimit) {
+                if (lane == 0) atomicAdd(&a.err[0], 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            pr = probe_issue(a.st, t, chain_pos, step, 128 * wv, 64);
+            pr2 = probe_issue(a.st, t, chain_pos, step, 128 * wv + 64, 64);
+        }
+        if (lane == 0) {
+            const uint64_t sm = r0.sum + (r0.found ? 0ull : r1.sum);
+            misc[18 + 2 * wv] = uint32_t(sm);
+            misc[19 + 2 * wv] = uint32_t(sm >> 32);
+            misc[26 + wv] = (r0.found || r1.found) ? 1u : 0u;
+        }
+        lds_barrier();
+    }
     if (wv == 0) {
         uint64_t excl = 0;
         uint32_t ptail = 0, pend = 0;
@@ -2002,7 +2040,22 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
             excl = uint64_t(tif) * 110000u;
             if (lane == 0) publish(a.st, t, 1, a.tag, excl + A);
         } else {
-            excl = lookback_wave<IE_W_AHEAD>(pr, a.st, t, chain_pos, step, a.tag, a.err, nullptr, a.deep_lb != 0);
+            bool done = false;
+            if (deep) {  // the waves' sums in predecessor order, up to the first window with an inclusive prefix
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    if (!done) {
+                        excl += uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[18 + 2 * w]))) |
+                                (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[19 + 2 * w]))) << 32);
+                        done = __builtin_amdgcn_readfirstlane(misc[26 + w]) != 0;
+                    }
+                }
+                if (!done) excl = 0;  // more than 512 predecessors back: the wave-0 walk from the start
+            }
+            if (!done) {
+                const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr;
+                excl = lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
+            }
             const bool have = uint32_t(pr.gt >> 56) == a.tag;  // (lane 0's probe read the tail)
             const bool split = ((start_bit + excl) & 31) != 0;
             ptail = have ? uint32_t(pr.gt) : 0u;
