@@ -457,7 +457,7 @@ Geometry geometry(int w, int h, int n, int nframes, int bpt = 0) {
     g.by = h / n;
     g.gpr = (g.bx + bpt - 1) / bpt;
     g.gpf = g.gpr * g.by;
-    const int tpt = ie::encode_threads_per_tile();
+    const int tpt = ie::encode_threads_per_tile();  // groups per tile
     g.tpf = (g.gpf + tpt - 1) / tpt;
     g.ntiles = g.tpf * nframes;
     return g;
@@ -501,7 +501,6 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     const bool vec_ok = (reinterpret_cast<uintptr_t>(L.dy) % size_t(bpt * c->n) == 0) &&
                         (L.stride % (bpt * c->n) == 0) && (L.nframes == 1 || L.frame_pitch % (bpt * c->n) == 0);
     int r;
-    if ((r = prepare_state(c, g.ntiles, L.nframes))) return r;
     ie::EncArgs a{};
     a.y = L.dy;
     a.stride = L.stride;
@@ -526,15 +525,6 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     a.out_pitch_words = L.segmented ? L.out_pitch / 4 : 0;
     a.start_bit = L.start_bit;
     a.start_dev = L.start_dev;
-    a.st = c->d_state;
-    a.ticket = c->use_ticket ? c->d_ticket : nullptr;
-    a.ticket_base = c->ticket_base;
-    a.tag = c->tag;
-    a.frame_start = c->d_frame_start;
-    a.chain_end = L.chain_end ? L.chain_end : c->d_chain_end;
-    a.err = c->d_err;
-    a.wave_fix = c->d_wave_fix;
-    c->last_fix_words = (L.mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
     a.tab = c->d_tab;
     a.rec_bits = c->h_tab->rec_bits;
     a.tri = (c->n == 4 && (a.rec_bits - 4) / 17 <= 10) ? 1 : 0;  // bl_max = (rec_bits - 4) / (1 + N*N); 3 bl <= 30
@@ -543,7 +533,6 @@ int launch_chain(ie_ctx* c, const Launch& L) {
 #endif
     a.coef = L.coef;
     a.hist = L.hist;
-    if (L.hist) HIPCHK(c, hipMemsetAsync(L.hist, 0, size_t(L.nframes) * 256 * sizeof(uint32_t), c->stream));
 #ifndef IE_PROFILE
 #define IE_PROFILE 0
 #endif
@@ -560,6 +549,17 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     const char* stamp_file = nullptr;
 #endif
     a.ablate = ablate | IE_ABLATE_FORCE;  // IE_ABLATE_FORCE: A/B builds of an ablation
+    if ((r = prepare_state(c, g.ntiles, L.nframes))) return r;
+    a.st = c->d_state;
+    a.ticket = c->use_ticket ? c->d_ticket : nullptr;
+    a.ticket_base = c->ticket_base;
+    a.tag = c->tag;
+    a.frame_start = c->d_frame_start;
+    a.chain_end = L.chain_end ? L.chain_end : c->d_chain_end;
+    a.err = c->d_err;
+    a.wave_fix = c->d_wave_fix;
+    c->last_fix_words = (L.mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
+    if (L.hist) HIPCHK(c, hipMemsetAsync(L.hist, 0, size_t(L.nframes) * 256 * sizeof(uint32_t), c->stream));
     uint64_t* d_stamps = nullptr;
     if (stamp_file) {
         HIPCHK(c, hipMalloc(&d_stamps, size_t(g.ntiles) * ie::kStamps * sizeof(uint64_t)));

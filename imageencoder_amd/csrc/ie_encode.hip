@@ -611,7 +611,7 @@ struct TileGeo {
     int nblk, byi, bx0;  // blocks of this thread's group (nblk = 0: none)
 };
 
-template <int N, int BPT = Geo<N>::BPT>
+template <int N, int BPT = Geo<N>::BPT, int TG = kEncTPB>
 __device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
     TileGeo g;
     // Independent images interleave their tiles (frame = t % nframes), so every frame's chain
@@ -629,7 +629,7 @@ __device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
     g.chain_pos = a.segmented ? g.tif : t;  // tiles before this one in its chain
     // group gi = base + tid: the division by gpr is split into a wave-uniform (scalar) part and a
     // per-lane remainder r < gpr + kEncTPB, divided by a multiply-high with ceil(2^32 / gpr)
-    const int base = g.tif * kEncTPB;
+    const int base = g.tif * TG;  // (TG groups per tile; tid: the thread's group within it)
     const int q0 = int(fdiv(uint32_t(base), a.div_gpr)), r0 = base - q0 * a.gpr;
     const uint32_t r = uint32_t(r0 + tid);
     const uint32_t dq = (a.gpr == 1) ? r : __umulhi(r, a.gpr_magic);  // (2^32 does not fit the magic)
@@ -1491,22 +1491,18 @@ __device__ __forceinline__ float round_block_lean4(const EncTables* __restrict__
 #ifndef IE_W_DBG
 #define IE_W_DBG 0
 #endif
-#ifndef IE_W_POOL
-#define IE_W_POOL 0  // 0: FP64 tasks compacted per wave; 2: one list per tile, structural results as 2-bit deltas
-#endif
 #ifndef IE_W_AHEAD
 #define IE_W_AHEAD 2  // look-back windows per round trip (each holds 4 VGPRs live beside slots 2-3)
 #endif
 #ifndef IE_W_WAVES
-#define IE_W_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD): 76 VGPRs, no scratch (7 spills with IE_W_POOL 0)
+#define IE_W_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD): 76 VGPRs, no scratch (7 spills)
 #endif
-constexpr int kWReg = 1024;  // words per wave region: [4 rows][256 blocks] pixels, then the two slot-pair images in turn
+constexpr int kWReg = 1024;  // words per wave region: [4 rows][64 NS blocks] pixels, then the slot-pair images in turn
 constexpr int kWTask = 128;  // words per wave: fix-up tasks [64] + results [64]
 constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9] excl, [10] ptail, [11] tail pending, [12] ticket,
                              // [16..17] FP64 task counters, [18..25] small-launch window sums, [26..29] their found flags
 constexpr int kWRows = 16 * 16 + 3 * 16;  // FP64 rows P[16][16], then S, rq, qd (doubles)
-constexpr int kWDelta = 256;  // IE_W_POOL 2: one word per lane of the tile, the FP64 fix-up's structural deltas
-constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc + kWDelta) * 4 + kWRows * 8;
+constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc) * 4 + kWRows * 8;
 
 // Inclusive scan over the 64 lanes of a wave by DPP row shifts and row broadcasts (six VALU).
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
@@ -1568,7 +1564,11 @@ __device__ __forceinline__ uint32_t slot_tail32(const uint32_t* I, uint32_t n, u
     } while (0)
 
 __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, const EncTables* __restrict__ tab) {
+    // (two slots per lane -- twice the tiles for small launches -- measured slower on a lone 4K
+    // frame, 23.9 against 18.2 us: the phases are bound by the SIMDs' issue, not by one wave's
+    // latency, and twice the tiles lengthen the look-back)
     constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
+    constexpr int GW = 16 * NS, BW = 64 * NS, TG = 4 * GW;  // groups / blocks per wave, groups per tile
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar registers
@@ -1576,8 +1576,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     uint32_t* const task = smem + 4 * kWReg + wv * kWTask;
     uint32_t* const res = task + 64;
     uint32_t* const misc = smem + 4 * kWReg + 4 * kWTask;
-    uint32_t* const sdelta = misc + kWMisc;  // [4 waves][64 lanes]
-    double* const srow = reinterpret_cast<double*>(sdelta + kWDelta);
+    double* const srow = reinterpret_cast<double*>(misc + kWMisc);
 
     int t;
     if (a.ticket) {
@@ -1591,27 +1590,24 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     WSTAMP(0);
     WRTSTAMP(14);
     asm volatile("; PHASE w0" ::: "memory");
-    if (tid == 0) {  // the tile's FP64 task counters (IE_W_POOL): structural, whole-block
-        misc[16] = 0u;
-        misc[17] = 0u;
-    }
     // every coefficient's FP64 row and its S, rq, qd: the fix-up reads them from LDS
     for (int i = tid; i < kWRows; i += TPB)
         srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
                 : (i < NN * NN + 2 * NN) ? tab->rq[i - NN * NN - NN] : tab->qd[i - NN * NN - 2 * NN];
-    const TileGeo g = tile_geo<4, 4>(a, t, tid);
+    const TileGeo g = tile_geo<4, 4, TG>(a, t, tid);  // lane l of wave w: group 64 w + l of the tile
     const uint64_t start_bit = a.start_dev ? *a.start_dev : a.start_bit;
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     // groups in this tile / in this wave (>= 8 per tile: launch precondition)
-    const int ng = min(TPB, a.groups_per_frame - tif * TPB);
-    const int nbw = 4 * min(64, max(0, ng - 64 * wv));  // blocks of this wave
-    const int wlast = (ng - 1) >> 6;                    // the tile's last non-empty wave
+    const int ng = min(TG, a.groups_per_frame - tif * TG);
+    const int nbw = 4 * min(GW, max(0, ng - GW * wv));  // blocks of this wave
+    const int wlast = (ng - 1) / GW;                    // the tile's last non-empty wave
     if (!(IE_W_DBG & 64) && g.nblk) {
+        // pixel row r of the wave's block j at reg[r BW + j]: a lane's 16 bytes are its group's row
         const uint8_t* base = a.y + size_t(frame) * a.frame_pitch + size_t(g.byi) * N * a.stride + size_t(g.bx0) * N;
 #pragma unroll
         for (int r = 0; r < N; r++)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
-                                             (__attribute__((address_space(3))) void*)(reg + r * 256), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, 0);
     }
     lds_barrier();                                            // srow visible (the pixel DMA stays in flight)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
@@ -1626,7 +1622,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         __builtin_amdgcn_sched_barrier(0);
         uint32_t rows[N][1];
 #pragma unroll
-        for (int r = 0; r < N; r++) rows[r][0] = reg[r * 256 + 64 * b + lane];
+        for (int r = 0; r < N; r++) rows[r][0] = reg[r * BW + 64 * b + lane];
         float x[NN];
         block_pixels<N, 1>(rows, 0, x);
         uint32_t sf;
@@ -1653,161 +1649,15 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     WSTAMP(2);
     asm volatile("; PHASE w2" ::: "memory");
     // ------------------------------------------------------------ FP64 fix-up
-    if constexpr (IE_W_POOL) {
-        // One task list for the whole tile (IE_W_POOL): every flagged coefficient -- structural s
-        // of slot b, or all 16 of a whole-block request -- takes a slot from an LDS counter, and
-        // the tile's waves evaluate 64 tasks per wave-round: about two FP64 rounds per tile
-        // instead of one or two per wave.  Task word: wave << 12 | lane << 6 | slot << 4 | k; the
-        // evaluating lane overwrites it with the result.  Passes of kWPoolCap tasks (the per-wave
-        // task areas, pooled) keep any count bounded.
-        constexpr uint32_t kWPoolCap = 4 * kWTask;
-        uint32_t* const pool = smem + 4 * kWReg;
-        // structural tasks first (one counter), then whole-block requests in groups of 16 from a
-        // 16-aligned start (another counter), so that no group straddles a window
-        const uint32_t sfl = flags & 0x7777u, wfl = flags & 0x8888u;
-        const uint32_t ns = uint32_t(__popc(sfl)), nwb = uint32_t(__popc(wfl));
-        uint32_t sbase = 0, wbase = 0;
-        if (ns) sbase = atomicAdd(&misc[16], ns);  // (LDS atomics with return)
-        if (nwb) wbase = atomicAdd(&misc[17], nwb);
-        if constexpr (IE_W_POOL == 2) sdelta[wv * 64 + lane] = 0u;
-        lds_barrier();
-        const uint32_t nstruct = __builtin_amdgcn_readfirstlane(misc[16]);
-        const uint32_t wb0 = (nstruct + 15u) & ~15u;
-        const uint32_t total = wb0 + 16u * __builtin_amdgcn_readfirstlane(misc[17]);
-        for (uint32_t w0 = 0; w0 < total; w0 += kWPoolCap) {  // (uniform)
-            // this lane's tasks in the window [w0, w0 + cap): same order as the patch below
-            // (unsigned offsets: a task before the window wraps to a huge i, and counting on wraps
-            // it back to the right place in a later window)
-            if (flags) {
-                uint32_t i = sbase - w0, j = wb0 + 16u * wbase - w0;
-                uint32_t own = (uint32_t(wv) << 12) | (uint32_t(lane) << 6);
-                asm volatile("" : "+v"(own));  // (opaque per window: keeps the task words from being hoisted)
-#pragma unroll
-                for (int b = 0; b < NS; b++) {
-                    const uint32_t tb = own | (uint32_t(b) << 4);
-#pragma unroll
-                    for (int ss = 0; ss < 3; ss++)
-                        if ((sfl >> (4 * b + ss)) & 1u) {
-                            if (i < kWPoolCap) {
-                                if constexpr (IE_W_POOL == 2)  // wave, lane, slot, s, and the FP32 value (high half)
-                                    pool[i] = (own >> 2) | (uint32_t(b) << 2) | uint32_t(ss) |
-                                              (zp[b][Structural<N>::zpos(ss) >> 1] & 0xFFFF0000u);
-                                else
-                                    pool[i] = tb | uint32_t(Structural<N>::k[ss]);
-                            }
-                            i++;
-                        }
-                    if ((wfl >> (4 * b + 3)) & 1u) {
-                        if (j < kWPoolCap)
-                            for (uint32_t k = 0; k < 16u; k++) pool[j + k] = tb | k | 0x4000u;
-                        j += 16u;
-                    }
-                }
-            }
-            lds_barrier();  // tasks written; every wave's pixels are in LDS (each waited for its DMA)
-            if (w0 == 0) WSTAMP(11);
-            const uint32_t nwin = min(kWPoolCap, total - w0);
-            for (uint32_t r = uint32_t(wv) * 64u; r < nwin; r += 256u) {  // (uniform per wave)
-                const uint32_t gi = w0 + r + uint32_t(lane);  // the task's index in the tile's list
-                if (r + uint32_t(lane) >= nwin || (gi >= nstruct && gi < wb0)) {
-                    // past the window, or the padding before the 16-aligned whole-block groups: no task
-                } else if (IE_W_POOL == 2 && gi < nstruct) {
-                    // structural task: the FP64 value's difference from the owner's FP32 rounding
-                    // (-1, 0 or +1: both round a value within the FP32 bound of a tie) goes into the
-                    // owner's delta word as 2 bits at 6 * slot + 2 * s
-                    const uint32_t tk = pool[r + lane];
-                    const int ss = int(tk & 3u), b = int((tk >> 2) & 3u), ol = int((tk >> 4) & 63u);
-                    const int ow = int((tk >> 10) & 3u);
-                    const int k = Structural<N>::k[0] * (ss == 0) + Structural<N>::k[1] * (ss == 1) + Structural<N>::k[2] * (ss == 2);
-                    const uint32_t* opx = smem + ow * kWReg + 64 * b + ol;
-                    const int y1 = (IE_W_DBG & 128) ? int(int16_t(tk >> 16)) + int(opx[0] & 1u)  // profiling: no FP64
-                                                    : exact_coef_rows4(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                                       srow[NN * NN + 2 * NN + k], opx);
-                    const uint32_t d = uint32_t(y1 - int(int16_t(tk >> 16))) & 3u;
-                    if (d) atomicOr(&sdelta[ow * 64 + ol], d << (6 * b + 2 * ss));
-                } else {
-                    const uint32_t tk = pool[r + lane];
-                    const int k = int(tk & 15u), b = int((tk >> 4) & 3u), ol = int((tk >> 6) & 63u);
-                    const int ow = int((tk >> 12) & 3u);
-                    const uint32_t* opx = smem + ow * kWReg + 64 * b + ol;  // the owner's pixel rows, 256 words apart
-                    const uint32_t v = (IE_W_DBG & 128) ? (opx[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
-                                     : uint32_t(exact_coef_rows4(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                                 srow[NN * NN + 2 * NN + k], opx)) & 0xFFFFu;
-                    if (tk & 0x4000u) {
-                        // whole-block group (16-aligned, inside this wave's round, every task word
-                        // read above): the result as int16 at its zig-zag place of the group's
-                        // first 32 bytes -- the owner reads its block back as 8 packed words
-                        constexpr uint64_t kPos = 0xFEA9DB83C7426510ull;  // ZigZagInv<4>::pos, a nibble each
-                        const uint32_t zpos = uint32_t(kPos >> (4 * k)) & 15u;
-                        reinterpret_cast<uint16_t*>(pool + ((r + lane) & ~15u))[zpos] = uint16_t(v);
-                    } else {
-                        pool[r + lane] = v;
-                    }
-                }
-            }
-            if (w0 == 0) WSTAMP(12);
-            lds_barrier();  // results in place
-            if (w0 == 0) WSTAMP(13);
-            if constexpr (IE_W_POOL == 2) {
-                if (__ballot(sfl != 0) && w0 + kWPoolCap >= total) {  // (after the last window)
-                    // branch-free: every structural coefficient += its 2-bit delta (0 unless the
-                    // FP64 evaluation rounded it otherwise), as int16 in the high half of its word
-                    const uint32_t dw = sdelta[wv * 64 + lane];
-#pragma unroll
-                    for (int b = 0; b < NS; b++)
-#pragma unroll
-                        for (int ss = 0; ss < 3; ss++) {
-                            const int zw = Structural<N>::zpos(ss) >> 1;  // (high halves, see below)
-                            const int d = __builtin_amdgcn_sbfe(int(dw), 6 * b + 2 * ss, 2);
-                            zp[b][zw] = uint32_t(d << 16) + zp[b][zw];
-                        }
-                }
-            } else if (sfl) {
-                uint32_t i = sbase - w0;
-#pragma unroll
-                for (int b = 0; b < NS; b++) {
-#pragma unroll
-                    for (int ss = 0; ss < 3; ss++)
-                        if ((sfl >> (4 * b + ss)) & 1u) {
-                            const int zw = Structural<N>::zpos(ss) >> 1;  // (high halves, see below)
-                            if (i < kWPoolCap) zp[b][zw] = __builtin_amdgcn_perm(pool[i], zp[b][zw], 0x05040100u);
-                            i++;
-                        }
-                }
-            }
-            if (__ballot(wfl != 0)) {
-                // whole blocks: the 8 packed words the evaluators assembled, taken by selects (a
-                // conditional overwrite of the packed registers costs spills at this occupancy)
-                uint32_t j = wb0 + 16u * wbase - w0;
-#pragma unroll
-                for (int b = 0; b < NS; b++) {
-                    const bool hit = ((wfl >> (4 * b + 3)) & 1u) && j < kWPoolCap;
-                    const uint32_t* src = pool + (hit ? j : 0u);
-                    const u32x4 v0 = *reinterpret_cast<const u32x4*>(src);
-                    const u32x4 v1 = *reinterpret_cast<const u32x4*>(src + 4);
-                    zp[b][0] = hit ? v0.x : zp[b][0];
-                    zp[b][1] = hit ? v0.y : zp[b][1];
-                    zp[b][2] = hit ? v0.z : zp[b][2];
-                    zp[b][3] = hit ? v0.w : zp[b][3];
-                    zp[b][4] = hit ? v1.x : zp[b][4];
-                    zp[b][5] = hit ? v1.y : zp[b][5];
-                    zp[b][6] = hit ? v1.z : zp[b][6];
-                    zp[b][7] = hit ? v1.w : zp[b][7];
-                    j += ((wfl >> (4 * b + 3)) & 1u) ? 16u : 0u;
-                }
-            }
-            if (w0 + kWPoolCap < total) lds_barrier();  // the next window rewrites the list
-        }
-    }
     static_assert(Structural<4>::zpos(0) & Structural<4>::zpos(1) & Structural<4>::zpos(2) & 1,
                   "4x4 structural coefficients sit in high halves of the packed words");
     auto block_px = [&](int b, int owner) {
         BlockPx<N> px;
 #pragma unroll
-        for (int r = 0; r < N; r++) px.w[r] = reg[r * 256 + 64 * b + owner];
+        for (int r = 0; r < N; r++) px.w[r] = reg[r * BW + 64 * b + owner];
         return px;
     };
-    if (!IE_W_POOL && !(IE_W_DBG & 1) && __ballot(flags != 0)) {
+    if (!(IE_W_DBG & 1) && __ballot(flags != 0)) {
         const uint32_t sf = flags & 0x7777u;
         const uint32_t cnt = __popc(sf);
         uint32_t pre = 0, total = 0;
@@ -1911,7 +1761,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     asm volatile("; PHASE w3" ::: "memory");
     // ------------------------------------------------------------ sizing + the wave's offsets
     uint32_t blw[NS], rb[NS];
-    const uint32_t k0 = uint32_t(tif * TPB + 64 * wv) * 4u;  // the wave's first block (frame raster order)
+    const uint32_t k0 = uint32_t(tif * TG + GW * wv) * 4u;  // the wave's first block (frame raster order)
 #pragma unroll
     for (int b = 0; b < NS; b++) {
         const bool valid = 64 * b + lane < nbw;
@@ -1963,16 +1813,19 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);  // successors may resolve now
     // look-back probes, in flight while emitting.  A launch too small to fill the chip (deep_lb:
     // its tiles reach their look-back together, so a tile's nearest inclusive prefix is far away):
-    // the four waves read predecessors [128 wv, 128 wv + 128) in two windows each -- 512 in one
-    // round trip; otherwise wave 0 reads the nearest kProbe0.
+    // the four waves read predecessors [64 DW wv, 64 DW (wv + 1)) in DW windows each -- 256 DW in
+    // one round trip; otherwise wave 0 reads the nearest kProbe0.
+    constexpr int DW = 2;
     const bool deep = a.deep_lb != 0;
-    Probe pr{0, 0, 0}, pr2{0, 0, 0};
+    Probe pr[DW];
+#pragma unroll
+    for (int i = 0; i < DW; i++) pr[i] = Probe{0, 0, 0};
     if (chain_pos != 0) {
         if (deep) {
-            pr = probe_issue(a.st, t, chain_pos, step, 128 * wv, 64);
-            pr2 = probe_issue(a.st, t, chain_pos, step, 128 * wv + 64, 64);
+#pragma unroll
+            for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
         } else if (wv == 0) {
-            pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
+            pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
         }
     }
 
@@ -2005,27 +1858,38 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
     uint32_t* const out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
     if (deep && chain_pos != 0 && !(IE_W_DBG & 16)) {
-        // every wave sums its two windows (read again until every value it needs is published;
-        // its predecessors never wait on this tile) for wave 0 to combine
-        WinSum r0, r1;
+        // every wave sums its windows in order, up to the first with an inclusive prefix (read
+        // again until every value it needs is published; its predecessors never wait on this
+        // tile), for wave 0 to combine
+        uint64_t sm = 0;
+        bool found = false;
         unsigned spins = 0;
         for (;;) {
-            r0 = window_sum(pr, chain_pos, 128 * wv, 64, a.tag);
-            r1 = window_sum(pr2, chain_pos, 128 * wv + 64, 64, a.tag);
-            if (r0.ready && (r0.found || r1.ready)) break;
+            bool ready = true;
+            sm = 0;
+            found = false;
+#pragma unroll
+            for (int i = 0; i < DW; i++) {
+                const WinSum r = window_sum(pr[i], chain_pos, 64 * (DW * wv + i), 64, a.tag);
+                if (!found) {
+                    ready = ready && r.ready;
+                    sm += r.sum;
+                    found = r.found;
+                }
+            }
+            if (ready) break;
             if (++spins > kSpinLimit) {
                 if (lane == 0) atomicAdd(&a.err[0], 1u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
-            pr = probe_issue(a.st, t, chain_pos, step, 128 * wv, 64);
-            pr2 = probe_issue(a.st, t, chain_pos, step, 128 * wv + 64, 64);
+#pragma unroll
+            for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
         }
         if (lane == 0) {
-            const uint64_t sm = r0.sum + (r0.found ? 0ull : r1.sum);
             misc[18 + 2 * wv] = uint32_t(sm);
             misc[19 + 2 * wv] = uint32_t(sm >> 32);
-            misc[26 + wv] = (r0.found || r1.found) ? 1u : 0u;
+            misc[26 + wv] = found ? 1u : 0u;
         }
         lds_barrier();
     }
@@ -2050,15 +1914,15 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                         done = __builtin_amdgcn_readfirstlane(misc[26 + w]) != 0;
                     }
                 }
-                if (!done) excl = 0;  // more than 512 predecessors back: the wave-0 walk from the start
+                if (!done) excl = 0;  // more than 256 DW predecessors back: the wave-0 walk from the start
             }
             if (!done) {
-                const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr;
+                const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr[0];
                 excl = lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
             }
-            const bool have = uint32_t(pr.gt >> 56) == a.tag;  // (lane 0's probe read the tail)
+            const bool have = uint32_t(pr[0].gt >> 56) == a.tag;  // (lane 0's probe read the tail)
             const bool split = ((start_bit + excl) & 31) != 0;
-            ptail = have ? uint32_t(pr.gt) : 0u;
+            ptail = have ? uint32_t(pr[0].gt) : 0u;
             pend = (!have && split) ? 1u : 0u;
         }
         if (lane == 0) {
