@@ -51,6 +51,18 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
+// Inclusive minimum over lanes 0..l of a wave by DPP row shifts and row broadcasts (six VALU, no
+// LDS): lanes a shift reads from outside the wave keep their own value.
+__device__ __forceinline__ uint32_t wave_incl_min_dpp(uint32_t v) {
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(int(~0u), int(v), 0x111, 0xF, 0xF, false)));  // row_shr:1
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(int(~0u), int(v), 0x112, 0xF, 0xF, false)));  // row_shr:2
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(int(~0u), int(v), 0x114, 0xF, 0xF, false)));  // row_shr:4
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(int(~0u), int(v), 0x118, 0xF, 0xF, false)));  // row_shr:8
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(int(~0u), int(v), 0x142, 0xA, 0xF, false)));  // row_bcast:15
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(int(~0u), int(v), 0x143, 0xC, 0xF, false)));  // row_bcast:31
+    return v;
+}
+
 // Exclusive workgroup scan of per-thread bit counts (TPB threads).  scratch: >= TPB/64 words of
 // LDS.  Returns the thread's exclusive offset; *total receives the workgroup sum.
 template <int TPB = kTPB>

@@ -533,19 +533,26 @@ __device__ __forceinline__ int stage_words16(uint32_t* L, const uint32_t* W, uin
 // chunk's end).  Results: a walk that merged takes its owner's exit (owner chains are read-only
 // chases; only non-roots are written).  The valid-header bitmap comes 32 positions at a time from
 // bitwise operations on shifted windows (valid_mask32, ie_recbits.h).
+// The first valid position at or after p before ce (ce: a chunk end, a multiple of 32), else ce.
+// NZ[i]: the first bitmap word at or after word i holding a valid position (a sentinel past the
+// last), so a run of positions where no record can start costs one read, not one per word.
 template <int N>
-__device__ __forceinline__ uint32_t next_valid(const uint32_t* VB, uint32_t p, uint32_t ce) {
+__device__ __forceinline__ uint32_t next_valid(const uint32_t* VB, const uint16_t* NZ, uint32_t p, uint32_t ce) {
     if (p >= ce) return p;
     uint32_t wi = p >> 5, msk = VB[wi] & (0xFFFFFFFFu << (p & 31u));
-    const uint32_t wend = ce >> 5;
-    while (!msk && ++wi < wend) msk = VB[wi];
-    return msk ? (wi << 5) + uint32_t(__builtin_ctz(msk)) : ce;
+    if (!msk) {
+        wi = NZ[wi + 1];
+        if (wi >= (ce >> 5)) return ce;
+        msk = VB[wi];
+    }
+    return (wi << 5) + uint32_t(__builtin_ctz(msk));
 }
 
 __host__ __device__ constexpr int rec_table2_words(uint32_t C, int D, int tm, int hbits) {
-    // L (stream words, 16-byte aligned staging: +4), VB, claims, then u16 res / tgt and u32 walk list
+    // L (stream words, 16-byte aligned staging: +4), VB, claims, then u16 res / tgt, the u32 walk
+    // list and the u16 next-valid-word table (tm CW + 1 entries)
     return (rec_table_stream_words(uint32_t(tm) * C) + 4 + 3) / 4 * 4 + tm * int(C >> 5) + (1 << hbits) +
-           2 * tm * (D + 1);
+           2 * tm * (D + 1) + (tm * int(C >> 5) + 2) / 2;
 }
 
 template <int N>
@@ -573,6 +580,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     uint16_t* res = reinterpret_cast<uint16_t*>(H + HM + 1);
     uint16_t* tgt = res + tm * D1;
     uint32_t* wl = H + HM + 1 + tm * D1;  // after res + tgt (tm * D1 words together)
+    uint16_t* NZ = reinterpret_cast<uint16_t*>(wl + tm * D1);
     const RecSpan sp = rec_span(a);
     const uint64_t c0 = sp.start + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
@@ -597,6 +605,19 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
             if (cut < 32u) msk &= (1u << cut) - 1u;
         }
         VB[i] = msk;
+    }
+    __syncthreads();
+    {  // NZ: a suffix minimum over the bitmap words, 64 at a time from the end (lane l takes
+       // word b0 + 63 - l, so the suffix is a DPP prefix over the lanes)
+        const uint32_t nwd = uint32_t(m) * CW;
+        uint32_t carry = nwd;
+        for (int b0 = int((nwd - 1) & ~63u); b0 >= 0; b0 -= 64) {
+            const uint32_t i = uint32_t(b0 + 63 - lane);
+            const uint32_t v = min(wave_incl_min_dpp((i < nwd && VB[i]) ? i : nwd), carry);
+            if (i < nwd) NZ[i] = uint16_t(v);
+            carry = __builtin_amdgcn_readlane(v, 63);
+        }
+        if (lane == 0) NZ[nwd] = uint16_t(nwd);
     }
     __syncthreads();
     wstamp(2);
@@ -633,7 +654,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         uint32_t vs = 0xFFFFFFFFu;
         if (lane < m && De < C) {
             const uint32_t cs = uint32_t(lane) * C, ce = cs + C;
-            const uint32_t v = next_valid<N>(VB, cs + De, ce);
+            const uint32_t v = next_valid<N>(VB, NZ, cs + De, ce);
             if (v < ce) vs = v;
         }
         const uint64_t bm = __ballot(vs != 0xFFFFFFFFu);
@@ -687,7 +708,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
                         wsteps = 0;
                     } else {
                         p += rec_len_head<N>(head, a.rle);  // p is valid: a record starts here
-                        p = next_valid<N>(VB, p, ce);
+                        p = next_valid<N>(VB, NZ, p, ce);
                     }
                 }
             }
@@ -726,7 +747,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
             out = d - C;
         } else {
             const uint32_t cs = j * C, ce = cs + C;
-            const uint32_t nv = next_valid<N>(VB, cs + d, ce);
+            const uint32_t nv = next_valid<N>(VB, NZ, cs + d, ce);
             if (nv >= ce) {
                 out = nv - ce;
             } else {

@@ -23,7 +23,8 @@ from tests import oracle_lib as O  # noqa: E402
 w, h = 3840, 2160
 q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
 c = Codec(0, q, n)
-y = synth.frame(kind, w, h, 5) if kind in ("U", "M") else np.full((h, w), 77, np.uint8)
+y = (synth.frame("U", w, h, synth.DEFAULT_SEED) if kind == "G"  # the bench's image 0
+     else synth.frame(kind, w, h, 5) if kind in ("U", "M") else np.full((h, w), 77, np.uint8))
 out = torch.zeros(stream_bound(w, h, n, 1, 0), dtype=torch.uint8, device="cuda")
 pix = torch.empty((h, w), dtype=torch.uint8, device="cuda")
 _, end = c.encode_frames(torch.from_numpy(y).cuda(), w, h, out)

@@ -17,7 +17,8 @@ w, h = 3840, 2160
 q = O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n)
 c = Codec(0, q, n)
 yy, xx = np.mgrid[0:h, 0:w]
-kinds = {"U": synth.frame("U", w, h, 5), "M": synth.frame("M", w, h, 5),
+kinds = {"G": synth.frame("U", w, h, synth.DEFAULT_SEED),  # the bench's image 0 (the golden synU4k frame)
+         "U": synth.frame("U", w, h, 5), "M": synth.frame("M", w, h, 5),
          "grad": ((xx * 3 + yy * 5) % 256).astype(np.uint8), "flat": np.full((h, w), 77, np.uint8)}
 # the reference's example images (natural content; README.md:175-183 sizes)
 for name, (ew, eh) in {"ex1": (936, 936), "ex2": (512, 512), "ex3": (400, 400), "ex4": (4096, 912)}.items():
