@@ -50,7 +50,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ROUND = "r04"  # profiles/<ROUND>_traffic_<workload>.json: this round's counter passes (tools/gpu_traffic.sh)
 # the dominant kernel of each workload's timed launch (launch_encode: 4x4 FAST over whole 16-byte
 # groups runs encode4w_kernel; 8x8 runs encode_kernel<8>)
-KERNEL = {"c2": "encode4w_kernel", "c3": "encode_kernel<8,false>", "c4": "encode4w_kernel", "c5": "encode4w_kernel"}
+KERNEL = {"c2": "encode4w_kernel<false>", "c3": "encode_kernel<8,false>", "c4": "encode4w_kernel<false>",
+          "c5": "encode4w_kernel<false>"}
 
 WORKLOADS = {
     "c2": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=False,
@@ -83,6 +84,8 @@ def parse():
     p.add_argument("--no-check", action="store_true", help="skip the output self-check")
     p.add_argument("--batch", type=int, default=None, help="frames per launch (default: the workload's)")
     p.add_argument("--resident", type=int, default=None, help="distinct resident frames (default: the workload's)")
+    p.add_argument("--no-pack-overlap", dest="pack_overlap", action="store_false",
+                   help="C5: run the Huffman packs on the encode's stream (no second context)")
     p.add_argument("--no-single-frame", dest="single_frame", action="store_false",
                    help="skip timing one-image launches (configs[1] taken literally: one 4K frame per launch)")
     return p.parse_args()
@@ -303,6 +306,13 @@ def main():
         else:
             hpitch = 2 * pitch  # >= 32-bit codes x payload bytes
             houts = torch.zeros(hpitch * B, dtype=torch.uint8, device=dev)
+            # the packs on a second context's stream: each overlaps the next batch's encode
+            # (ie_set_pack_context; --no-pack-overlap keeps them on the encode's stream)
+            if args.pack_overlap:
+                pack_codec = Codec(local)
+                pack_stream = torch.cuda.Stream(dev)
+                pack_codec.set_stream(pack_stream.cuda_stream)
+                codec.set_pack_context(pack_codec)
             hsizes = []
             pending = []  # the batch whose trees + pack are still to do: (output buffer, slot)
 
@@ -326,7 +336,9 @@ def main():
                 drain()
                 pending.append((out, i % 2))
         wall, gpu_s = timer.run(step, args.warmup, args.steps, drain=drain)
-        codec.sync()  # raises if any asynchronous launch of the timed region timed out
+        codec.sync()  # raises if any asynchronous launch of the timed region timed out (pack context too)
+        if cfg["huffman"] and args.pack_overlap:
+            codec.set_pack_context(None)  # the per-stage timings below are taken on one stream
         px_total = world * args.steps * B * w * h
         in_bytes_per_launch = B * w * h
         # dominant kernel alone: the block encoder's launch time on its stream
@@ -365,7 +377,7 @@ def main():
                                     nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False, count_bytes=True)
             _, g3 = timer.run(enc_counted, 1, args.steps)
             t_cnt = g3 / args.steps
-            extra["counted_encode"] = {"kernel": "encode_kernel<4,false,HIST>", "launch_us": round(t_cnt * 1e6, 2),
+            extra["counted_encode"] = {"kernel": "encode4w_kernel<true>", "launch_us": round(t_cnt * 1e6, 2),
                                        "frac": round((B * w * h + out_bytes_per_launch) / t_cnt / 1e9 / HBM_PEAK_GBS, 4)}
             extra["huffman_roofline"] = {
                 "bound": "hbm", "achieved": round(hbytes / (t_h + t_p) / 1e9, 1), "peak": HBM_PEAK_GBS,

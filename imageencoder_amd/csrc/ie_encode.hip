@@ -1518,8 +1518,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 // One slot image I (bit 0 at absolute stream bit X) to the output words, by one wave: words
 // [r0, nw) counted from floor(X / 32), word r = alignbit(I[r - 1], I[r], X % 32) with I[-1] =
 // prev (the 32 bits before X); the partial word nw is left to whoever writes the next bits.
+template <typename Cnt = NoCount>
 __device__ __forceinline__ void store_slot(uint32_t* __restrict__ out, const uint32_t* I, uint64_t X, uint32_t nw,
-                                           uint32_t r0, uint32_t prev, int lane) {
+                                           uint32_t r0, uint32_t prev, int lane, const Cnt& cnt = Cnt{}) {
     if (nw <= r0) return;
     const uint64_t w0 = X >> 5;
     const uint32_t s = uint32_t(X) & 31u;
@@ -1528,7 +1529,11 @@ __device__ __forceinline__ void store_slot(uint32_t* __restrict__ out, const uin
         return bswap32(__builtin_amdgcn_alignbit(r ? am : prev, I[r], s));
     };
     const uint32_t hd = min(nw - r0, uint32_t((4u - uint32_t((w0 + r0) & 3u)) & 3u));
-    if (uint32_t(lane) < hd) out[w0 + r0 + lane] = word(r0 + lane);
+    if (uint32_t(lane) < hd) {
+        const uint32_t v = word(r0 + lane);
+        out[w0 + r0 + lane] = v;
+        cnt(w0 + r0 + lane, v);
+    }
     const uint32_t rq = r0 + hd, nq = (nw - rq) >> 2;
     for (uint32_t q = lane; q < nq; q += 64) {
         const uint32_t r = rq + 4u * q;
@@ -1539,9 +1544,17 @@ __device__ __forceinline__ void store_slot(uint32_t* __restrict__ out, const uin
         const v4u v = {bswap32(__builtin_amdgcn_alignbit(a0, b0, s)), bswap32(__builtin_amdgcn_alignbit(b0, b1, s)),
                        bswap32(__builtin_amdgcn_alignbit(b1, b2, s)), bswap32(__builtin_amdgcn_alignbit(b2, b3, s))};
         __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(out + w0 + r));
+        cnt(w0 + r, v.x);
+        cnt(w0 + r + 1, v.y);
+        cnt(w0 + r + 2, v.z);
+        cnt(w0 + r + 3, v.w);
     }
     const uint32_t rt = rq + 4u * nq;
-    if (uint32_t(lane) < nw - rt) out[w0 + rt + lane] = word(rt + lane);
+    if (uint32_t(lane) < nw - rt) {
+        const uint32_t v = word(rt + lane);
+        out[w0 + rt + lane] = v;
+        cnt(w0 + rt + lane, v);
+    }
 }
 
 // The last 32 bits of the stream up to the end of a slot image of n bits, given the 32 bits
@@ -1563,6 +1576,10 @@ __device__ __forceinline__ uint32_t slot_tail32(const uint32_t* I, uint32_t n, u
         if (IE_PROFILE && a.stamps && lane == 0) a.stamps[size_t(t) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
+// HIST (ie_encode_images_counted): every stored byte also counted into a per-tile LDS histogram
+// (256 words after misc), merged into a.hist[frame] at the end -- the Huffman pass's byte counts
+// without reading the stream back.
+template <bool HIST>
 __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, const EncTables* __restrict__ tab) {
     // (two slots per lane -- twice the tiles for small launches -- measured slower on a lone 4K
     // frame, 23.9 against 18.2 us: the phases are bound by the SIMDs' issue, not by one wave's
@@ -1576,7 +1593,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     uint32_t* const task = smem + 4 * kWReg + wv * kWTask;
     uint32_t* const res = task + 64;
     uint32_t* const misc = smem + 4 * kWReg + 4 * kWTask;
-    double* const srow = reinterpret_cast<double*>(misc + kWMisc);
+    uint32_t* const hl = misc + kWMisc;  // HIST: the tile's byte histogram
+    double* const srow = reinterpret_cast<double*>(misc + kWMisc + (HIST ? 256 : 0));
 
     int t;
     if (a.ticket) {
@@ -1590,6 +1608,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     WSTAMP(0);
     WRTSTAMP(14);
     asm volatile("; PHASE w0" ::: "memory");
+    if constexpr (HIST) hl[tid] = 0u;  // (visible after the first barrier)
     // every coefficient's FP64 row and its S, rq, qd: the fix-up reads them from LDS
     for (int i = tid; i < kWRows; i += TPB)
         srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
@@ -1953,15 +1972,25 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         // the wave's first word is written by the previous wave (or, pending, later by this one)
         const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
         uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[10]) : 0u;
+        // HIST: bytes at or past the chain's last byte are padding
+        const HistCount hc{hl, chain_last ? (start_bit + excl + A + 7) / 8 : ~0ull};
+        auto count = [&](uint64_t gw, uint32_t v) {
+            if constexpr (HIST) hc(gw, v);
+        };
         // pair 0 is stored as soon as the tile's position is known; the region then takes pair 1
         // (one wave's LDS operations complete in order)
         auto store_pair = [&](uint32_t S0, uint32_t n) {
             if (!n) return;
             const uint64_t Xb = Xw + S0;
             const uint32_t nw = uint32_t(((Xb + n) >> 5) - (Xb >> 5));
-            store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
+            if constexpr (HIST) store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane, hc);
+            else store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
             prev = slot_tail32(reg, n, prev);
         };
+        if constexpr (HIST) {
+            if (wv == 0 && chain_pos == 0)  // the words before the first record word: the caller's header
+                for (uint32_t i = lane; i < uint32_t(start_bit >> 5); i += 64) hc(i, out[i]);
+        }
         store_pair(0u, S2);
         WSTAMP(9);
     asm volatile("; PHASE w9" ::: "memory");
@@ -1977,25 +2006,33 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         const uint64_t E = Xw + Tw;
         const uint32_t e = uint32_t(E) & 31u;
         if (lane == 0) {
-            if (e) {  // the wave's last, partial word
-                if (wv < wlast) out[E >> 5] = bswap32((prev << (32u - e)) | (misc[4 + wv + 1] >> e));
-                else if (chain_last) out[E >> 5] = bswap32(prev << (32u - e));
+            if (e && (wv < wlast || chain_last)) {  // the wave's last, partial word
+                const uint32_t v = bswap32((prev << (32u - e)) | (wv < wlast ? misc[4 + wv + 1] >> e : 0u));
+                out[E >> 5] = v;
+                count(E >> 5, v);
             }
             if (wv == wlast) publish(a.st, t, 2, a.tag, prev);  // the tile's last 32 bits
             if (wv == 0 && pend) {  // the first word, with the predecessor's tail
                 const uint32_t pt = wait_tail(a.st, t - step, a.tag, a.err);
                 const uint32_t s = uint32_t(Xw) & 31u;
-                out[Xw >> 5] = bswap32((pt << (32u - s)) | (misc[4] >> s));
+                const uint32_t v = bswap32((pt << (32u - s)) | (misc[4] >> s));
+                out[Xw >> 5] = v;
+                count(Xw >> 5, v);
             }
         }
         WSTAMP(10);
         WRTSTAMP(15);
     asm volatile("; PHASE w10" ::: "memory");
     }
+    if constexpr (HIST) {
+        lds_barrier();  // every wave's bytes counted
+        if (hl[tid]) atomicAdd(&a.hist[size_t(frame) * 256 + tid], hl[tid]);
+    }
 }
 
 void launch_encode4w(const EncArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(encode4w_kernel, dim3(a.ntiles), dim3(256), kWLdsBytes, s, a, a.tab);
+    if (a.hist) hipLaunchKernelGGL(encode4w_kernel<true>, dim3(a.ntiles), dim3(256), kWLdsBytes + 1024, s, a, a.tab);
+    else hipLaunchKernelGGL(encode4w_kernel<false>, dim3(a.ntiles), dim3(256), kWLdsBytes, s, a, a.tab);
 }
 
 // The streamed host path's per-image header words: word i (read from page-locked host memory
@@ -2028,7 +2065,7 @@ void launch_encode4w(const EncArgs& a, hipStream_t s);
 void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt) {
     EncArgs a = a0;
     // 4x4 FAST over whole 16-byte groups: the wave-local encoder (encode4w_kernel)
-    if (IE_ENC_W && n == 4 && !exact && !a.hist && bpt == 4 && a.vec_ok && a.bx % 4 == 0 &&
+    if (IE_ENC_W && n == 4 && !exact && bpt == 4 && a.vec_ok && a.bx % 4 == 0 &&
         a.groups_per_frame % 8 == 0 && a.rec_bits <= 252 && !a.ablate) {
         launch_encode4w(a, s);
         return;

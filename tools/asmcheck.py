@@ -97,7 +97,8 @@ def static_lds(path):
 BUDGETS = {
     "_ZN2ie13encode_kernelILi4ELb0ELb0ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": (5, 0),
     "_ZN2ie13encode_kernelILi8ELb0ELb0ELi1EEEvNS_7EncArgsEPKNS_9EncTablesE": (4, 0),
-    "_ZN2ie15encode4w_kernelENS_7EncArgsEPKNS_9EncTablesE": (6, 0),
+    "_ZN2ie15encode4w_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
+    "_ZN2ie15encode4w_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
 }
 
 
