@@ -84,6 +84,8 @@ def parse():
     p.add_argument("--no-check", action="store_true", help="skip the output self-check")
     p.add_argument("--batch", type=int, default=None, help="frames per launch (default: the workload's)")
     p.add_argument("--resident", type=int, default=None, help="distinct resident frames (default: the workload's)")
+    p.add_argument("--chunks", type=int, default=None,
+                   help="C4: pipelined sub-batches per step (default: the workload's, 4)")
     p.add_argument("--no-pack-overlap", dest="pack_overlap", action="store_false",
                    help="C5: run the Huffman packs on the encode's stream (no second context)")
     p.add_argument("--no-single-frame", dest="single_frame", action="store_false",
@@ -522,7 +524,7 @@ def main():
         parallelism = f"independent images sharded x{world} (no collective)"
         cpu_frame = frames[0].cpu().numpy() if rank == 0 else None
     else:  # c4: one gop=1 video stream, frames sharded over ranks, RCCL gather to rank 0
-        K = cfg["chunks"]
+        K = args.chunks or cfg["chunks"]
         m = max(B // K, 1)  # frames per rank per chunk
         nloc = m * K
         F = nloc * world

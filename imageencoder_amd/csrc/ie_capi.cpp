@@ -538,9 +538,6 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     a.tab = c->d_tab;
     a.rec_bits = c->h_tab->rec_bits;
     a.tri = (c->n == 4 && (a.rec_bits - 4) / 17 <= 10) ? 1 : 0;  // bl_max = (rec_bits - 4) / (1 + N*N); 3 bl <= 30
-#ifdef IE_NOTRI  // A/B aid: pairs only
-    a.tri = 0;
-#endif
     a.coef = L.coef;
     a.hist = L.hist;
 #ifndef IE_PROFILE

@@ -549,10 +549,11 @@ __device__ __forceinline__ uint32_t next_valid(const uint32_t* VB, const uint16_
 }
 
 __host__ __device__ constexpr int rec_table2_words(uint32_t C, int D, int tm, int hbits) {
-    // L (stream words, 16-byte aligned staging: +4), VB, claims, then u16 res / tgt, the u32 walk
-    // list and the u16 next-valid-word table (tm CW + 1 entries)
+    // L (stream words, 16-byte aligned staging: +4), VB, claims, then u16 res / tgt, the u16 walk
+    // list (walk ids: the start position follows from the id, except a chunk's v*), the chunks'
+    // v* positions and the u16 next-valid-word table (tm CW + 1 entries)
     return (rec_table_stream_words(uint32_t(tm) * C) + 4 + 3) / 4 * 4 + tm * int(C >> 5) + (1 << hbits) +
-           2 * tm * (D + 1) + (tm * int(C >> 5) + 2) / 2;
+           tm * (D + 1) + (tm * (D + 1) + 1) / 2 + tm + (tm * int(C >> 5) + 2) / 2;
 }
 
 template <int N>
@@ -579,8 +580,9 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     const uint32_t HM = (1u << a.hbits) - 1u;
     uint16_t* res = reinterpret_cast<uint16_t*>(H + HM + 1);
     uint16_t* tgt = res + tm * D1;
-    uint32_t* wl = H + HM + 1 + tm * D1;  // after res + tgt (tm * D1 words together)
-    uint16_t* NZ = reinterpret_cast<uint16_t*>(wl + tm * D1);
+    uint16_t* wl = reinterpret_cast<uint16_t*>(H + HM + 1 + tm * D1);  // after res + tgt (tm * D1 words together)
+    uint32_t* vst = H + HM + 1 + tm * D1 + (tm * D1 + 1) / 2;          // [tm] every chunk's v* position
+    uint16_t* NZ = reinterpret_cast<uint16_t*>(vst + tm);
     const RecSpan sp = rec_span(a);
     const uint64_t c0 = sp.start + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
@@ -645,8 +647,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         while (bits) {
             const uint32_t b = __builtin_ctz(bits);
             bits &= bits - 1u;
-            const uint32_t pos = j * C + (w << 5) + b;
-            wl[at++] = (pos << 16) | (j * D1 + (w << 5) + b);
+            wl[at++] = uint16_t(j * D1 + (w << 5) + b);  // (starts at j C + (w << 5) + b)
         }
         nw += __shfl(incl, 63, 64);
     }
@@ -660,7 +661,8 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         const uint64_t bm = __ballot(vs != 0xFFFFFFFFu);
         if (vs != 0xFFFFFFFFu) {
             const uint32_t r = __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u));
-            wl[nw + r] = (vs << 16) | (uint32_t(lane) * D1 + D);
+            wl[nw + r] = uint16_t(uint32_t(lane) * D1 + D);
+            vst[lane] = vs;
         }
         nw += uint32_t(__popcll(bm));
     }
@@ -675,10 +677,10 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
             if (!act) {
                 const uint32_t r = nxt + __builtin_amdgcn_mbcnt_hi(uint32_t(need >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(need), 0u));
                 if (r < nw) {
-                    const uint32_t e = wl[r];
-                    p = e >> 16;
-                    id = e & 0xFFFFu;
-                    ce = (id / D1 + 1u) * C;
+                    id = wl[r];
+                    const uint32_t j = id / D1, d = id - j * D1;
+                    p = (d < uint32_t(D)) ? j * C + d : vst[j];
+                    ce = (j + 1u) * C;
                     act = true;
                 }
             }
@@ -731,7 +733,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     wstamp(4);
     // 4. merged walks take their root's exit (read-only chases; only non-roots are written)
     for (uint32_t r = lane; r < nw; r += 64) {
-        const uint32_t id = wl[r] & 0xFFFFu;
+        const uint32_t id = wl[r];
         uint32_t x = tgt[id];
         if (x == kNoOwner) continue;
         for (uint32_t y = tgt[x]; y != kNoOwner; y = tgt[x]) x = y;

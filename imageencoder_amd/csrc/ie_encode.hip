@@ -53,9 +53,6 @@ template <> struct ZigZagInv<8> {
 #ifndef IE_PROFILE
 #define IE_PROFILE 0
 #endif
-#ifndef IE_K8_PROF
-#define IE_K8_PROF 0  // 1: encode_kernel<8> reads the profiling fields in every build (round 3's spill workaround)
-#endif
 #ifndef IE_BPT4
 #define IE_BPT4 4
 #endif
@@ -506,13 +503,9 @@ __device__ __forceinline__ uint32_t size_block(uint32_t (&zp)[N * N / 2], int rl
 }
 
 // OR the low `len` bits of v (MSB first) into the LDS bit image at bit p (len + p%32 <= 64).
-#ifndef IE_ASM_OR
-#define IE_ASM_OR 1
-#endif
 __device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t v, uint32_t len) {
     const uint32_t s = p & 31u;
     const uint64_t x = uint64_t(v) << (64u - len - s);
-#if IE_ASM_OR
     // The image is the dynamic LDS area at LDS byte address 0 (the encode kernels allocate no static
     // LDS; tools/asmcheck.py checks their group_segment_fixed_size): the word pair's byte address
     // straight from p, the second word through the instruction's offset field.
@@ -520,19 +513,12 @@ __device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t
     const uint32_t a = (p >> 3) & ~3u;
     asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a), "v"(uint32_t(x >> 32)), "v"(uint32_t(x))
                  : "memory");
-#else
-    atomicOr(&img[p >> 5], uint32_t(x >> 32));
-    atomicOr(&img[(p >> 5) + 1], uint32_t(x));
-#endif
 }
 
 // Branch-free variant: every pair is written (past Lw the packed coefficients are zero, so
 // those ORs are no-ops) and the wave leaves the loop once no lane has a pair left: no per-lane
 // exec-mask juggling per pair.  The zero pairs may land up to 2 * 16 * N*N/2 bits past the
 // record: the image keeps that much slack.
-#ifndef IE_EMIT2
-#define IE_EMIT2 1
-#endif
 template <int N>
 __device__ __forceinline__ void emit_block2(uint32_t* img, uint32_t p, const uint32_t (&zp)[N * N / 2], uint32_t blw,
                                             int rle) {
@@ -554,12 +540,9 @@ __device__ __forceinline__ void emit_block2(uint32_t* img, uint32_t p, const uin
     }
 }
 
-// IE_EMIT_ALL: every triple is ORed in, without a wave-wide "any lane still has one" exit per
-// field (past Lw the coefficients are zero): the v_cmp + branch per field cost more than the
-// skipped fields save unless every lane of the wave has a short record (measured -2 % on C2).
-#ifndef IE_EMIT_ALL
-#define IE_EMIT_ALL 1
-#endif
+// Every triple is ORed in, without a wave-wide "any lane still has one" exit per field (past Lw
+// the coefficients are zero): the v_cmp + branch per field cost more than the skipped fields save
+// unless every lane of the wave has a short record (measured -2 % on C2).
 // 4x4 RLE records when every bl of the matrix is <= 11 (EncArgs::tri, from the host's record
 // bound): the header, Lw and z0 in one field of 4 + 2*bl bits, then the coefficients THREE at a
 // time (3*bl <= 33 bits, within scatter_bits' 64-bit window): 6 ORed fields per block instead of
@@ -573,34 +556,9 @@ __device__ __forceinline__ void emit_block3(uint32_t* img, uint32_t p, const uin
     p += 4u + 2u * bl;
 #pragma unroll
     for (int j = 0; j < 5; j++) {
-        if (!IE_EMIT_ALL && !__ballot(uint32_t(3 * j + 1) < lw)) break;  // no lane has coefficient 3j+1
         const uint32_t v = (((z(3 * j + 1) << bl) | z(3 * j + 2)) << bl) | z(3 * j + 3);
         scatter_bits(img, p, v, 3u * bl);
         p += 3u * bl;
-    }
-}
-
-// The record of one sized block at bit p of the tile image (Block.cpp:372-413): bl in 4 bits,
-// [Lw in bl bits,] then the coefficients two at a time (2*bl <= 32 bits per OR pair).
-template <int N>
-__device__ __forceinline__ void emit_block(uint32_t* img, uint32_t p, const uint32_t (&zp)[N * N / 2], uint32_t blw,
-                                           int rle) {
-    const uint32_t bl = blw & 0xFFu, lw = blw >> 8;
-    const uint32_t m = (1u << bl) - 1u;
-    if (rle) {
-        scatter_bits(img, p, ((bl & 0xFu) << bl) | lw, 4u + bl);
-        p += 4u + bl;
-    } else {
-        scatter_bits(img, p, bl & 0xFu, 4u);
-        p += 4u;
-    }
-#pragma unroll
-    for (int j = 0; j < N * N / 2; j++) {
-        if (uint32_t(2 * j) < lw) {
-            const uint32_t lo = zp[j] & m, hi = (zp[j] >> 16) & m;
-            scatter_bits(img, p, (lo << bl) | hi, 2u * bl);
-            p += 2u * bl;
-        }
     }
 }
 
@@ -663,59 +621,11 @@ __device__ __forceinline__ void load_tile(const EncArgs& a, const TileGeo& g, ui
         if (stamps && tid == 0) stamps[size_t(t) * kStamps + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// Emission through a per-lane 64-bit accumulator: whole words are ORed into the (zeroed) image
-// as they complete, so a lane issues ~one LDS operation per 32 output bits instead of two per field.
-#ifndef IE_EMIT_SINK
-#define IE_EMIT_SINK 0
-#endif
-struct WordSink {
-    uint32_t* img;
-    uint64_t acc;
-    uint32_t n;   // bits in acc not yet written (< 32)
-    uint32_t wi;  // word index of the next word
-    __device__ __forceinline__ WordSink(uint32_t* l, uint32_t p) : img(l), acc(0), n(p & 31u), wi(p >> 5) {}
-    __device__ __forceinline__ void put(uint32_t len, uint32_t v) {  // len in [1, 32], v < 2^len
-        acc = (acc << len) | v;
-        n += len;
-        if (n >= 32) {
-            n -= 32;
-            atomicOr(&img[wi], uint32_t(acc >> n));
-            wi++;
-        }
-    }
-    __device__ __forceinline__ void finish() {
-        if (n) atomicOr(&img[wi], uint32_t(acc << (32 - n)));
-    }
-};
-
-template <int N>
-__device__ __forceinline__ void emit_block_sink(WordSink& k, const uint32_t (&zp)[N * N / 2], uint32_t blw, int rle) {
-    const uint32_t bl = blw & 0xFFu, lw = blw >> 8;
-    const uint32_t m = (1u << bl) - 1u;
-    if (rle) k.put(4u + bl, ((bl & 0xFu) << bl) | lw);
-    else k.put(4u, bl & 0xFu);
-#pragma unroll
-    for (int j = 0; j < N * N / 2; j++) {
-        if (uint32_t(2 * j) < lw) {
-            const uint32_t lo = zp[j] & m, hi = (zp[j] >> 16) & m;
-            if (uint32_t(2 * j + 1) < lw) k.put(2u * bl, (lo << bl) | hi);
-            else k.put(bl, lo);
-        }
-    }
-}
-
-// Occupancy hint: __launch_bounds__'s second argument (Geo<N>::WAVES).  IE_LB_ATTR=1 states it
-// as amdgpu_waves_per_eu instead (A/B aid: measured slower).
-#ifndef IE_LB_ATTR
-#define IE_LB_ATTR 0
-#endif
+// Occupancy hint: __launch_bounds__'s second argument (Geo<N>::WAVES; stating it as
+// amdgpu_waves_per_eu instead measured slower).
 // The EXACT 4x4 kernel (FP64 for every coefficient) keeps four waves per SIMD.
 template <int N, bool EXACT> constexpr int enc_waves() { return (N == 4 && EXACT) ? 4 : Geo<N>::WAVES; }
-#if IE_LB_ATTR
-#define IE_ENC_BOUNDS(N, EXACT) __launch_bounds__(kEncTPB) __attribute__((amdgpu_waves_per_eu((enc_waves<N, EXACT>()), 8)))
-#else
 #define IE_ENC_BOUNDS(N, EXACT) __launch_bounds__(kEncTPB, (enc_waves<N, EXACT>()))
-#endif
 // HIST: count the stored bytes into a per-tile LDS histogram (256 words after the misc area),
 // merged into a.hist[frame] at the end: the Huffman pass's histogram without re-reading the stream.
 struct HistCount {
@@ -743,11 +653,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     constexpr int BPT = BB;
     constexpr int WPR = BPT * N / 4;
     constexpr int TPB = kEncTPB;
-#ifdef IE_STATIC_IMG4  // A/B aid: a static image of this many bits per block (4x4 only)
-    __shared__ __attribute__((aligned(16))) uint32_t smem[image_words_for(4, 4, IE_STATIC_IMG4) + 32 + 2 * (3 * NN + 9)];
-#else
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // [a.img_words + 32]
-#endif
     // Dynamic LDS: [tile image: img_words][misc: 32 words][HIST: 256 words][srow]; the image at
     // LDS address 0, so its addresses need no base.
     uint32_t* img = smem;
@@ -770,8 +676,8 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     // Profiling hooks (IE_ABLATE / IE_STAMPS) exist only in IE_PROFILE builds (tools/variants.sh):
     // in the product build they are constants, so they hold no scalar registers.  (Round 3 kept them
     // live in the 8x8 kernel to dodge a spill; with its pixels in LDS and the fix-up reading them
-    // from there the 8x8 kernel has no scratch without that: IE_K8_PROF=1 restores it for A/B.)
-    constexpr bool kProf = IE_PROFILE || (N == 8 && IE_K8_PROF);
+    // from there the 8x8 kernel has no scratch without that.)
+    constexpr bool kProf = IE_PROFILE != 0;
     const int ablate = kProf ? a.ablate : 0;
     uint64_t* const stamps = kProf ? a.stamps : nullptr;
     // Tile order = dispatch order.  Workgroups are dispatched in increasing blockIdx, so every
@@ -844,7 +750,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         }
     } else if constexpr (kLdsPix) {
         static_assert((BPT == 4 || BPT == 1) && WPR == BPT && TPB % 64 == 0, "LDS pixel layout: 4 * BPT bytes per lane per row");
-        if (IE_PROFILE && (ablate & 4096)) {
+        if (ablate & 4096) {
             // profiling: no pixel loads at all (the LDS holds whatever the previous tile left)
         } else if (!__ballot(!(a.vec_ok && nblk == BPT))) {  // every group of the wave is whole: DMA
             const uint8_t* base =
@@ -882,7 +788,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     if constexpr (kLdsPix || kLdsPix8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
 
     asm volatile("; PHASE load_done" ::: "memory");
-    if (IE_PROFILE && (ablate & 512)) return;  // profiling: instruction count of the prologue + load alone
+    if (ablate & 512) return;  // profiling: instruction count of the prologue + load alone
     if (stamps) {  // profiling: wait for the pixels so the stamp marks their arrival
         uint32_t acc = 0;
 #pragma unroll
@@ -968,7 +874,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         }
     }
     asm volatile("; PHASE quant_done" ::: "memory");
-    if (IE_PROFILE && (ablate & 1024)) {  // profiling: ... + transform + rounding (keep the results live)
+    if (ablate & 1024) {  // profiling: ... + transform + rounding (keep the results live)
         uint32_t acc = flags;
 #pragma unroll
         for (int b = 0; b < BPT; b++)
@@ -1324,7 +1230,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         mybits += rbits[b];
     }
     asm volatile("; PHASE size_done" ::: "memory");
-    if (IE_PROFILE && (ablate & 2048)) {  // profiling: ... + FP64 fix-up + sizing
+    if (ablate & 2048) {  // profiling: ... + FP64 fix-up + sizing
         uint32_t acc = mybits;
 #pragma unroll
         for (int b = 0; b < BPT; b++)
@@ -1348,29 +1254,17 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     lds_barrier();
     asm volatile("; PHASE scan_done" ::: "memory");
     STAMP(6);
-    if (!(ablate & 2)) {
-        if (IE_EMIT_SINK) {
-            if (mybits) {
-                WordSink k(img, off);
+    if (!(ablate & 2)) {  // the records: header + Lw + z0 and coefficient triples, or pairs
+        uint32_t p = off;
 #pragma unroll
-                for (int b = 0; b < BPT; b++)
-                    if (rbits[b]) emit_block_sink<N>(k, zp[b], blw[b], a.rle);
-                k.finish();
+        for (int b = 0; b < BPT; b++) {
+            if (N == 4 && a.tri && a.rle) {
+                if constexpr (N == 4)
+                    if (rbits[b]) emit_block3(img, p, zp[b], blw[b]);
+            } else {
+                if (rbits[b]) emit_block2<N>(img, p, zp[b], blw[b], a.rle);
             }
-        } else {
-            uint32_t p = off;
-#pragma unroll
-            for (int b = 0; b < BPT; b++) {
-                if (N == 4 && a.tri && a.rle) {
-                    if constexpr (N == 4)
-                        if (rbits[b]) emit_block3(img, p, zp[b], blw[b]);
-                } else if (IE_EMIT2) {
-                    if (rbits[b]) emit_block2<N>(img, p, zp[b], blw[b], a.rle);
-                } else {
-                    if (rbits[b]) emit_block<N>(img, p, zp[b], blw[b], a.rle);
-                }
-                p += rbits[b];
-            }
+            p += rbits[b];
         }
     }
     lds_barrier();
@@ -1501,7 +1395,12 @@ constexpr int kWReg = 1024;  // words per wave region: [4 rows][64 NS blocks] pi
 constexpr int kWTask = 128;  // words per wave: fix-up tasks [64] + results [64]
 constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9] excl, [10] ptail, [11] tail pending, [12] ticket,
                              // [16..17] FP64 task counters, [18..25] small-launch window sums, [26..29] their found flags
-constexpr int kWRows = 16 * 16 + 3 * 16;  // FP64 rows P[16][16], then S, rq, qd (doubles)
+#ifndef IE_W_SROW_ALL
+#define IE_W_SROW_ALL 1  // 1: all 16 FP64 rows in LDS; 0: the structural three (whole blocks read the table)
+#endif
+// FP64 rows in LDS (doubles): P[16][16] then S, rq, qd of every coefficient, or (IE_W_SROW_ALL 0)
+// the rows of the three structural coefficients and their S, rq, qd
+constexpr int kWRows = IE_W_SROW_ALL ? 16 * 16 + 3 * 16 : 3 * 16 + 3 * 3;
 constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc) * 4 + kWRows * 8;
 
 // Inclusive scan over the 64 lanes of a wave by DPP row shifts and row broadcasts (six VALU).
@@ -1609,9 +1508,13 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     WRTSTAMP(14);
     asm volatile("; PHASE w0" ::: "memory");
     if constexpr (HIST) hl[tid] = 0u;  // (visible after the first barrier)
-    // every coefficient's FP64 row and its S, rq, qd: the fix-up reads them from LDS
+    // the FP64 rows and their S, rq, qd: the fix-up reads them from LDS
     for (int i = tid; i < kWRows; i += TPB)
-        srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
+        srow[i] = !IE_W_SROW_ALL ? (i < 3 * NN ? tab->P[Structural<N>::k[i / NN] * NN + i % NN]
+                                  : i < 3 * NN + 3 ? tab->S[Structural<N>::k[i - 3 * NN]]
+                                  : i < 3 * NN + 6 ? tab->rq[Structural<N>::k[i - 3 * NN - 3]]
+                                  : tab->qd[Structural<N>::k[i - 3 * NN - 6]])
+                : (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
                 : (i < NN * NN + 2 * NN) ? tab->rq[i - NN * NN - NN] : tab->qd[i - NN * NN - 2 * NN];
     const TileGeo g = tile_geo<4, 4, TG>(a, t, tid);  // lane l of wave w: group 64 w + l of the tile
     const uint64_t start_bit = a.start_dev ? *a.start_dev : a.start_bit;
@@ -1700,9 +1603,12 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                 const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
                 const BlockPx<N> px = block_px(b, owner);
                 const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
+                const int y = !IE_W_SROW_ALL ? exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
+                                                                  srow[3 * NN + 6 + s], px)
+                                             : exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                                 srow[NN * NN + 2 * NN + k], px);
                 res[lane] = (IE_W_DBG & 128) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
-                                             : uint32_t(exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                                          srow[NN * NN + 2 * NN + k], px)) & 0xFFFFu;
+                                             : uint32_t(y) & 0xFFFFu;
             }
             wave_sync();
             // the owners take their results back: the flagged positions in bit order, each a
@@ -1747,8 +1653,10 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                     const uint32_t tk = task[lane >> 4];
                     const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
                     const BlockPx<N> px = block_px(b, owner);
-                    res[lane] = uint32_t(exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                           srow[NN * NN + 2 * NN + k], px)) & 0xFFFFu;
+                    const int y = !IE_W_SROW_ALL ? exact_coef_row<N>(tab->P + k * NN, tab->S[k], tab->rq[k], tab->qd[k], px)
+                                                 : exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                                     srow[NN * NN + 2 * NN + k], px);
+                    res[lane] = uint32_t(y) & 0xFFFFu;
                 }
                 wave_sync();
                 m = wf;
@@ -2073,13 +1981,8 @@ void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt)
     a.img_words = image_words_for(n, bpt, a.rec_bits);
     if (n == 4 && a.img_words < fix_words<4>()) a.img_words = fix_words<4>();
     if (n == 8 && a.img_words < kFix8Words) a.img_words = kFix8Words;
-#ifdef IE_STATIC_IMG4
-    a.img_words = image_words_for(4, 4, IE_STATIC_IMG4);
-    const size_t lds = 0;
-#else
     const size_t rows = exact ? 0 : (n == 4 ? size_t(n * n * n * n + 3 * n * n) : size_t(3 * n * n + 9));
     const size_t lds = (size_t(a.img_words) + 32 + (a.hist ? 256 : 0)) * sizeof(uint32_t) + rows * sizeof(double);
-#endif
     const dim3 grid(a.ntiles), block(kEncTPB);
     if (a.hist) {  // segmented 4x4 FAST launches only (ie_encode_images_counted; 8x8 would spill)
         hipLaunchKernelGGL((encode_kernel<4, false, true>), grid, block, lds, s, a, a.tab);
