@@ -68,9 +68,6 @@ template <> struct ZigZagInv<8> {
 #ifndef IE_TPB
 #define IE_TPB 256
 #endif
-#ifndef IE_PIX64
-#define IE_PIX64 1  // measured -0.6 % on C2 (same-process A/B)
-#endif
 constexpr int kEncTPB = IE_TPB;
 template <int N> struct Geo;
 template <> struct Geo<4> {  // IE_BPT4 blocks side by side: 4 * IE_BPT4 bytes per pixel row per lane
@@ -91,10 +88,7 @@ constexpr int image_words_for(int n, int bpt, int rec_bits) {
 }
 
 // Structural fix-up compaction (FAST 4x4): per-wave LDS task slots in the (not yet built) tile
-// image, after the per-lane whole-block result slots [0, kEncTPB * 8).
-#ifndef IE_FIX_COMPACT
-#define IE_FIX_COMPACT 1
-#endif
+// image, after the pixel area.
 #ifndef IE_FIX_UNROLL
 #define IE_FIX_UNROLL 16
 #endif
@@ -102,16 +96,10 @@ constexpr int image_words_for(int n, int bpt, int rec_bits) {
 // destination) in the fix-up's pixel area, laid out per wave as [row r][lane][4 words] (block b
 // of a lane = word b of each row), and every block reads its four rows back when it is
 // transformed: no pixel registers live across the tile's phases.
-#ifndef IE_LDS_PIX
-#define IE_LDS_PIX 1
-#endif
 constexpr int kFixPix = 0;  // [BPT][TPB] x 4 words: the pixels
 template <int B> constexpr int fix_tasks() { return kFixPix + B * kEncTPB * 4; }  // per wave: [64] tasks, [64] results
 template <int B> constexpr int fix_words() { return fix_tasks<B>() + (kEncTPB / 64) * 128; }  // the image is never smaller
 // 8x8: one 16-word block per lane at a 20-word stride (16-byte writes land on distinct banks)
-#ifndef IE_FIX_COMPACT8
-#define IE_FIX_COMPACT8 1
-#endif
 constexpr int kFix8Stride = 20;
 constexpr int kFix8Tasks = kFix8Stride * kEncTPB;
 constexpr int kNsStage = 4;  // non-structural rows staged per pass, per wave
@@ -713,10 +701,10 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     const uint64_t start_bit = a.start_dev ? *a.start_dev : a.start_bit;
     const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
     const int nblk = g.nblk, byi = g.byi, bx0 = g.bx0;
-    constexpr bool kLdsPix = IE_LDS_PIX && N == 4 && !EXACT;
+    constexpr bool kLdsPix = N == 4 && !EXACT;
     // 8x8 FAST: the pixels in LDS too, [8 rows][64 lanes][2 words] per wave (block row r of lane l
     // = words r*128 + 2l, 2l+1): no pixel registers live through the transform and the fix-up
-    constexpr bool kLdsPix8 = IE_LDS_PIX && N == 8 && !EXACT;
+    constexpr bool kLdsPix8 = N == 8 && !EXACT;
     // kLdsPix: this wave's [4 rows][64 lanes][BPT] words; block b of a lane = word b of each row
     constexpr int kRowW = (N == 8) ? 128 : 64 * BPT;
     uint32_t* const pwave = img + kFixPix + (tid >> 6) * (N * kRowW);
@@ -803,7 +791,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     // fix-up requests, 4 bits per block: bits 0-2 structural coefficient s, bit 3 the whole block
     uint32_t flags = 0;
     uint64_t near8 = 0;  // 8x8: per-coefficient requests of the lane's one block
-    uint32_t pix_next[N];  // IE_PIX64: the odd block's rows, read with the even block's
+    uint32_t pix_next[N];  // the odd block's rows, read with the even block's
     (void)pix_next;
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
@@ -834,8 +822,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                 block_pixels<N, 2>(rows, 0, x);
             } else if constexpr (kLdsPix) {
                 uint32_t rows[N][1];
-#if IE_PIX64
-                // two blocks' rows per 8-byte read (2-way instead of 4-way bank conflicts)
+                // two blocks' rows per 8-byte read (2-way instead of 4-way bank conflicts: -0.6 %)
                 if constexpr (BPT % 2 == 0) {
                     if (b % 2 == 0) {
 #pragma unroll
@@ -848,10 +835,10 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
 #pragma unroll
                         for (int r = 0; r < N; r++) rows[r][0] = pix_next[r];
                     }
-                } else
-#endif
+                } else {
 #pragma unroll
-                for (int r = 0; r < N; r++) rows[r][0] = pwave[r * kRowW + lane * BPT + b];
+                    for (int r = 0; r < N; r++) rows[r][0] = pwave[r * kRowW + lane * BPT + b];
+                }
                 block_pixels<N, 1>(rows, 0, x);
             } else {
                 block_pixels<N, WPR>(seg, b, x);
@@ -886,26 +873,15 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
     STAMP(3);
 
     // ---------------------------------------------------------------- 1b. FP64 fix-up
-    // Every lane re-evaluates its own requests in the reference's FP64 order -- no compaction,
-    // no barrier: a wave loops as long as any lane still has one.  Structural coefficient s of
-    // block b: its P row comes from the LDS copy; a whole-block request (rare): fix_block, with
-    // its per-lane result slot in the (not yet built) tile image.
-    if constexpr (!EXACT && N == 8 && IE_FIX_COMPACT8) {
+    // Requests compacted per wave into an LDS task list, evaluated one per lane in the
+    // reference's FP64 order, patched back by their owners (below: 8x8, then 4x4).
+    if constexpr (!EXACT && N == 8) {
         // 8x8: one task per flagged coefficient, compacted per wave as for 4x4: the lane's block
         // (16 words) goes to an LDS slot, lane i evaluates task i in FP64 -- the structural
         // coefficients' rows from the LDS copy, any other row from the (L2-resident) table --
         // and the owners patch their results in.
         const unsigned nfix = unsigned(__popcll(near8));
         if (__ballot(near8 != 0)) {
-            uint32_t* pxl = img;  // (!kLdsPix8) [TPB] x kFix8Stride words
-            if constexpr (!kLdsPix8) {
-#pragma unroll
-                for (int q4 = 0; q4 < 4; q4++) {
-                    u32x4 v;
-                    v.x = seg[2 * q4][0]; v.y = seg[2 * q4][1]; v.z = seg[2 * q4 + 1][0]; v.w = seg[2 * q4 + 1][1];
-                    *reinterpret_cast<u32x4*>(pxl + kFix8Stride * tid + 4 * q4) = v;
-                }
-            }
             const uint32_t cnt = nfix;
             uint32_t pre = 0, total = 0;
 #pragma unroll
@@ -952,17 +928,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
                         const double S = (s >= 0) ? srow[3 * NN + s] : tab->S[k];
                         const double rq = (s >= 0) ? srow[3 * NN + 3 + s] : tab->rq[k];
                         const double qd = (s >= 0) ? srow[3 * NN + 6 + s] : tab->qd[k];
-                        if constexpr (kLdsPix8) {
-                            res[lane] = uint32_t(exact_coef_rows8(P, S, rq, qd, pwave + 2 * (owner & 63))) & 0xFFFFu;
-                        } else {
-                            BlockPx<N> px;
-#pragma unroll
-                            for (int q4 = 0; q4 < 4; q4++) {
-                                const u32x4 w4 = *reinterpret_cast<const u32x4*>(pxl + kFix8Stride * owner + 4 * q4);
-                                px.w[4 * q4] = w4.x; px.w[4 * q4 + 1] = w4.y; px.w[4 * q4 + 2] = w4.z; px.w[4 * q4 + 3] = w4.w;
-                            }
-                            res[lane] = uint32_t(exact_coef_row<N>(P, S, rq, qd, px)) & 0xFFFFu;
-                        }
+                        res[lane] = uint32_t(exact_coef_rows8(P, S, rq, qd, pwave + 2 * (owner & 63))) & 0xFFFFu;
                         done = true;
                     }
                     wave_sync();  // the next pass rewrites the staged rows
@@ -988,56 +954,17 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
         }
         const unsigned wsum = unsigned(wave_sum64(nfix));
         if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
-    } else if constexpr (!EXACT && N == 8) {
-        // 8x8: one coefficient per request, its FP64 row from the (L2-resident) table
-        uint64_t nr = near8;
-        const unsigned nfix = unsigned(__popcll(near8));
-        while (__ballot(nr != 0)) {
-            if (nr) {
-                const int k = __ffsll((unsigned long long)nr) - 1;
-                nr &= nr - 1;
-                BlockPx<N> px;
-#pragma unroll
-                for (int r = 0; r < N; r++)
-#pragma unroll
-                    for (int m = 0; m < N / 4; m++) px.w[r * (N / 4) + m] = seg[r][m];
-                const uint32_t v = uint32_t(exact_coef_inl<N>(tab, k, px)) & 0xFFFFu;
-                const int kz = ZigZagInv<N>::pos[k];
-#pragma unroll
-                for (int j = 0; j < NP; j++)
-                    if ((kz >> 1) == j)
-                        zp[0][j] = (kz & 1) ? ((zp[0][j] & 0xFFFFu) | (v << 16)) : ((zp[0][j] & 0xFFFF0000u) | v);
-            }
-        }
-        const unsigned wsum = unsigned(wave_sum64(nfix));
-        if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
-    } else if constexpr (!EXACT && IE_FIX_COMPACT) {
+    } else if constexpr (!EXACT) {
         // Structural requests, compacted per wave: the wave's pixels go to LDS (so the pixel
         // registers die here), every request gets a task number (a 4-plane ballot prefix), lane i
         // evaluates task i in FP64 and the owners patch their results in.  One FP64 evaluation
         // per 64 requests instead of one per lane per request.
         if (__ballot(flags != 0)) {
-            // the pixels of block b of thread `owner` (of this wave): kLdsPix reads the tile's
-            // LDS pixel layout; otherwise they are copied there first, [BPT][TPB] x 16 bytes
-            uint32_t* pxl = img + kFixPix;
-            if constexpr (!kLdsPix) {
-#pragma unroll
-                for (int bb = 0; bb < BPT; bb++) {
-                    u32x4 v;
-                    v.x = seg[0][(bb * N) / 4]; v.y = seg[1][(bb * N) / 4];
-                    v.z = seg[2][(bb * N) / 4]; v.w = seg[3][(bb * N) / 4];
-                    *reinterpret_cast<u32x4*>(pxl + 4 * (bb * TPB + tid)) = v;
-                }
-            }
+            // the pixels of block b of thread `owner` (of this wave): the tile's LDS pixel layout
             auto block_px = [&](int b, int owner) {
                 BlockPx<N> px;
-                if constexpr (kLdsPix) {
 #pragma unroll
-                    for (int r = 0; r < N; r++) px.w[r] = pwave[r * kRowW + (owner & 63) * BPT + b];
-                } else {
-                    const u32x4 v = *reinterpret_cast<const u32x4*>(pxl + 4 * (b * TPB + owner));
-                    px.w[0] = v.x; px.w[1] = v.y; px.w[2] = v.z; px.w[3] = v.w;
-                }
+                for (int r = 0; r < N; r++) px.w[r] = pwave[r * kRowW + (owner & 63) * BPT + b];
                 return px;
             };
             const uint32_t sf = flags & (0x77777777u >> (32 - 4 * BPT));
@@ -1145,67 +1072,6 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
             }
         }
         const unsigned wsum = unsigned(wave_sum64(__popc(flags)));
-        if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
-    } else if constexpr (!EXACT) {
-        uint32_t sf = flags & (0x77777777u >> (32 - 4 * BPT));
-        while (__ballot(sf != 0)) {
-            if (sf) {
-                const int bit = __ffs(sf) - 1;
-                sf &= sf - 1;
-                const int b = bit >> 2, s = bit & 3;
-                BlockPx<N> px;
-#pragma unroll
-                for (int r = 0; r < N; r++)
-#pragma unroll
-                    for (int m = 0; m < N / 4; m++) {
-                        uint32_t v = seg[r][m];
-#pragma unroll
-                        for (int bb = 1; bb < BPT; bb++) v = (b == bb) ? seg[r][(bb * N) / 4 + m] : v;
-                        px.w[r * (N / 4) + m] = v;
-                    }
-                const int ks = kFullRows ? Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) +
-                                               Structural<N>::k[2] * (s == 2)
-                                         : s;
-                const uint32_t v = uint32_t(exact_coef_row<N>(rowP(ks), rowS(ks), rowRq(ks), rowQd(ks), px)) & 0xFFFFu;
-#pragma unroll
-                for (int bb = 0; bb < BPT; bb++)
-#pragma unroll
-                    for (int ss = 0; ss < 3; ss++) {
-                        const int zpos = Structural<N>::zpos(ss);
-                        if (b == bb && s == ss)
-                            zp[bb][zpos >> 1] = (zpos & 1) ? ((zp[bb][zpos >> 1] & 0xFFFFu) | (v << 16))
-                                                           : ((zp[bb][zpos >> 1] & 0xFFFF0000u) | v);
-                    }
-            }
-        }
-        uint32_t wf = flags & (0x88888888u >> (32 - 4 * BPT));
-        unsigned nfix = __popc(flags);
-        while (__ballot(wf != 0)) {
-            if (wf) {
-                const int b = (__ffs(wf) - 1) >> 2;
-                wf &= wf - 1;
-                BlockPx<N> px;
-#pragma unroll
-                for (int r = 0; r < N; r++)
-#pragma unroll
-                    for (int m = 0; m < N / 4; m++) {
-                        uint32_t v = seg[r][m];
-#pragma unroll
-                        for (int bb = 1; bb < BPT; bb++) v = (b == bb) ? seg[r][(bb * N) / 4 + m] : v;
-                        px.w[r * (N / 4) + m] = v;
-                    }
-                uint32_t* res = img + tid * NP;  // this lane's slot (the image is built later)
-                fix_block<N>(tab, px, res);
-#pragma unroll
-                for (int bb = 0; bb < BPT; bb++)
-                    if (b == bb) {
-#pragma unroll
-                        for (int j = 0; j < NP; j++) zp[bb][j] = res[j];
-                    }
-            }
-        }
-        // statistics: one plain store per wave (a shared atomic counter would serialise the waves)
-        const unsigned wsum = unsigned(wave_sum64(nfix));
         if ((tid & 63) == 0) a.wave_fix[size_t(t) * (TPB / 64) + (tid >> 6)] = wsum;
     }
     asm volatile("; PHASE fix_done" ::: "memory");
