@@ -86,8 +86,6 @@ def parse():
     p.add_argument("--resident", type=int, default=None, help="distinct resident frames (default: the workload's)")
     p.add_argument("--chunks", type=int, default=None,
                    help="C4: pipelined sub-batches per step (default: the workload's, 4)")
-    p.add_argument("--no-pack-overlap", dest="pack_overlap", action="store_false",
-                   help="C5: run the Huffman packs on the encode's stream (no second context)")
     p.add_argument("--no-single-frame", dest="single_frame", action="store_false",
                    help="skip timing one-image launches (configs[1] taken literally: one 4K frame per launch)")
     return p.parse_args()
@@ -308,13 +306,6 @@ def main():
         else:
             hpitch = 2 * pitch  # >= 32-bit codes x payload bytes
             houts = torch.zeros(hpitch * B, dtype=torch.uint8, device=dev)
-            # the packs on a second context's stream: each overlaps the next batch's encode
-            # (ie_set_pack_context; --no-pack-overlap keeps them on the encode's stream)
-            if args.pack_overlap:
-                pack_codec = Codec(local)
-                pack_stream = torch.cuda.Stream(dev)
-                pack_codec.set_stream(pack_stream.cuda_stream)
-                codec.set_pack_context(pack_codec)
             hsizes = []
             pending = []  # the batch whose trees + pack are still to do: (output buffer, slot)
 
@@ -338,9 +329,7 @@ def main():
                 drain()
                 pending.append((out, i % 2))
         wall, gpu_s = timer.run(step, args.warmup, args.steps, drain=drain)
-        codec.sync()  # raises if any asynchronous launch of the timed region timed out (pack context too)
-        if cfg["huffman"] and args.pack_overlap:
-            codec.set_pack_context(None)  # the per-stage timings below are taken on one stream
+        codec.sync()  # raises if any asynchronous launch of the timed region timed out
         px_total = world * args.steps * B * w * h
         in_bytes_per_launch = B * w * h
         # dominant kernel alone: the block encoder's launch time on its stream

@@ -58,7 +58,6 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.ie_last_error.restype = C.c_char_p
     L.ie_set_stream.argtypes = [vp, vp]
     L.ie_sync.argtypes = [vp]
-    L.ie_set_pack_context.argtypes = [vp, vp]
     L.ie_set_quant.argtypes = [vp, u16p, C.c_int]
     L.ie_cos_table.argtypes = [vp, vp]
     L.ie_last_stage_ms.argtypes = [vp, C.c_int, C.POINTER(C.c_float)]
@@ -293,9 +292,6 @@ class Codec:
 
     def close(self):
         if getattr(self, "h", None):
-            if getattr(self, "_pack", None) is not None:
-                self.L.ie_set_pack_context(self.h, None)
-                self._pack = None
             if _host is not None:
                 _host.ieh_release(self.h)
             self.L.ie_destroy(self.h)
@@ -316,13 +312,6 @@ class Codec:
 
     def sync(self):
         self._chk(self.L.ie_sync(self.h))
-
-    def set_pack_context(self, pack: "Codec | None"):
-        """Run this codec's batched Huffman packs on ``pack``'s stream and scratch
-        (ie_set_pack_context): each pack overlaps this codec's next encode.  ``pack`` is kept
-        alive while attached; None detaches."""
-        self._chk(self.L.ie_set_pack_context(self.h, pack.h if pack is not None else None))
-        self._pack = pack
 
     def set_quant(self, q, n: int | None = None):
         q = np.ascontiguousarray(np.asarray(q, dtype=np.uint16).ravel())

@@ -129,12 +129,6 @@ struct ie_ctx {
     size_t cap_gop_tile = 0;
     uint64_t* d_gop_pos = nullptr;
     size_t cap_gop_pos = 0;
-    // ie_set_pack_context: batched Huffman packs run on another context (its stream and scratch),
-    // beside this context's next encode, which waits for them (ev_packdone) before it overwrites
-    // what they read
-    ie_ctx* pack_ctx = nullptr;
-    hipEvent_t ev_packdone = nullptr;
-    bool pack_wait = false;
 };
 
 namespace {
@@ -500,10 +494,6 @@ struct Launch {
 };
 
 int launch_chain(ie_ctx* c, const Launch& L) {
-    if (c->pack_wait) {  // a pack on the pack context may still read the buffers this launch writes
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_packdone, 0));
-        c->pack_wait = false;
-    }
     const int bpt = ie::encode_blocks_per_thread(c->n);
     const Geometry g = geometry(L.w, L.h, c->n, L.nframes, bpt);
     // a launch too small to fill the chip: its tiles reach the look-back together (deep windows)
@@ -1513,7 +1503,6 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_gop_bits);
     (void)hipFree(c->d_gop_tile);
     (void)hipFree(c->d_gop_pos);
-    if (c->ev_packdone) (void)hipEventDestroy(c->ev_packdone);
     pipe_free(c->pipe);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -1528,24 +1517,8 @@ int ie_set_stream(ie_ctx* c, void* s) {
     return IE_OK;
 }
 
-int ie_set_pack_context(ie_ctx* c, ie_ctx* pack) {
-    if (!c || pack == c) return IE_EINVAL;
-    if (pack && pack->device != c->device) return fail(c, IE_EINVAL, "pack context on another device");
-    if (c->pack_ctx && c->pack_ctx != pack) {
-        int r = ie_sync(c->pack_ctx);  // the old pack context's work is checked before it is let go
-        if (r) return fail(c, r, ie_last_error(c->pack_ctx));
-        c->pack_wait = false;
-    }
-    c->pack_ctx = pack;
-    return IE_OK;
-}
-
 int ie_sync(ie_ctx* c) {
     if (!c) return IE_EINVAL;
-    if (c->pack_ctx) {
-        int r = ie_sync(c->pack_ctx);
-        if (r) return fail(c, r, ie_last_error(c->pack_ctx));
-    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     unsigned timeouts = 0;
     int r = read_errors(c, &timeouts, nullptr);  // fails if an unchecked launch timed out
@@ -2049,24 +2022,6 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
                           uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit) {
     if (!c || !in || !n || count <= 0 || !code || !len || !out || !start_bit || (!prefix && prefix_pitch))
         return IE_EINVAL;
-    if (c->pack_ctx) {
-        // on the pack context's stream, after everything issued so far on this one (the input's
-        // encode and histogram); this context's next encode waits for the pack
-        ie_ctx* pc = c->pack_ctx;
-        HIPCHK(c, hipSetDevice(c->device));
-        if (!c->ev_packdone) HIPCHK(c, hipEventCreateWithFlags(&c->ev_packdone, hipEventDisableTiming));
-        HIPCHK(c, hipEventRecord(c->ev_packdone, c->stream));
-        HIPCHK(c, hipStreamWaitEvent(pc->stream, c->ev_packdone, 0));
-        ie_ctx* keep = pc->pack_ctx;
-        pc->pack_ctx = nullptr;  // (no chains of pack contexts)
-        const int r = ie_huffman_pack_batch(pc, in, in_pitch, n, count, code, len, prefix, prefix_pitch, out, out_pitch,
-                                            start_bit, end_bit);
-        pc->pack_ctx = keep;
-        if (r) return fail(c, r, ie_last_error(pc));
-        HIPCHK(c, hipEventRecord(c->ev_packdone, pc->stream));
-        c->pack_wait = true;
-        return IE_OK;
-    }
     c->fused_count = 0;  // the staged tables overwrite the batch scratch
     if (!is_device_ptr(in) || !is_device_ptr(out))
         return fail(c, IE_EINVAL, "batched Huffman input and output must be device memory");

@@ -294,14 +294,28 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
     Probe pr{0, 0, 0};
     if (tid < 64 && chain_pos != 0) pr = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
     const uint32_t nw = (A + 31) >> 5;
-    for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
+    if constexpr (MAXLEN <= 16) {
+        // only the words two threads share need zeros first: every thread's first and end word
+        // (and the word past the image, the store's look-ahead); the words strictly inside a
+        // thread's bits are written whole, without an OR
+        if (mybits) {
+            img[off >> 5] = 0u;
+            img[(off + mybits) >> 5] = 0u;
+        }
+        if (tid == 0) img[nw] = 0u;
+    } else {
+        for (uint32_t w = tid; w < nw + 1; w += kTPB) img[w] = 0u;
+    }
     __syncthreads();
     if (mybits) {
         if constexpr (MAXLEN <= 16) {
             // two codes at a time (<= 32 bits), so at most one completed word per step; bits of
-            // acc above the pending ones are stale and never reach a word (32-bit truncation)
+            // acc above the pending ones are stale and never reach a word (32-bit truncation).
+            // The first completed word may hold the previous thread's bits (OR); later ones are
+            // this thread's alone (plain store); the partial end word is shared with the next.
             uint64_t acc = 0;
             uint32_t n = off & 31u, wi = off >> 5;
+            const uint32_t w0 = wi;
 #pragma unroll
             for (int i = 0; i < NPAIR; i++) {
                 const uint32_t l = (lp[i / 4] >> (8 * (i % 4))) & 0xFFu;
@@ -309,7 +323,8 @@ __global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
                 n += l;
                 if (n >= 32u) {
                     n -= 32u;
-                    atomicOr(&img[wi], uint32_t(acc >> n));
+                    if (wi == w0) atomicOr(&img[wi], uint32_t(acc >> n));
+                    else img[wi] = uint32_t(acc >> n);
                     wi++;
                 }
             }

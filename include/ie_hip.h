@@ -68,14 +68,6 @@ int ie_set_stream(ie_ctx* ctx, void* hip_stream);
  * packs, bit copies) since the last check -- that launch's output is invalid.  Later launches
  * then order their tiles by an atomic ticket.  Call it after a pipeline of asynchronous calls. */
 int ie_sync(ie_ctx* ctx);
-/* Batched Huffman packs (ie_huffman_pack_batch, and the after-encode pipeline that calls it) of
- * ctx run on `pack`'s stream and scratch instead: after everything already issued on ctx's
- * stream, and beside ctx's next encode, which waits for them before it writes.  A pipeline of
- * batches (encode i, histogram i, then the pack of batch i-1) thus overlaps each pack with the
- * next encode.  ie_sync(ctx) also syncs and checks `pack`.  NULL detaches (after syncing the old
- * pack context); `pack` must outlive the attachment.  (No reference counterpart: the reference's
- * Huffman pass is serial, Huffman.cpp:233-344.) */
-int ie_set_pack_context(ie_ctx* ctx, ie_ctx* pack);
 
 /* Quantisation matrix, n x n row-major uint16 (MatrixReader<N>::read, MatrixReader.cpp:65-134;
  * used as double[] via getData, :195-198).  n = 4 or 8 (the reference's compile-time

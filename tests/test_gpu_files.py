@@ -363,22 +363,15 @@ def test_huffman_after_encode_pipeline(codec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("packctx", [False, True], ids=["one_stream", "pack_context"])
 @pytest.mark.parametrize("counted", [False, True], ids=["hist_pass", "counted_encode"])
-def test_huffman_after_encode_pipelined(codec, counted, packctx):
+def test_huffman_after_encode_pipelined(codec, counted):
     """Batches pipelined as in bench.py's C5 step: batch i+1's encode and histogram are issued
     before batch i's trees + pack (two output buffers, histogram slots alternating); every
     image's Huffman-coded file still equals the reference's.  counted: the byte counts come from
-    the encoder itself (ie_encode_images_counted).  pack_context: the packs run on a second
-    context's stream beside the next encode (ie_set_pack_context), at 1080p so they overlap."""
+    the encoder itself (ie_encode_images_counted)."""
     import torch
-    from imageencoder_amd import Codec, stream_bound, write_header
+    from imageencoder_amd import stream_bound, write_header
     n, q, w, h, f, nb = 4, O.read_matrix("matrix.txt", 4), 256, 128, 3, 4
-    if packctx:
-        w, h = 1920, 1080
-        pc = Codec(0)
-        pc.set_stream(torch.cuda.Stream().cuda_stream)
-        codec.set_pack_context(pc)
     codec.set_quant(q, n)
     hdr, hb = write_header(n, q, True, w, h, huffman=True)
     pitch = (stream_bound(w, h, n, 1, hb) + 255) // 256 * 256
@@ -404,12 +397,8 @@ def test_huffman_after_encode_pipelined(codec, counted, packctx):
         pending = b
     sizes[pending] = codec.huffman_finish_after_encode(outs[pending % 2], pitch, f, pending % 2, houts[pending],
                                                        hpitch)
-    try:
-        codec.sync()
-        torch.cuda.synchronize()
-    finally:
-        if packctx:
-            codec.set_pack_context(None)
+    codec.sync()
+    torch.cuda.synchronize()
     for b in range(nb):
         host = houts[b].cpu().numpy()
         for k in range(f):
