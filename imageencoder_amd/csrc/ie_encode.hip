@@ -1261,12 +1261,9 @@ constexpr int kWReg = 1024;  // words per wave region: [4 rows][64 NS blocks] pi
 constexpr int kWTask = 128;  // words per wave: fix-up tasks [64] + results [64]
 constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9] excl, [10] ptail, [11] tail pending, [12] ticket,
                              // [16..17] FP64 task counters, [18..25] small-launch window sums, [26..29] their found flags
-#ifndef IE_W_SROW_ALL
-#define IE_W_SROW_ALL 1  // 1: all 16 FP64 rows in LDS; 0: the structural three (whole blocks read the table)
-#endif
-// FP64 rows in LDS (doubles): P[16][16] then S, rq, qd of every coefficient, or (IE_W_SROW_ALL 0)
-// the rows of the three structural coefficients and their S, rq, qd
-constexpr int kWRows = IE_W_SROW_ALL ? 16 * 16 + 3 * 16 : 3 * 16 + 3 * 3;
+// FP64 rows in LDS (doubles): P[16][16] then S, rq, qd of every coefficient (the structural
+// three alone measured equal: the LDS they would free does not add a tile per CU at 78 VGPRs)
+constexpr int kWRows = 16 * 16 + 3 * 16;
 constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc) * 4 + kWRows * 8;
 
 // Inclusive scan over the 64 lanes of a wave by DPP row shifts and row broadcasts (six VALU).
@@ -1376,11 +1373,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     if constexpr (HIST) hl[tid] = 0u;  // (visible after the first barrier)
     // the FP64 rows and their S, rq, qd: the fix-up reads them from LDS
     for (int i = tid; i < kWRows; i += TPB)
-        srow[i] = !IE_W_SROW_ALL ? (i < 3 * NN ? tab->P[Structural<N>::k[i / NN] * NN + i % NN]
-                                  : i < 3 * NN + 3 ? tab->S[Structural<N>::k[i - 3 * NN]]
-                                  : i < 3 * NN + 6 ? tab->rq[Structural<N>::k[i - 3 * NN - 3]]
-                                  : tab->qd[Structural<N>::k[i - 3 * NN - 6]])
-                : (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
+        srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
                 : (i < NN * NN + 2 * NN) ? tab->rq[i - NN * NN - NN] : tab->qd[i - NN * NN - 2 * NN];
     const TileGeo g = tile_geo<4, 4, TG>(a, t, tid);  // lane l of wave w: group 64 w + l of the tile
     const uint64_t start_bit = a.start_dev ? *a.start_dev : a.start_bit;
@@ -1469,10 +1462,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                 const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
                 const BlockPx<N> px = block_px(b, owner);
                 const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
-                const int y = !IE_W_SROW_ALL ? exact_coef_row<N>(srow + s * NN, srow[3 * NN + s], srow[3 * NN + 3 + s],
-                                                                  srow[3 * NN + 6 + s], px)
-                                             : exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                                 srow[NN * NN + 2 * NN + k], px);
+                const int y = exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                srow[NN * NN + 2 * NN + k], px);
                 res[lane] = (IE_W_DBG & 128) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
                                              : uint32_t(y) & 0xFFFFu;
             }
@@ -1519,9 +1510,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                     const uint32_t tk = task[lane >> 4];
                     const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
                     const BlockPx<N> px = block_px(b, owner);
-                    const int y = !IE_W_SROW_ALL ? exact_coef_row<N>(tab->P + k * NN, tab->S[k], tab->rq[k], tab->qd[k], px)
-                                                 : exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                                     srow[NN * NN + 2 * NN + k], px);
+                    const int y = exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                    srow[NN * NN + 2 * NN + k], px);
                     res[lane] = uint32_t(y) & 0xFFFFu;
                 }
                 wave_sync();

@@ -17,5 +17,6 @@ step hufdec_trace timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-fo
 TAILN=6 step gop timeout -k 10 200 python3 tools/prof_gop.py
 step gop_trace timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/gop -o run -- python3 $R/tools/prof_gop.py
 TAILN=30 step stamps env NFS="1 16" timeout -k 10 300 bash tools/gpu_stamps.sh
-TAILN=40 step pmc timeout -k 10 400 bash tools/gpu_pmc_insts.sh
+TAILN=40 step pmc env LIBS="imageencoder_amd/lib/libie_hip.so imageencoder_amd/lib/var_v1/libie_hip.so" timeout -k 10 400 bash tools/gpu_pmc_insts.sh
+TAILN=6 step ab_single env TESTS=none AB="product r02" ABARGS="--frames 1 --iters 40" timeout -k 10 300 bash tools/gpu_ab.sh
 exit 0
