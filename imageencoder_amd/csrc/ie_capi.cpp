@@ -2236,7 +2236,8 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
     if (!nchunks) return IE_OK;
     // d_walk: [cap] entries, [cap] symbol bases, then 128 words of top-level entries (256 x u32)
     if ((r = ensure(c, c->d_walk, c->cap_walk, 2 * nchunks + 130))) return r;
-    if ((r = ensure(c, c->d_count, c->cap_count, nchunks))) return r;
+    // per-chunk symbol counts, then the walk workgroups' totals (ie::kTPB chunks each)
+    if ((r = ensure(c, c->d_count, c->cap_count, nchunks + (nchunks + ie::kTPB - 1) / ie::kTPB + 1))) return r;
     if ((r = ensure(c, c->d_rtab, c->cap_rtab, ie::huffman_table_rows(nbits, start_bit, chunk_bits) + 2))) return r;
     uint64_t* wk = c->d_walk;
     const size_t cap = (c->cap_walk - 130) / 2;

@@ -44,35 +44,6 @@ __device__ __forceinline__ uint32_t getbits(const uint32_t* W, uint64_t p, int l
     return uint32_t((v << (p & 31)) >> (64 - l));
 }
 
-// exclusive scan of per-chunk counts: one workgroup, each thread owns kScanRun consecutive counts
-// (one block scan per kTPB * kScanRun counts instead of one per kTPB; measured faster than an
-// LDS-transposed coalesced variant)
-constexpr int kScanRun = 32;
-__global__ __launch_bounds__(kTPB) void scan_counts_kernel(const uint32_t* count, uint64_t* base, int n) {
-    __shared__ uint32_t scratch[8];
-    uint64_t carry = 0;  // the same in every thread
-    for (int s = 0; s < n; s += kTPB * kScanRun) {
-        const int i0 = s + int(threadIdx.x) * kScanRun;
-        uint32_t v[kScanRun];
-        uint32_t sum = 0;
-#pragma unroll
-        for (int j = 0; j < kScanRun; j++) {
-            v[j] = (i0 + j < n) ? count[i0 + j] : 0u;
-            sum += v[j];
-        }
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan(sum, scratch, &tot);
-        uint64_t run = carry + ex;
-#pragma unroll
-        for (int j = 0; j < kScanRun; j++) {
-            if (i0 + j < n) base[i0 + j] = run;
-            run += v[j];
-        }
-        carry += tot;
-        __syncthreads();  // scratch is reused by the next strip's scan
-    }
-}
-
 // ---- Huffman decode (Huffman.cpp:354-402; the per-bit tree walk of :190-204) -------------------
 // One lane per chunk of bits decodes symbols with a prefix table until it leaves the chunk; its
 // entry comes from composed transfer tables (the exact parse at the end of this file); a scan of
@@ -95,8 +66,9 @@ struct HufArgs {
     const uint16_t* lut;
     uint64_t* entry;
     uint32_t* count;
+    uint32_t* wgsum;    // [walk workgroups] their chunks' symbol totals
     unsigned* changed;  // [1] invalid code on the emitting walk
-    const uint64_t* base;
+    uint64_t* base;     // symbols before each chunk within its walk workgroup
     uint8_t* out;
     uint16_t* lvl[kRecMaxLevels];  // mode 2: the composition's levels
     int levels;
@@ -138,40 +110,64 @@ __device__ __forceinline__ uint64_t huf_walk(const HufArgs& a, const uint16_t* l
 
 // The counting walk: each chunk from its true entry (its top-level entry through every level's
 // prefix map of the composed transfer tables), symbols counted; the entry is kept for the emit.
+// The workgroup scans its chunks' counts: base[k] = the symbols before chunk k among the
+// workgroup's, wgsum[g] = the workgroup's total (no separate scan launch).
 __global__ __launch_bounds__(kTPB) void huf_walk_kernel(HufArgs a) {
     __shared__ uint16_t l1[1 << kHufL1];
+    __shared__ uint32_t scratch[8];
     huf_l1(a.lut, l1);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= a.nchunks) return;
-    const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
-    int u = k;
-    for (int l = 0; l < a.levels; l++) u /= kHufG;
-    uint32_t x = a.E[u];
-    for (int l = a.levels - 1; l >= 0; l--) {
-        int ul = k;
-        for (int m = 0; m < l; m++) ul /= kHufG;
-        x = a.lvl[l][size_t(ul) * kHufD + x];
+    uint32_t c = 0;
+    if (k < a.nchunks) {
+        const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
+        int u = k;
+        for (int l = 0; l < a.levels; l++) u /= kHufG;
+        uint32_t x = a.E[u];
+        for (int l = a.levels - 1; l >= 0; l--) {
+            int ul = k;
+            for (int m = 0; m < l; m++) ul /= kHufG;
+            x = a.lvl[l][size_t(ul) * kHufD + x];
+        }
+        const uint64_t e = cstart + x;
+        a.entry[k] = e;
+        huf_walk(a, l1, e, cstart + a.chunk_bits, &c, nullptr, false);
+        a.count[k] = c;
     }
-    const uint64_t e = cstart + x;
-    a.entry[k] = e;
-    uint32_t c;
-    huf_walk(a, l1, e, cstart + a.chunk_bits, &c, nullptr, false);
-    a.count[k] = c;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(c, scratch, &tot);
+    if (k < a.nchunks) a.base[k] = ex;
+    if (threadIdx.x == 0) a.wgsum[blockIdx.x] = tot;
+}
+
+// The symbols before workgroup g's chunks: the totals of the workgroups before it, summed by the
+// whole workgroup (every thread receives it).
+__device__ __forceinline__ uint64_t huf_wg_prefix(const uint32_t* wgsum, int g, uint32_t* scratch) {
+    uint64_t part = 0;
+    for (int i = threadIdx.x; i < g; i += kTPB) part += wgsum[i];
+    const uint64_t w = wave_sum64(part);
+    if ((threadIdx.x & 63) == 0) reinterpret_cast<uint64_t*>(scratch)[threadIdx.x >> 6] = w;
+    __syncthreads();
+    const uint64_t* s64 = reinterpret_cast<const uint64_t*>(scratch);
+    return s64[0] + s64[1] + s64[2] + s64[3];
 }
 
 __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
     __shared__ uint16_t l1[1 << kHufL1];
+    __shared__ uint32_t scratch[8];
     huf_l1(a.lut, l1);
+    const uint64_t pre = huf_wg_prefix(a.wgsum, int(blockIdx.x), scratch);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.nchunks) return;
     const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
     uint32_t c;
-    huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, a.out + a.base[k], true);
+    huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, a.out + pre + a.base[k], true);
 }
 
-// total receives the symbol count (device, 1 word) = base[last] + count[last].
-__global__ void huf_total_kernel(const uint64_t* base, const uint32_t* count, int n, uint64_t* total) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) *total = base[n - 1] + count[n - 1];
+// total receives the symbol count (device, 1 word): the sum of the walk's workgroup totals.
+__global__ __launch_bounds__(kTPB) void huf_total_kernel(const uint32_t* wgsum, int nwg, uint64_t* total) {
+    __shared__ uint32_t scratch[8];
+    const uint64_t t = huf_wg_prefix(wgsum, nwg, scratch);
+    if (threadIdx.x == 0) *total = t;
 }
 
 // ---- exact record parse: transfer tables, composed -------------------------------------------
@@ -1065,6 +1061,7 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
     a.lut = lut;
     a.entry = entry;
     a.count = count;
+    a.wgsum = count + nchunks;  // [ceil(nchunks / kTPB)] after the counts (huffman_count_words)
     a.changed = changed;
     a.base = base;
     a.out = out;
@@ -1080,8 +1077,7 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
     a.levels = levels;
     a.E = E;
     hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
-    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), blk, 0, s, count, base, nchunks);
-    hipLaunchKernelGGL(huf_total_kernel, dim3(1), dim3(1), 0, s, base, count, nchunks, total);
+    hipLaunchKernelGGL(huf_total_kernel, dim3(1), blk, 0, s, a.wgsum, int(g.x), total);
     return levels;
 }
 
