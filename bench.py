@@ -58,9 +58,12 @@ WORKLOADS = {
                golden="synU4k_4x4"),
     "c3": dict(w=3840, h=2160, n=8, matrix="matrix8_1.txt", batch=16, resident=64, gen="U", huffman=False,
                golden="synU4k_8x8"),
-    # c4: batch = frames per GPU per step, split into `chunks` pipelined sub-batches
+    # c4: batch = frames per GPU per step, split into `chunks` pipelined sub-batches (2: each rank's
+    # launch of 32 1080p frames is 4 064 tiles, 2.6 rounds of the chip's resident tiles -- 16
+    # frames were 1.3 rounds, 0.197 of HBM against 0.236 -- and the gather of the first still
+    # overlaps the encode of the second)
     "c4": dict(w=1920, h=1080, n=4, matrix="matrix.txt", batch=64, resident=128, gen="U", huffman=False,
-               chunks=4, golden="vidU1080x3_4x4"),
+               chunks=2, golden="vidU1080x3_4x4"),
     "c5": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=True,
                golden="synU4k_4x4_huff"),
 }
@@ -85,7 +88,7 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="frames per launch (default: the workload's)")
     p.add_argument("--resident", type=int, default=None, help="distinct resident frames (default: the workload's)")
     p.add_argument("--chunks", type=int, default=None,
-                   help="C4: pipelined sub-batches per step (default: the workload's, 4)")
+                   help="C4: pipelined sub-batches per step (default: the workload's, 2)")
     p.add_argument("--no-single-frame", dest="single_frame", action="store_false",
                    help="skip timing one-image launches (configs[1] taken literally: one 4K frame per launch)")
     return p.parse_args()
