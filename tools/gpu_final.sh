@@ -14,5 +14,5 @@ TAILN=3 step pytest timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:
 step smoke timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench_default timeout -k 10 400 python bench.py
-for wl in ${WLS:-c3 c4 c5}; do step bench_$wl timeout -k 10 400 python bench.py --workload $wl --steps 10 --warmup 2 --cpu-iters 2; done
+for wl in ${WLS-c3 c4 c5}; do step bench_$wl timeout -k 10 400 python bench.py --workload $wl --steps 10 --warmup 2 --cpu-iters 2; done
 exit 0
