@@ -51,7 +51,7 @@ ROUND = "r04"  # profiles/<ROUND>_traffic_<workload>.json: this round's counter 
 # the dominant kernel of each workload's timed launch (launch_encode: 4x4 FAST over whole 16-byte
 # groups runs encode4w_kernel; 8x8 runs encode_kernel<8>)
 KERNEL = {"c2": "encode4w_kernel<false>", "c3": "encode_kernel<8,false>", "c4": "encode4w_kernel<false>",
-          "c5": "encode4w_kernel<false>"}
+          "c5": "encode4w_kernel<true>"}
 
 WORKLOADS = {
     "c2": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=False,
@@ -371,8 +371,11 @@ def main():
                                     nframes=B, start_bit=hdr_bits, mode=mode, want_sizes=False, count_bytes=True)
             _, g3 = timer.run(enc_counted, 1, args.steps)
             t_cnt = g3 / args.steps
-            extra["counted_encode"] = {"kernel": "encode4w_kernel<true>", "launch_us": round(t_cnt * 1e6, 2),
-                                       "frac": round((B * w * h + out_bytes_per_launch) / t_cnt / 1e9 / HBM_PEAK_GBS, 4)}
+            # the roofline prices the launch the step runs (the counting encoder); the plain encoder
+            # (same kernel without the byte counts) is reported beside it
+            extra["plain_encode"] = {"kernel": "encode4w_kernel<false>", "launch_us": round(enc_s * 1e6, 2),
+                                     "frac": round((B * w * h + out_bytes_per_launch) / enc_s / 1e9 / HBM_PEAK_GBS, 4)}
+            enc_s = t_cnt
             extra["huffman_roofline"] = {
                 "bound": "hbm", "achieved": round(hbytes / (t_h + t_p) / 1e9, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(hbytes / (t_h + t_p) / 1e9 / HBM_PEAK_GBS, 4),

@@ -616,20 +616,26 @@ template <int N, bool EXACT> constexpr int enc_waves() { return (N == 4 && EXACT
 #define IE_ENC_BOUNDS(N, EXACT) __launch_bounds__(kEncTPB, (enc_waves<N, EXACT>()))
 // HIST: count the stored bytes into a per-tile LDS histogram (256 words after the misc area),
 // merged into a.hist[frame] at the end: the Huffman pass's histogram without re-reading the stream.
-struct HistCount {
+// R > 1: R copies of each bin, bin b of lane l at b * R + l % R (the same byte in several lanes of
+// one ds_add no longer serialises on one address)
+template <int R = 1>
+struct HistCountT {
     uint32_t* hl;
     uint64_t limit;  // bytes at stream positions >= limit are padding (the chain's last word)
+    uint32_t lo = 0;  // l % R
+    __device__ __forceinline__ void add(uint32_t b) const { atomicAdd(&hl[b * R + lo], 1u); }
     __device__ __forceinline__ void operator()(uint64_t gw, uint32_t v) const {
         if (limit == ~0ull) {  // (wave-uniform) not the chain's last tile: every byte counts
 #pragma unroll
-            for (int k = 0; k < 4; k++) atomicAdd(&hl[(v >> (8 * k)) & 0xFFu], 1u);
+            for (int k = 0; k < 4; k++) add((v >> (8 * k)) & 0xFFu);
         } else {
 #pragma unroll
             for (int k = 0; k < 4; k++)
-                if (4 * gw + k < limit) atomicAdd(&hl[(v >> (8 * k)) & 0xFFu], 1u);
+                if (4 * gw + k < limit) add((v >> (8 * k)) & 0xFFu);
         }
     }
 };
+using HistCount = HistCountT<1>;
 
 // BB: blocks per thread (4x4: 4; the LDS pixel layout also takes 1 -- measured on one 4K frame,
 // 2 025 tiles of one block per lane took 36 us against 20 us for 506 tiles of four: the longer
@@ -1265,6 +1271,10 @@ constexpr int kWMisc = 32;   // [0..3] wave bits, [4..7] wave head words, [8..9]
 // three alone measured equal: the LDS they would free does not add a tile per CU at 78 VGPRs)
 constexpr int kWRows = 16 * 16 + 3 * 16;
 constexpr int kWLdsBytes = (4 * kWReg + 4 * kWTask + kWMisc) * 4 + kWRows * 8;
+// HIST: copies of the byte histogram (tools/ab.py --op counted, 16 4K frames: counting costs 20.3 us
+// over a launch without it at 1 copy, 15.8 at 4; 8 and 16 copies cost a tile per CU and are slower,
+// two 16-bit bins per word slower still -- the LDS read-modify-write of 112 M byte-adds is the floor)
+constexpr int kWHistRep = 4;
 
 // Inclusive scan over the 64 lanes of a wave by DPP row shifts and row broadcasts (six VALU).
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
@@ -1356,7 +1366,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     uint32_t* const res = task + 64;
     uint32_t* const misc = smem + 4 * kWReg + 4 * kWTask;
     uint32_t* const hl = misc + kWMisc;  // HIST: the tile's byte histogram
-    double* const srow = reinterpret_cast<double*>(misc + kWMisc + (HIST ? 256 : 0));
+    constexpr int HR = kWHistRep, HWORDS = 256 * HR;
+    double* const srow = reinterpret_cast<double*>(misc + kWMisc + (HIST ? HWORDS : 0));
 
     int t;
     if (a.ticket) {
@@ -1370,7 +1381,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     WSTAMP(0);
     WRTSTAMP(14);
     asm volatile("; PHASE w0" ::: "memory");
-    if constexpr (HIST) hl[tid] = 0u;  // (visible after the first barrier)
+    if constexpr (HIST)
+        for (int i = tid; i < HWORDS; i += TPB) hl[i] = 0u;  // (visible after the first barrier)
     // the FP64 rows and their S, rq, qd: the fix-up reads them from LDS
     for (int i = tid; i < kWRows; i += TPB)
         srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
@@ -1737,7 +1749,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
         uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[10]) : 0u;
         // HIST: bytes at or past the chain's last byte are padding
-        const HistCount hc{hl, chain_last ? (start_bit + excl + A + 7) / 8 : ~0ull};
+        const HistCountT<HR> hc{hl, chain_last ? (start_bit + excl + A + 7) / 8 : ~0ull, uint32_t(lane % HR)};
         auto count = [&](uint64_t gw, uint32_t v) {
             if constexpr (HIST) hc(gw, v);
         };
@@ -1790,12 +1802,15 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     }
     if constexpr (HIST) {
         lds_barrier();  // every wave's bytes counted
-        if (hl[tid]) atomicAdd(&a.hist[size_t(frame) * 256 + tid], hl[tid]);
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < HR; r++) c += hl[tid * HR + r];
+        if (c) atomicAdd(&a.hist[size_t(frame) * 256 + tid], c);
     }
 }
 
 void launch_encode4w(const EncArgs& a, hipStream_t s) {
-    if (a.hist) hipLaunchKernelGGL(encode4w_kernel<true>, dim3(a.ntiles), dim3(256), kWLdsBytes + 1024, s, a, a.tab);
+    if (a.hist) hipLaunchKernelGGL(encode4w_kernel<true>, dim3(a.ntiles), dim3(256), kWLdsBytes + 1024 * kWHistRep, s, a, a.tab);
     else hipLaunchKernelGGL(encode4w_kernel<false>, dim3(a.ntiles), dim3(256), kWLdsBytes, s, a, a.tab);
 }
 
