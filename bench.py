@@ -58,12 +58,13 @@ WORKLOADS = {
                golden="synU4k_4x4"),
     "c3": dict(w=3840, h=2160, n=8, matrix="matrix8_1.txt", batch=16, resident=64, gen="U", huffman=False,
                golden="synU4k_8x8"),
-    # c4: batch = frames per GPU per step, split into `chunks` pipelined sub-batches (2: each rank's
-    # launch of 32 1080p frames is 4 064 tiles, 2.6 rounds of the chip's resident tiles -- 16
-    # frames were 1.3 rounds, 0.197 of HBM against 0.236 -- and the gather of the first still
-    # overlaps the encode of the second)
+    # c4: batch = frames per GPU per step, split into `chunks` pipelined sub-batches (1: each rank's
+    # launch is all 64 of its 1080p frames, 8 128 tiles, 5.3 rounds of the chip's resident tiles --
+    # 0.260 of HBM against 0.234 for two 32-frame launches and 0.197 for four 16-frame ones; the
+    # step at N = 1 is within 1 %, and at N > 1 rank 0's ingress of the other ranks' streams, not
+    # the encode the gather could overlap, sets it)
     "c4": dict(w=1920, h=1080, n=4, matrix="matrix.txt", batch=64, resident=128, gen="U", huffman=False,
-               chunks=2, golden="vidU1080x3_4x4"),
+               chunks=1, golden="vidU1080x3_4x4"),
     "c5": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=True,
                golden="synU4k_4x4_huff"),
 }

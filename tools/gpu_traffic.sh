@@ -10,7 +10,7 @@ BOPT="--steps 6 --warmup 1 --no-cpu --no-single-frame --no-e2e --no-decode --no-
 for wl in ${WLS:-c2 c3 c4 c5}; do
   case $wl in
     c3) K=encode_kernel; G="";;
-    c4) K="encode4w_kernel<false>"; G=1040384;;  # the 32-frame sub-batch launches: 32 x ceil(32400 groups / 256) tiles x 256 threads
+    c4) K="encode4w_kernel<false>"; G=2080768;;  # the 64-frame launches: 64 x ceil(32400 groups / 256) tiles x 256 threads
     c5) K="encode4w_kernel<true>"; G="";;        # the counting encoder the C5 step runs
     *)  K="encode4w_kernel<false>"; G="";;
   esac
