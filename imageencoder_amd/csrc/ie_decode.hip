@@ -196,6 +196,7 @@ __global__ __launch_bounds__(kTPB) void huf_total_kernel(const uint32_t* wgsum, 
 //                      reference's order (algo.cpp:343-363), +128, clamp, truncate
 //                      (Block.cpp:100-107).
 constexpr uint32_t kNoOwner = 0xFFFFu;
+constexpr uint32_t kRoot = 0x8000u;  // table pass: a walk result that is an exit, not an owner
 
 // bits [p, p+l) of the LDS stream copy L (MSB-first words), l <= 32, p relative to the copy
 __device__ __forceinline__ uint32_t lbits(const uint32_t* L, uint32_t p, int l) {
@@ -545,11 +546,12 @@ __device__ __forceinline__ uint32_t next_valid(const uint32_t* VB, const uint16_
 }
 
 __host__ __device__ constexpr int rec_table2_words(uint32_t C, int D, int tm, int hbits) {
-    // L (stream words, 16-byte aligned staging: +4), VB, claims, then u16 res / tgt, the u16 walk
-    // list (walk ids: the start position follows from the id, except a chunk's v*), the chunks'
-    // v* positions and the u16 next-valid-word table (tm CW + 1 entries)
+    // L (stream words, 16-byte aligned staging: +4), VB, claims, then the u16 walk results (an
+    // exit with kRoot set, or the owner a merged walk joined), the u16 walk list (walk ids: the
+    // start position follows from the id, except a chunk's v*), the chunks' v* positions and the
+    // u16 next-valid-word table (tm CW + 1 entries)
     return (rec_table_stream_words(uint32_t(tm) * C) + 4 + 3) / 4 * 4 + tm * int(C >> 5) + (1 << hbits) +
-           tm * (D + 1) + (tm * (D + 1) + 1) / 2 + tm + (tm * int(C >> 5) + 2) / 2;
+           2 * ((tm * (D + 1) + 1) / 2) + tm + (tm * int(C >> 5) + 2) / 2;
 }
 
 template <int N>
@@ -574,10 +576,12 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     uint32_t* VB = Ls + SW;
     uint32_t* H = VB + tm * int(CW);
     const uint32_t HM = (1u << a.hbits) - 1u;
+    // res[id]: kRoot | the exit of a walk that left its chunk, or the id of the walk it merged into
+    // (ids < D1 * tm < kRoot; one u16 per walk keeps a wave in 4.8 KB of LDS: 32 waves per CU)
     uint16_t* res = reinterpret_cast<uint16_t*>(H + HM + 1);
-    uint16_t* tgt = res + tm * D1;
-    uint16_t* wl = reinterpret_cast<uint16_t*>(H + HM + 1 + tm * D1);  // after res + tgt (tm * D1 words together)
-    uint32_t* vst = H + HM + 1 + tm * D1 + (tm * D1 + 1) / 2;          // [tm] every chunk's v* position
+    const int RW = (tm * D1 + 1) / 2;                                  // words of res, and of wl
+    uint16_t* wl = reinterpret_cast<uint16_t*>(H + HM + 1 + RW);
+    uint32_t* vst = H + HM + 1 + 2 * RW;                               // [tm] every chunk's v* position
     uint16_t* NZ = reinterpret_cast<uint16_t*>(vst + tm);
     const RecSpan sp = rec_span(a);
     const uint64_t c0 = sp.start + uint64_t(k0) * C;
@@ -669,25 +673,26 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         uint32_t nxt = 0, p = 0, id = 0, ce = 0, nsteps = 0, wsteps = 0, rsteps = 0;
         bool act = false;
         for (;;) {
-            const uint64_t need = __ballot(!act);
-            if (!act) {
-                const uint32_t r = nxt + __builtin_amdgcn_mbcnt_hi(uint32_t(need >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(need), 0u));
-                if (r < nw) {
-                    id = wl[r];
-                    const uint32_t j = id / D1, d = id - j * D1;
-                    p = (d < uint32_t(D)) ? j * C + d : vst[j];
-                    ce = (j + 1u) * C;
-                    act = true;
+            if (nxt < nw) {  // (wave-uniform) walks left in the list: idle lanes take the next ones
+                const uint64_t need = __ballot(!act);
+                if (!act) {
+                    const uint32_t r = nxt + __builtin_amdgcn_mbcnt_hi(uint32_t(need >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(need), 0u));
+                    if (r < nw) {
+                        id = wl[r];
+                        const uint32_t j = id / D1, d = id - j * D1;
+                        p = (d < uint32_t(D)) ? j * C + d : vst[j];
+                        ce = (j + 1u) * C;
+                        act = true;
+                    }
                 }
+                nxt += uint32_t(__popcll(need));
             }
-            nxt += uint32_t(__popcll(need));
             if (!__ballot(act)) break;
             if (act) {
                 nsteps++;
                 wsteps++;
                 if (p >= ce) {  // left the chunk
-                    res[id] = uint16_t(p - ce);
-                    tgt[id] = uint16_t(kNoOwner);
+                    res[id] = uint16_t(kRoot | (p - ce));
                     act = false;
                     rsteps += wsteps;  // (profiling: steps of walks that reached the chunk's end)
                     wsteps = 0;
@@ -701,7 +706,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
                     const uint32_t o = atomicCAS(&H[(p * 2654435761u) >> 16 & HM], 0xFFFFFFFFu, key);
                     const uint32_t own = (o != 0xFFFFFFFFu && (o >> 16) == p) ? (o & 0xFFFFu) : kNoOwner;
                     if (own != kNoOwner) {
-                        tgt[id] = uint16_t(own);
+                        res[id] = uint16_t(own);
                         act = false;
                         wsteps = 0;
                     } else {
@@ -727,13 +732,15 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     }
     __syncthreads();
     wstamp(4);
-    // 4. merged walks take their root's exit (read-only chases; only non-roots are written)
+    // 4. merged walks take their root's exit.  A lane may overwrite an entry another lane's chase
+    // passes through: it writes the root's own value (kRoot | exit), so that chase ends there with
+    // the same answer.
     for (uint32_t r = lane; r < nw; r += 64) {
         const uint32_t id = wl[r];
-        uint32_t x = tgt[id];
-        if (x == kNoOwner) continue;
-        for (uint32_t y = tgt[x]; y != kNoOwner; y = tgt[x]) x = y;
-        res[id] = res[x];
+        uint32_t x = res[id];
+        if (x & kRoot) continue;
+        while (!(x & kRoot)) x = res[x];
+        res[id] = uint16_t(x);
     }
     __syncthreads();
     // 5. every entry: its walk's exit
@@ -749,7 +756,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
             if (nv >= ce) {
                 out = nv - ce;
             } else {
-                out = res[j * D1 + min(nv - cs, uint32_t(D))];
+                out = res[j * D1 + min(nv - cs, uint32_t(D))] & ~kRoot;
             }
         }
         T[e] = uint16_t(out);
