@@ -672,22 +672,20 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     {
         uint32_t nxt = 0, p = 0, id = 0, ce = 0, nsteps = 0, wsteps = 0, rsteps = 0;
         bool act = false;
-        for (;;) {
-            if (nxt < nw) {  // (wave-uniform) walks left in the list: idle lanes take the next ones
-                const uint64_t need = __ballot(!act);
-                if (!act) {
-                    const uint32_t r = nxt + __builtin_amdgcn_mbcnt_hi(uint32_t(need >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(need), 0u));
-                    if (r < nw) {
-                        id = wl[r];
-                        const uint32_t j = id / D1, d = id - j * D1;
-                        p = (d < uint32_t(D)) ? j * C + d : vst[j];
-                        ce = (j + 1u) * C;
-                        act = true;
-                    }
+        // (a) while the list lasts: idle lanes take the next walks, every step claims its position
+        while (nxt < nw) {  // (wave-uniform)
+            const uint64_t need = __ballot(!act);
+            if (!act) {
+                const uint32_t r = nxt + __builtin_amdgcn_mbcnt_hi(uint32_t(need >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(need), 0u));
+                if (r < nw) {
+                    id = wl[r];
+                    const uint32_t j = id / D1, d = id - j * D1;
+                    p = (d < uint32_t(D)) ? j * C + d : vst[j];
+                    ce = (j + 1u) * C;
+                    act = true;
                 }
-                nxt += uint32_t(__popcll(need));
             }
-            if (!__ballot(act)) break;
+            nxt += uint32_t(__popcll(need));
             if (act) {
                 nsteps++;
                 wsteps++;
@@ -715,6 +713,19 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
                     }
                 }
             }
+        }
+        // (b) the list is empty: the walks still going (a chunk's true path and the odd wrong-phase
+        // survivor, which would meet it later) run to their chunk's end without claims -- no new
+        // walk can merge into them, so a claim would only stop a survivor a few steps early, and
+        // each step is a third cheaper without one
+        if (act) {
+            while (p < ce) {
+                nsteps++;
+                wsteps++;
+                p = next_valid<N>(VB, NZ, p + rec_len_head<N>(lbits(L, s0 + p, 20), a.rle), ce);
+            }
+            res[id] = uint16_t(kRoot | (p - ce));
+            rsteps += wsteps;
         }
 #if IE_PROFILE
         if (ws) {
