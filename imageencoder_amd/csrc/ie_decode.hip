@@ -673,6 +673,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         uint32_t nxt = 0, p = 0, id = 0, ce = 0, nsteps = 0, wsteps = 0, rsteps = 0;
         bool act = false;
         // (a) while the list lasts: idle lanes take the next walks, every step claims its position
+        // (claiming 4-16 steps longer measured equal or slower)
         while (nxt < nw) {  // (wave-uniform)
             const uint64_t need = __ballot(!act);
             if (!act) {
