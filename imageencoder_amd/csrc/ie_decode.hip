@@ -217,6 +217,14 @@ __device__ __forceinline__ uint32_t rec_len_head(uint32_t head, int rle) {
     const uint32_t lw = (head & 0xFFFFu) >> (16 - bl);
     return lw <= uint32_t(NN) ? 4u + bl * (lw + 1u) : 1u;
 }
+// rec_len_head without branches (the walk loops: every lane runs it every step)
+template <int N>
+__device__ __forceinline__ uint32_t rec_len_sel(uint32_t head, int rle) {
+    constexpr uint32_t NN = N * N;
+    const uint32_t bl = head >> 16;
+    const uint32_t lw = rle ? ((head & 0xFFFFu) >> (16u - bl)) : NN - 1u;  // (bl = 0: shifted out)
+    return (bl != 0u && lw <= NN) ? 4u + bl * (lw + 1u) : 1u;
+}
 // length of the record at p, 0 if no record can start there
 template <int N>
 __device__ __forceinline__ uint32_t rec_len(const uint32_t* L, uint32_t p, int rle) {
@@ -719,11 +727,20 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         // survivor, which would meet it later) run to their chunk's end without claims -- no new
         // walk can merge into them, so a claim would only stop a survivor a few steps early, and
         // each step is a third cheaper without one
+        const uint32_t CWm = uint32_t(m) * CW - 1u;  // the last bitmap word
         if (act) {
             while (p < ce) {
                 nsteps++;
                 wsteps++;
-                p = next_valid<N>(VB, NZ, p + rec_len_head<N>(lbits(L, s0 + p, 20), a.rle), ce);
+                p += rec_len_sel<N>(lbits(L, s0 + p, 20), a.rle);
+                // next_valid without branches: the bitmap word, the next non-empty word and that
+                // word are all read (the last read is needed only past an empty word)
+                const uint32_t wi = min(p >> 5, CWm), nz = NZ[wi + 1];
+                const uint32_t mk = VB[wi] & (0xFFFFFFFFu << (p & 31u));
+                const uint32_t m2 = VB[min(nz, CWm)];
+                const uint32_t q = mk ? (wi << 5) + uint32_t(__builtin_ctz(mk))
+                                      : (nz < (ce >> 5) ? (nz << 5) + uint32_t(__builtin_ctz(m2)) : ce);
+                p = p >= ce ? p : q;
             }
             res[id] = uint16_t(kRoot | (p - ce));
             rsteps += wsteps;
