@@ -553,6 +553,19 @@ __device__ __forceinline__ uint32_t next_valid(const uint32_t* VB, const uint16_
     return (wi << 5) + uint32_t(__builtin_ctz(msk));
 }
 
+// next_valid without branches, for the loops every lane runs: the bitmap word, the next non-empty
+// word and that word's bits are all read (the last only matters past an empty word); word
+// indices are clamped to the chunk's last bitmap word, so every read stays inside the chunk.
+__device__ __forceinline__ uint32_t next_valid_sel(const uint32_t* VB, const uint16_t* NZ, uint32_t p, uint32_t ce) {
+    const uint32_t cw = (ce >> 5) - 1u;  // the chunk's last bitmap word
+    const uint32_t wi = min(p >> 5, cw), nz = NZ[wi + 1];
+    const uint32_t mk = VB[wi] & (0xFFFFFFFFu << (p & 31u));
+    const uint32_t m2 = VB[min(uint32_t(nz), cw)];
+    const uint32_t q = mk ? (wi << 5) + uint32_t(__builtin_ctz(mk))
+                          : (nz <= cw ? (uint32_t(nz) << 5) + uint32_t(__builtin_ctz(m2)) : ce);
+    return p >= ce ? p : q;
+}
+
 __host__ __device__ constexpr int rec_table2_words(uint32_t C, int D, int tm, int hbits) {
     // L (stream words, 16-byte aligned staging: +4), VB, claims, then the u16 walk results (an
     // exit with kRoot set, or the owner a merged walk joined), the u16 walk list (walk ids: the
@@ -727,20 +740,11 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
         // survivor, which would meet it later) run to their chunk's end without claims -- no new
         // walk can merge into them, so a claim would only stop a survivor a few steps early, and
         // each step is a third cheaper without one
-        const uint32_t CWm = uint32_t(m) * CW - 1u;  // the last bitmap word
         if (act) {
             while (p < ce) {
                 nsteps++;
                 wsteps++;
-                p += rec_len_sel<N>(lbits(L, s0 + p, 20), a.rle);
-                // next_valid without branches: the bitmap word, the next non-empty word and that
-                // word are all read (the last read is needed only past an empty word)
-                const uint32_t wi = min(p >> 5, CWm), nz = NZ[wi + 1];
-                const uint32_t mk = VB[wi] & (0xFFFFFFFFu << (p & 31u));
-                const uint32_t m2 = VB[min(nz, CWm)];
-                const uint32_t q = mk ? (wi << 5) + uint32_t(__builtin_ctz(mk))
-                                      : (nz < (ce >> 5) ? (nz << 5) + uint32_t(__builtin_ctz(m2)) : ce);
-                p = p >= ce ? p : q;
+                p = next_valid_sel(VB, NZ, p + rec_len_sel<N>(lbits(L, s0 + p, 20), a.rle), ce);
             }
             res[id] = uint16_t(kRoot | (p - ce));
             rsteps += wsteps;
@@ -781,7 +785,7 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
             out = d - C;
         } else {
             const uint32_t cs = j * C, ce = cs + C;
-            const uint32_t nv = next_valid<N>(VB, NZ, cs + d, ce);
+            const uint32_t nv = next_valid_sel(VB, NZ, cs + d, ce);
             if (nv >= ce) {
                 out = nv - ce;
             } else {
