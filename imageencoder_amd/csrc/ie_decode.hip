@@ -730,8 +730,8 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
                         act = false;
                         wsteps = 0;
                     } else {
-                        p += rec_len_head<N>(head, a.rle);  // p is valid: a record starts here
-                        p = next_valid<N>(VB, NZ, p, ce);
+                        // (p is valid: a record starts here)
+                        p = next_valid_sel(VB, NZ, p + rec_len_sel<N>(head, a.rle), ce);
                     }
                 }
             }
@@ -865,7 +865,7 @@ __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
         uint16_t* pos = a.pos + size_t(k) * kRecPosCap;
         uint32_t p = cs + x;
         while (p < ce) {
-            const uint32_t l = rec_len_head<N>(lbits(L, p, 20), a.rle);
+            const uint32_t l = rec_len_sel<N>(lbits(L, p, 20), a.rle);
             if (l > 1u) {
                 if (R < uint32_t(kRecPosCap)) pos[R] = uint16_t(p - cb);
                 R++;
