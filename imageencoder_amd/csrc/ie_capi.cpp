@@ -295,6 +295,33 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
         }
     }
 
+    // 4x4 matrix-pipe plan (quot4j): G[k][m] = S/q * the row and column basis factors of term m
+    if (n == 4) {
+        const double K2 = std::cos(M_PI / 8.0), K4 = std::cos(M_PI / 4.0), K6 = std::cos(3.0 * M_PI / 8.0);
+        auto f = [&](int u, int m) -> double {  // factor of basis dct4j_b(u, m) in 1-D row u
+            if (u == 0) return 1.0;
+            if (u == 2) return K4;
+            if (u == 1) return m == 0 ? K2 : K6;
+            return m == 0 ? K6 : -K2;
+        };
+        for (int u = 0; u < 4; u++)
+            for (int v = 0; v < 4; v++) {
+                int m = 0;
+                for (int a = 0; a < ie::dct4j_nb(u); a++)
+                    for (int bb = 0; bb < ie::dct4j_nb(v); bb++) T->plan4j.G[4 * u + v][m++] = float(sq[4 * u + v] * f(u, a) * f(v, bb));
+            }
+        static const int B[4][4] = {{1, 1, 1, 1}, {1, -1, -1, 1}, {1, 0, 0, -1}, {0, 1, -1, 0}};
+        for (int l = 0; l < 64; l++) {
+            const int r = l & 31, h = l >> 5, rho = (r & 3) + 4 * (r >> 3), hr = (r >> 2) & 1;
+            for (int w = 0; w < 4; w++) T->mfma_w[l][w] = 0u;
+            if (h != hr) continue;
+            for (int j = 0; j < 16; j++) {
+                const int c = B[rho >> 2][j >> 2] * B[rho & 3][j & 3];
+                T->mfma_w[l][j >> 2] |= uint32_t(uint8_t(int8_t(c))) << (8 * (j & 3));
+            }
+        }
+    }
+
     // tracked run of the kernel's transform on raw pixels
     std::vector<Trk> b(nn);
     for (int k = 0; k < nn; k++) {
@@ -304,6 +331,16 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
         b[k].integ = true;
     }
     TrkOp op{nn};
+    // the matrix-pipe form: the sixteen J exact (pixels - 128), then quot4j's FP32 stage
+    std::vector<Trk> bj(nn);
+    if (n == 4) {
+        std::vector<Trk> xs(b), J(nn);
+        for (int k = 0; k < nn; k++) xs[k].c0 = -128.0;
+        ie::dct4j_ints(xs.data(), J.data(), op);
+        for (int k = 0; k < nn; k++)
+            if (!J[k].integ || J[k].E != 0.0) return false;  // the integer stage must be exact
+        ie::quot4j(J.data(), bj.data(), T->plan4j, op);
+    }
     if (n == 4) ie::quot4(b.data(), T->plan4, op);
     else ie::quot8(b.data(), T->dct, T->g, op);
     // Largest record: |Q_k| <= 128 * sum_ij |S_k P_k[ij]| / q_k (|x| <= 128), so bl <= the widest
@@ -330,34 +367,40 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
         }
     }
     bool ok = true;
-    T->dc_exact = 0;
-    T->lim_min = 0.5f;
-    for (int k = 0; k < nn; k++) {
-        const Trk& t = b[k];
-        double dev = 0.0, amax = 0.0, sa = 0.0;
-        for (int m = 0; m < nn; m++) {
-            const double ref = sq[k] * T->P[k * nn + m];
-            dev += std::fabs(t.a[m] - ref);
-            amax = std::max(amax, std::fabs(ref));
-            sa += t.a[m];
+    // per coefficient of one tracked transform: its tie limit (lim), the bound (thr), whether the
+    // DC quotient is exact, and the loosest limit of the non-structural coefficients (lim_min)
+    auto limits = [&](const std::vector<Trk>& tv, float* lim, float* thr, float* lim_min, int* dc_exact, float g0) {
+        *dc_exact = 0;
+        *lim_min = 0.5f;
+        for (int k = 0; k < nn; k++) {
+            const Trk& t = tv[k];
+            double dev = 0.0, amax = 0.0, sa = 0.0;
+            for (int m = 0; m < nn; m++) {
+                const double ref = sq[k] * T->P[k * nn + m];
+                dev += std::fabs(t.a[m] - ref);
+                amax = std::max(amax, std::fabs(ref));
+                sa += t.a[m];
+            }
+            if (dev > 1e-5 * (amax + 1e-30) * nn) ok = false;  // FP32 constants differ by ~1e-7 relative
+            const double bound = t.E + 128.0 * dev + std::fabs(t.c0 + 128.0 * sa) + 1e-9;
+            // coefficient 0: an integer sum (minus 128*N*N) scaled by a power of two is exact in FP32,
+            // and the reference computes it exactly too (c[0][*] = 1, C(0)^2 = 1/4, q a power of two)
+            if (k == 0 && t.E == 0.0 && double(g0) == sq[0] && TrkOp::is_pow2(sq[0])) {
+                if (thr) thr[k] = -1.0f;
+                lim[k] = 1.0f;  // never flagged
+                *dc_exact = 1;
+            } else {
+                if (thr) thr[k] = float(2.0 * bound);
+                lim[k] = float(0.5 - 2.0 * bound);
+                // the structural coefficients (0,N/2), (N/2,0), (N/2,N/2) are flagged one by one
+                const int h = n / 2;
+                const bool structural = (k == h) || (k == h * n) || (k == h * n + h);
+                if (!structural) *lim_min = std::min(*lim_min, lim[k]);
+            }
         }
-        if (dev > 1e-5 * (amax + 1e-30) * nn) ok = false;  // FP32 constants differ by ~1e-7 relative
-        const double bound = t.E + 128.0 * dev + std::fabs(t.c0 + 128.0 * sa) + 1e-9;
-        // coefficient 0: an integer sum (minus 128*N*N) scaled by a power of two is exact in FP32,
-        // and the reference computes it exactly too (c[0][*] = 1, C(0)^2 = 1/4, q a power of two)
-        if (k == 0 && t.E == 0.0 && double(T->g[0]) == sq[0] && TrkOp::is_pow2(sq[0])) {
-            T->thr[k] = -1.0f;
-            T->lim[k] = 1.0f;  // never flagged
-            T->dc_exact = 1;
-        } else {
-            T->thr[k] = float(2.0 * bound);
-            T->lim[k] = float(0.5 - 2.0 * bound);
-            // the structural coefficients (0,N/2), (N/2,0), (N/2,N/2) are flagged one by one
-            const int h = n / 2;
-            const bool structural = (k == h) || (k == h * n) || (k == h * n + h);
-            if (!structural) T->lim_min = std::min(T->lim_min, T->lim[k]);
-        }
-    }
+    };
+    limits(b, T->lim, T->thr, &T->lim_min, &T->dc_exact, T->g[0]);
+    if (n == 4) limits(bj, T->lim4j, nullptr, &T->lim_min4j, &T->dc_exact4j, T->plan4j.G[0][0]);
     return ok;
 }
 

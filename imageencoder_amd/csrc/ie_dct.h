@@ -125,6 +125,65 @@ __host__ __device__ inline void quot4(T* b, const Dct4Plan& P, const Op& op) {
     }
 }
 
+// N = 4 on the matrix pipe (encode4p_kernel).  The 1-D DCT rows are integer combinations of four
+// basis vectors -- e0 = (1,1,1,1), e2 = (1,-1,-1,1), o0 = (1,0,0,-1), o1 = (0,1,-1,0):
+//   row u=0: e0;  u=2: K4 e2;  u=1: K2 o0 + K6 o1;  u=3: K6 o0 - K2 o1      (Kk = cos(k pi/16))
+// so D[u][v] = C(u)C(v) sum_ij c[u][i] c[v][j] x[i][j] (algo.cpp:309-331) is a combination of the
+// sixteen INTEGER sums J[4 ia + ib] = sum_ij B_ia(i) B_ib(j) (x[i][j] - 128) with 1, 2 or 4
+// terms.  The device forms every J exactly in one v_mfma_i32_32x32x32_i8 per 64 blocks (pixels as
+// signed bytes x ^ 0x80 = x - 128, the {-1,0,1} pattern as the other operand); quot4j is the FP32
+// stage after it: t[uv] = sum_m G[uv][m] J[m-th term], one mul and up to three fmas per
+// coefficient (36 operations), G = S(uv)/q(uv) * the basis factors, each rounded once on the host.
+// dct4j_ints is the integer stage in plain arithmetic (the host's tracked run; exact either way).
+struct Dct4JPlan {
+    float G[16][4];  // [u*4+v][term]: terms (ia, ib) in the order of dct4j_terms
+};
+// the row (or column) basis indices of frequency u and how many there are
+__host__ __device__ constexpr int dct4j_nb(int u) { return (u & 1) ? 2 : 1; }
+__host__ __device__ constexpr int dct4j_b(int u, int m) { return (u & 1) ? 2 + m : (u >> 1); }
+
+template <class T, class Op>
+__host__ __device__ inline void dct4j_ints(const T* x, T* J, const Op& op) {
+    T R[4][4];  // R[i][ib]: row i against column basis ib
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const T s0 = op.add(x[4 * i + 0], x[4 * i + 3]), s1 = op.add(x[4 * i + 1], x[4 * i + 2]);
+        R[i][2] = op.sub(x[4 * i + 0], x[4 * i + 3]);
+        R[i][3] = op.sub(x[4 * i + 1], x[4 * i + 2]);
+        R[i][0] = op.add(s0, s1);
+        R[i][1] = op.sub(s0, s1);
+    }
+#pragma unroll
+    for (int ib = 0; ib < 4; ib++) {
+        const T s0 = op.add(R[0][ib], R[3][ib]), s1 = op.add(R[1][ib], R[2][ib]);
+        J[4 * 2 + ib] = op.sub(R[0][ib], R[3][ib]);
+        J[4 * 3 + ib] = op.sub(R[1][ib], R[2][ib]);
+        J[4 * 0 + ib] = op.add(s0, s1);
+        J[4 * 1 + ib] = op.sub(s0, s1);
+    }
+}
+
+template <class T, class Op, class Plan = Dct4JPlan>
+__host__ __device__ inline void quot4j(const T* J, T* t, const Plan& P, const Op& op) {
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int k = 4 * u + v;
+            T acc = op.mul(J[4 * dct4j_b(u, 0) + dct4j_b(v, 0)], P.G[k][0]);
+            int m = 1;
+#pragma unroll
+            for (int a = 0; a < dct4j_nb(u); a++)
+#pragma unroll
+                for (int b = 0; b < dct4j_nb(v); b++) {
+                    if (a == 0 && b == 0) continue;
+                    acc = op.fma(J[4 * dct4j_b(u, a) + dct4j_b(v, b)], P.G[k][m], acc);
+                    m++;
+                }
+            t[k] = acc;
+        }
+}
+
 // N = 8: the separable butterfly (dct2d<8>), the exact DC level shift, then the scale g.
 template <class T, class Op>
 __host__ __device__ inline void quot8(T* b, const DctConsts& k, const float* g, const Op& op) {

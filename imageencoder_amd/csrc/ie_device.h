@@ -22,6 +22,16 @@ struct EncTables {
     float lim_min;  // min of lim[k] over the non-structural coefficients: one compare per block
     int dc_exact;   // t[0] is exact in FP32 (q[0] a power of two): round it directly
     int rec_bits;   // largest record (bits) any block can produce with this matrix: sizes the tile image
+    // 4x4 on the matrix pipe (encode4p_kernel, quot4j in ie_dct.h): the FP32 stage's constants, its
+    // own tie limits (the tracked run of quot4j), and the i8 A fragment of every lane: lane l =
+    // (r = l & 31, h = l >> 5) holds in byte 4i + j the weight of pixel (i, j) in J[rho], rho =
+    // (r & 3) + 4 (r >> 3), when h == (r >> 2) & 1, else 0 -- so D register rho of a lane is J[rho]
+    // of the lane's OWN block (C/D row = (reg & 3) + 8 (reg >> 2) + 4 h).
+    Dct4JPlan plan4j;
+    float lim4j[16];
+    float lim_min4j;
+    int dc_exact4j;
+    uint32_t mfma_w[64][4];
     // the structural coefficients' rows P[k_s][*] (s = 0..2), then S, rq, qd of the three: the
     // fix-up's LDS copy, one contiguous block (3*NN + 9 doubles)
     double srow[3 * 64 + 9];
@@ -47,9 +57,10 @@ inline FastDiv make_fastdiv(uint32_t d) {
     f.mul = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << f.shr) - d)) / d + 1);
     return f;
 }
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-    return (__umulhi(n, f.mul) + n) >> f.shr;
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mul, uint32_t shr) {
+    return (__umulhi(n, mul) + n) >> shr;
 }
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return fdiv(n, f.mul, f.shr); }
 
 // One encode launch.  Tiles (workgroups) never straddle frames; a "chain" is the sequence of
 // tiles whose bit offsets accumulate: the whole batch (concatenated stream) or one frame

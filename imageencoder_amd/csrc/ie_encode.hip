@@ -557,18 +557,18 @@ struct TileGeo {
     int nblk, byi, bx0;  // blocks of this thread's group (nblk = 0: none)
 };
 
-template <int N, int BPT = Geo<N>::BPT, int TG = kEncTPB>
-__device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
+template <int N, int BPT = Geo<N>::BPT, int TG = kEncTPB, class Args = EncArgs>
+__device__ __forceinline__ TileGeo tile_geo(const Args& a, int t, int tid) {
     TileGeo g;
     // Independent images interleave their tiles (frame = t % nframes), so every frame's chain
     // advances together; a concatenated stream keeps chain order = tile order.
     // (wave-uniform divisions by launch constants: multiply-highs, FastDiv)
     if (a.segmented) {
-        g.tif = int(fdiv(uint32_t(t), a.div_frames));
+        g.tif = int(fdiv(uint32_t(t), a.div_frames.mul, a.div_frames.shr));
         g.frame = t - g.tif * a.nframes;
         g.step = a.nframes;
     } else {
-        g.frame = int(fdiv(uint32_t(t), a.div_tpf));
+        g.frame = int(fdiv(uint32_t(t), a.div_tpf.mul, a.div_tpf.shr));
         g.tif = t - g.frame * a.tiles_per_frame;
         g.step = 1;
     }
@@ -576,7 +576,7 @@ __device__ __forceinline__ TileGeo tile_geo(const EncArgs& a, int t, int tid) {
     // group gi = base + tid: the division by gpr is split into a wave-uniform (scalar) part and a
     // per-lane remainder r < gpr + kEncTPB, divided by a multiply-high with ceil(2^32 / gpr)
     const int base = g.tif * TG;  // (TG groups per tile; tid: the thread's group within it)
-    const int q0 = int(fdiv(uint32_t(base), a.div_gpr)), r0 = base - q0 * a.gpr;
+    const int q0 = int(fdiv(uint32_t(base), a.div_gpr.mul, a.div_gpr.shr)), r0 = base - q0 * a.gpr;
     const uint32_t r = uint32_t(r0 + tid);
     const uint32_t dq = (a.gpr == 1) ? r : __umulhi(r, a.gpr_magic);  // (2^32 does not fit the magic)
     const int gi = base + tid;
@@ -1809,7 +1809,557 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     }
 }
 
+// =============================================================================================
+// encode4p_kernel -- encode4w_kernel's tile (wave-local slots, the same emission, look-back and
+// store), made PERSISTENT and with the integer half of the transform on the matrix pipe.
+//   * Persistent: the grid is the number of tiles the chip holds at once (the occupancy API's
+//     answer, launch_encode4w); workgroup g walks tiles g, g + G, g + 2G, ... (ticket mode, the
+//     host's fallback, runs encode4w_kernel).  No workgroup is re-dispatched per tile, the FP64 rows and the matrix operand are staged once, and each wave
+//     issues its NEXT tile's pixel DMA into its own LDS region as soon as its last slot image has
+//     been read out -- the DMA flies while the wave finishes the tile (tail word, tail granule) and
+//     while the workgroup's other waves finish theirs.  Static order needs every workgroup resident:
+//     the grid never exceeds the occupancy answer, and a look-back timeout (should that ever not
+//     hold) makes the host redo the launch in ticket mode, as for encode4w_kernel.
+//   * Matrix pipe: per slot (64 blocks of one wave), ONE v_mfma_i32_32x32x32_i8 forms the sixteen
+//     integer basis sums J of every block (ie_dct.h quot4j: pixels as signed bytes x ^ 0x80, the
+//     {-1,0,1} A fragment from EncTables::mfma_w), which replaces the 16 pixel unpacks and the
+//     integer butterflies on the VALU; the FP32 stage (36 mul/fma) and the rounding follow, with
+//     the tie limits of quot4j's own tracked run (lim4j).  The FP64 fix-up, sizing, emission and
+//     store are encode4w_kernel's.
+//   * misc (the waves' bit counts, head words, position) alternates between two copies by tile
+//     parity, so a wave that runs ahead into its next tile never overwrites what a slower wave of
+//     the same workgroup still reads; the tile's two barriers order everything else.
+// =============================================================================================
+constexpr int kPMisc = 64;  // two copies of encode4w_kernel's 32 misc words
+constexpr int kPWfrag = 256;  // the matrix-pipe A fragments [64 lanes][4 words]
+constexpr int kPLdsBytes = (4 * kWReg + 4 * kWTask + kPMisc + kPWfrag) * 4 + kWRows * 8;
+
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+typedef int v16i32 __attribute__((ext_vector_type(16)));
+
+// round_block_lean4 with the limits passed in (quot4j's own)
+__device__ __forceinline__ float round_block_lean4j(const float (&t)[16], uint32_t (&zp)[8], uint32_t* sflags, bool dcx,
+                                                    float l0, float l1, float l2) {
+    constexpr int S0 = Structural<4>::k[0], S1 = Structural<4>::k[1], S2 = Structural<4>::k[2];
+    float emax = 0.0f;
+    uint32_t sf = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        uint32_t yb[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int k = ZigZag<4>::idx[2 * j + h];
+            const float y = t[k] + kMagic;
+            const float e = fabsf(t[k] - (y - kMagic));
+            yb[h] = __float_as_uint(y);
+            if (k == 0) {
+                const uint32_t dc = uint32_t(int(truncf(t[0] + copysignf(0.5f, t[0]))));
+                yb[h] = dcx ? dc : yb[h];
+                emax = dcx ? emax : fmaxf(emax, e);
+            } else if (k == S0) {
+                sf |= (e >= l0) ? 1u : 0u;
+            } else if (k == S1) {
+                sf |= (e >= l1) ? 2u : 0u;
+            } else if (k == S2) {
+                sf |= (e >= l2) ? 4u : 0u;
+            } else {
+                emax = fmaxf(emax, e);
+            }
+        }
+        zp[j] = __builtin_amdgcn_perm(yb[1], yb[0], 0x05040100u);
+        asm volatile("" : "+v"(zp[j]));
+    }
+    *sflags = sf;
+    return emax;
+}
+
+#ifndef IE_P_WAVES
+#define IE_P_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD)
+#endif
+
+template <bool HIST>
+__global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
+    constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
+    constexpr int GW = 16 * NS, BW = 64 * NS, TG = 4 * GW;  // groups / blocks per wave, groups per tile
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t* const reg = smem + wv * kWReg;  // this wave's pixels, later its two slot images
+    uint32_t* const task = smem + 4 * kWReg + wv * kWTask;
+    uint32_t* const res = task + 64;
+    uint32_t* const misc0 = smem + 4 * kWReg + 4 * kWTask;  // [2][32]
+    uint32_t* const wl = misc0 + kPMisc;  // [64][4]: the matrix-pipe A fragment of every lane
+    uint32_t* const hl = wl + kPWfrag;    // HIST: the tile's byte histogram
+    constexpr int HR = kWHistRep, HWORDS = 256 * HR;
+    double* const srow = reinterpret_cast<double*>(hl + (HIST ? HWORDS : 0));
+    const int G = int(gridDim.x);
+
+    // The launch arguments are read through a pointer to the kernel-argument segment that is
+    // re-derived every tile: loop-invariant loads would otherwise be hoisted out of the tile loop
+    // and the ~40 argument words held in scalar registers for the kernel's whole life (spills).
+    using KArgs = const __attribute__((address_space(4))) EncArgs;
+    KArgs* ka = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+    // static tile order (ticket mode runs encode4w_kernel: launch_encode4w)
+    int t = int(blockIdx.x);
+    if (t >= a_.ntiles) return;
+    // each wave's pixel rows of tile tt into its own region (row r of the wave's block j at
+    // reg[r BW + j]: a lane's 16 bytes are its group's row)
+    auto issue_pixels = [&](KArgs& a, int tt) {
+        const TileGeo gg = tile_geo<4, 4, TG>(a, tt, tid);
+        if (gg.nblk) {
+            const uint8_t* base = a.y + size_t(gg.frame) * a.frame_pitch + size_t(gg.byi) * N * a.stride + size_t(gg.bx0) * N;
+#pragma unroll
+            for (int r = 0; r < N; r++)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
+                                                 (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, 0);
+        }
+    };
+    issue_pixels(*ka, t);
+    if constexpr (HIST)
+        for (int i = tid; i < HWORDS; i += TPB) hl[i] = 0u;
+    for (int i = tid; i < kWRows; i += TPB)
+        srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
+                : (i < NN * NN + 2 * NN) ? tab->rq[i - NN * NN - NN] : tab->qd[i - NN * NN - 2 * NN];
+    // the matrix-pipe A fragments (constant for the whole launch; read back per slot: a register
+    // copy held across the tile loop measured as spills)
+    wl[tid] = tab->mfma_w[tid >> 2][tid & 3];
+    const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
+    const bool deep = a_.deep_lb != 0;
+    lds_barrier();  // srow (and the HIST bins) visible; the pixel DMA stays in flight
+
+    for (int iter = 0;; iter++) {
+        asm volatile("" : "+s"(ka));
+        KArgs& a = *ka;
+        // lane-derived values re-derived every tile as well: addresses computed from them would
+        // otherwise be hoisted out of the tile loop and held (spilled) across it
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63;
+        uint32_t* const misc = misc0 + (iter & 1) * 32;
+        const TileGeo g = tile_geo<4, 4, TG>(a, t, tid);
+        const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
+        const int ng = min(TG, a.groups_per_frame - tif * TG);
+        const int nbw = 4 * min(GW, max(0, ng - GW * wv));  // blocks of this wave
+        const int wlast = (ng - 1) / GW;                    // the tile's last non-empty wave
+        WSTAMP(0);
+        WRTSTAMP(14);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
+        WSTAMP(1);
+
+        // -------------------------------------------------------- transform + quantise, 4 slots
+        // (the table pointer is re-derived every tile so that the FP32 stage's 36 constants are
+        // loaded here, not hoisted out of the tile loop into scalar registers held for its whole life)
+        using KTab = const __attribute__((address_space(4))) EncTables;
+        KTab* tb = (KTab*)(tab);  // constant address space: scalar loads
+        asm volatile("" : "+s"(tb));
+        const bool dcx = tb->dc_exact4j != 0;
+        const float lim_s0 = tb->lim4j[Structural<4>::k[0]], lim_s1 = tb->lim4j[Structural<4>::k[1]],
+                    lim_s2 = tb->lim4j[Structural<4>::k[2]], lim_min = tb->lim_min4j;
+        uint32_t zp[NS][NP];
+        uint32_t flags = 0;  // 4 bits per slot: structural s (bits 0-2), whole block (bit 3)
+        auto slot_mfma = [&](int b) {
+            v4i32 px;
+#pragma unroll
+            for (int r = 0; r < N; r++) px[r] = int(reg[r * BW + 64 * b + lane] ^ 0x80808080u);  // x - 128 as i8
+            const v4i32 wfrag = *reinterpret_cast<const v4i32*>(wl + 4 * lane);
+            return __builtin_amdgcn_mfma_i32_32x32x32_i8(wfrag, px, v16i32{}, 0, 0, 0);
+        };
+#pragma unroll
+        for (int b = 0; b < NS; b++) {
+            __builtin_amdgcn_sched_barrier(0);
+            const v16i32 Jc = slot_mfma(b);
+            float Jf[16], x[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) Jf[k] = float(Jc[k]);
+            quot4j(Jf, x, tb->plan4j, FloatOp());
+            uint32_t sf;
+            const float emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
+            const uint32_t fb = (emax >= lim_min) ? 8u : sf;
+            if (64 * b + lane < nbw) flags |= fb << (4 * b);
+#pragma unroll
+            for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
+            asm volatile("" : "+v"(flags));
+        }
+        WSTAMP(2);
+
+        // -------------------------------------------------------- FP64 fix-up (encode4w_kernel's)
+        auto block_px = [&](int b, int owner) {
+            BlockPx<N> px;
+#pragma unroll
+            for (int r = 0; r < N; r++) px.w[r] = reg[r * BW + 64 * b + owner];
+            return px;
+        };
+        if (__ballot(flags != 0)) {
+            const uint32_t sf = flags & 0x7777u;
+            const uint32_t cnt = __popc(sf);
+            uint32_t pre = 0, total = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {  // cnt <= 12
+                const uint64_t bm = __ballot((cnt >> k) & 1u);
+                pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+                total += uint32_t(__popcll(bm)) << k;
+            }
+            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+                uint32_t m = sf, i = pre - r0;
+                while (m) {
+                    const int bit = __ffs(m) - 1;
+                    m &= m - 1;
+                    if (i < 64u) task[i] = (uint32_t(lane) << 4) | uint32_t(bit);
+                    i++;
+                }
+                wave_sync();
+                if (uint32_t(lane) < total - r0) {
+                    const uint32_t tk = task[lane];
+                    const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
+                    const BlockPx<N> px = block_px(b, owner);
+                    const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
+                    const int y = exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                    srow[NN * NN + 2 * NN + k], px);
+                    res[lane] = uint32_t(y) & 0xFFFFu;
+                }
+                wave_sync();
+                i = pre - r0;
+#pragma unroll
+                for (int b = 0; b < NS; b++)
+#pragma unroll
+                    for (int ss = 0; ss < 3; ss++) {
+                        if ((sf >> (4 * b + ss)) & 1u) {
+                            const int zw = Structural<N>::zpos(ss) >> 1;
+                            if (i < 64u) zp[b][zw] = __builtin_amdgcn_perm(res[i], zp[b][zw], 0x05040100u);  // res low -> high half
+                            i++;
+                        }
+                    }
+                wave_sync();
+            }
+            const uint32_t wf = flags & 0x8888u;
+            if (__ballot(wf != 0)) {
+                const uint32_t nb = __popc(wf);
+                uint32_t pb = 0, tb = 0;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {  // nb <= 4
+                    const uint64_t bm = __ballot((nb >> k) & 1u);
+                    pb += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+                    tb += uint32_t(__popcll(bm)) << k;
+                }
+                for (uint32_t r0 = 0; r0 < tb; r0 += 4) {
+                    uint32_t m = wf, j = pb - r0;
+                    while (m) {
+                        const int b = (__ffs(m) - 1) >> 2;
+                        m &= m - 1;
+                        if (j < 4u) task[j] = (uint32_t(lane) << 4) | uint32_t(b);
+                        j++;
+                    }
+                    wave_sync();
+                    if (uint32_t(lane >> 4) < tb - r0) {
+                        const uint32_t tk = task[lane >> 4];
+                        const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
+                        const BlockPx<N> px = block_px(b, owner);
+                        const int y = exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                        srow[NN * NN + 2 * NN + k], px);
+                        res[lane] = uint32_t(y) & 0xFFFFu;
+                    }
+                    wave_sync();
+                    m = wf;
+                    j = pb - r0;
+                    while (m) {
+                        const int b = (__ffs(m) - 1) >> 2;
+                        m &= m - 1;
+                        if (j < 4u) {
+                            const uint32_t* rr = res + 16 * j;
+#pragma unroll
+                            for (int jj = 0; jj < NP; jj++) {
+                                const uint32_t w = rr[ZigZag<N>::idx[2 * jj]] | (rr[ZigZag<N>::idx[2 * jj + 1]] << 16);
+#pragma unroll
+                                for (int bb = 0; bb < NS; bb++) zp[bb][jj] = (b == bb) ? w : zp[bb][jj];
+                            }
+                        }
+                        j++;
+                    }
+                    wave_sync();
+                }
+            }
+        }
+        {  // statistics: FP64 requests of this wave (one store)
+            const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan_dpp(uint32_t(__popc(flags))), 63);
+            if (lane == 0) a.wave_fix[size_t(t) * (TPB / 64) + wv] = wsum;
+        }
+        WSTAMP(3);
+
+        // -------------------------------------------------------- sizing + the wave's offsets
+        uint32_t blw[NS], rb[NS];
+        const uint32_t k0 = uint32_t(tif * TG + GW * wv) * 4u;  // the wave's first block (frame raster order)
+#pragma unroll
+        for (int b = 0; b < NS; b++) {
+            const bool valid = 64 * b + lane < nbw;
+            if (a.coef && valid) {
+                int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + k0 + 64 * b + lane) * NN;
+#pragma unroll
+                for (int k = 0; k < NN; k++) {
+                    const int kz = ZigZagInv<N>::pos[k];
+                    dst[k] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            blw[b] = size_block<N>(zp[b], a.rle, &rb[b]);
+            rb[b] = valid ? rb[b] : 0u;
+            asm volatile("" : "+v"(blw[b]), "+v"(rb[b]));
+#pragma unroll
+            for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const uint32_t s01 = rb[0] | (rb[1] << 16), s23 = rb[2] | (rb[3] << 16);
+        const uint32_t i01 = wave_incl_scan_dpp(s01), i23 = wave_incl_scan_dpp(s23);
+        const uint32_t t01 = __builtin_amdgcn_readlane(i01, 63), t23 = __builtin_amdgcn_readlane(i23, 63);
+        const uint32_t e01 = i01 - s01, e23 = i23 - s23;
+        uint32_t T[NS], off[NS];
+        T[0] = t01 & 0xFFFFu;
+        T[1] = t01 >> 16;
+        T[2] = t23 & 0xFFFFu;
+        T[3] = t23 >> 16;
+        off[0] = e01 & 0xFFFFu;
+        off[1] = e01 >> 16;
+        off[2] = e23 & 0xFFFFu;
+        off[3] = e23 >> 16;
+        const uint32_t S1 = T[0], S2 = S1 + T[1], S3 = S2 + T[2], Tw = S3 + T[3];
+        if (lane == 0) misc[wv] = Tw;
+        WSTAMP(4);
+        lds_barrier();  // ---- the tile's bit count and this wave's place in it
+        WSTAMP(5);
+        const int t_next = t + G;
+
+        uint32_t A = 0, W = 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
+            A += v;
+            W += (w < wv) ? v : 0u;
+        }
+        if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);
+        constexpr int DW = 2;
+        Probe pr[DW];
+#pragma unroll
+        for (int i = 0; i < DW; i++) pr[i] = Probe{0, 0, 0};
+        if (chain_pos != 0) {
+            if (deep) {
+#pragma unroll
+                for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
+            } else if (wv == 0) {
+                pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
+            }
+        }
+
+        const uint32_t reg_bit0 = uint32_t(wv * kWReg) * 32u;
+        const uint32_t Sb[NS] = {0u, S1, S2, S3};
+        auto zero_img = [&](uint32_t bits) {
+            const uint32_t nq = (bits + 127u) >> 7;  // 16-byte groups
+            uint32_t z;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // (a zero vector hoisted out of the tile loop was spilled)
+            for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(reg + 4 * q) = u32x4{z, z, z, z};
+        };
+        auto emit_slot = [&](int b) {  // slot b at its place in its pair's image
+            if (rb[b]) {
+                const uint32_t p = reg_bit0 + (Sb[b] - Sb[b & 2]) + off[b];
+                if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
+                else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
+            }
+        };
+        zero_img(S2);
+        wave_sync();
+        emit_slot(0);
+        emit_slot(1);
+        wave_sync();
+        WSTAMP(6);
+        if (lane == 0 && Tw) misc[4 + wv] = reg[0];  // the wave's first 32 bits
+
+        // -------------------------------------------------------- look-back (wave 0)
+        const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
+        uint32_t* const out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
+        if (deep && chain_pos != 0) {
+            uint64_t sm = 0;
+            bool found = false;
+            unsigned spins = 0;
+            for (;;) {
+                bool ready = true;
+                sm = 0;
+                found = false;
+#pragma unroll
+                for (int i = 0; i < DW; i++) {
+                    const WinSum r = window_sum(pr[i], chain_pos, 64 * (DW * wv + i), 64, a.tag);
+                    if (!found) {
+                        ready = ready && r.ready;
+                        sm += r.sum;
+                        found = r.found;
+                    }
+                }
+                if (ready) break;
+                if (++spins > kSpinLimit) {
+                    if (lane == 0) atomicAdd(&a.err[0], 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
+            }
+            if (lane == 0) {
+                misc[18 + 2 * wv] = uint32_t(sm);
+                misc[19 + 2 * wv] = uint32_t(sm >> 32);
+                misc[26 + wv] = found ? 1u : 0u;
+            }
+            lds_barrier();
+        }
+        if (wv == 0) {
+            uint64_t excl = 0;
+            uint32_t ptail = 0, pend = 0;
+            if (chain_pos == 0) {
+                const uint32_t s = uint32_t(start_bit & 31);
+                ptail = s ? (bswap32(out[start_bit >> 5]) >> (32 - s)) : 0u;
+            } else {
+                bool done = false;
+                if (deep) {
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        if (!done) {
+                            excl += uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[18 + 2 * w]))) |
+                                    (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[19 + 2 * w]))) << 32);
+                            done = __builtin_amdgcn_readfirstlane(misc[26 + w]) != 0;
+                        }
+                    }
+                    if (!done) excl = 0;
+                }
+                if (!done) {
+                    const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr[0];
+                    excl = lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
+                }
+                const bool have = uint32_t(pr[0].gt >> 56) == a.tag;
+                const bool split = ((start_bit + excl) & 31) != 0;
+                ptail = have ? uint32_t(pr[0].gt) : 0u;
+                pend = (!have && split) ? 1u : 0u;
+            }
+            if (lane == 0) {
+                if (chain_pos != 0) publish(a.st, t, 1, a.tag, excl + A);
+                misc[8] = uint32_t(excl);
+                misc[9] = uint32_t(excl >> 32);
+                misc[10] = ptail;
+                misc[11] = pend;
+                const uint64_t P = start_bit + excl;
+                if (tif == 0) a.frame_start[frame] = P;
+                if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
+            }
+        }
+        WSTAMP(7);
+        lds_barrier();  // ---- the tile's position
+        WSTAMP(8);
+
+        // -------------------------------------------------------- store, slot pair by slot pair
+        const bool more = t_next < a.ntiles;
+        if (Tw) {
+            const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[8]))) |
+                                  (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[9]))) << 32);
+            const uint64_t Xw = start_bit + excl + W;
+            const bool pend = __builtin_amdgcn_readfirstlane(misc[11]) != 0u;
+            const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
+            uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[10]) : 0u;
+            const HistCountT<HR> hc{hl, chain_last ? (start_bit + excl + A + 7) / 8 : ~0ull, uint32_t(lane % HR)};
+            auto count = [&](uint64_t gw, uint32_t v) {
+                if constexpr (HIST) hc(gw, v);
+            };
+            auto store_pair = [&](uint32_t S0, uint32_t n) {
+                if (!n) return;
+                const uint64_t Xb = Xw + S0;
+                const uint32_t nw = uint32_t(((Xb + n) >> 5) - (Xb >> 5));
+                if constexpr (HIST) store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane, hc);
+                else store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
+                prev = slot_tail32(reg, n, prev);
+            };
+            if constexpr (HIST) {
+                if (wv == 0 && chain_pos == 0)
+                    for (uint32_t i = lane; i < uint32_t(start_bit >> 5); i += 64) hc(i, out[i]);
+            }
+            store_pair(0u, S2);
+            WSTAMP(9);
+            if (Tw > S2) {
+                wave_sync();  // pair 0's image has been read
+                zero_img(Tw - S2);
+                wave_sync();
+                emit_slot(2);
+                emit_slot(3);
+                wave_sync();
+                store_pair(S2, Tw - S2);
+            }
+            const uint64_t E = Xw + Tw;
+            const uint32_t e = uint32_t(E) & 31u;
+            const uint32_t nexthead = (e && wv < wlast) ? misc[4 + wv + 1] : 0u;
+            // every read of this wave's region is complete (the stores consumed it): the next
+            // tile's pixels may land there now
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (more) issue_pixels(a, t_next);
+            if (lane == 0) {
+                if (e && (wv < wlast || chain_last)) {  // the wave's last, partial word
+                    const uint32_t v = bswap32((prev << (32u - e)) | (nexthead >> e));
+                    out[E >> 5] = v;
+                    count(E >> 5, v);
+                }
+                if (wv == wlast) publish(a.st, t, 2, a.tag, prev);  // the tile's last 32 bits
+                if (wv == 0 && pend) {  // the first word, with the predecessor's tail
+                    const uint32_t pt = wait_tail(a.st, t - step, a.tag, a.err);
+                    const uint32_t s = uint32_t(Xw) & 31u;
+                    const uint32_t v = bswap32((pt << (32u - s)) | (misc[4] >> s));
+                    out[Xw >> 5] = v;
+                    count(Xw >> 5, v);
+                }
+            }
+            WSTAMP(10);
+            WRTSTAMP(15);
+        } else if (more) {
+            issue_pixels(a, t_next);
+        }
+        if constexpr (HIST) {
+            lds_barrier();  // every wave's bytes counted
+            uint32_t c = 0;
+#pragma unroll
+            for (int r = 0; r < HR; r++) c += hl[tid * HR + r];
+            if (c) atomicAdd(&a.hist[size_t(frame) * 256 + tid], c);
+#pragma unroll
+            for (int r = 0; r < HR; r++) hl[tid * HR + r] = 0u;  // (the next tile adds after two barriers)
+        }
+        if (!more) break;
+        t = t_next;
+    }
+}
+
+#ifndef IE_ENC_P
+#define IE_ENC_P 1  // 0: 4x4 FAST batch launches run encode4w_kernel (A/B builds)
+#endif
+// Persistent workgroups per CU: the occupancy API's answer, capped at IE_P_PER_CU -- the number
+// tools/asmcheck.py (PERSIST) proves the SGPR admission rule lets in (the API can answer one more
+// than the hardware admits; a static-order grid with one workgroup not resident would stall).
+#ifndef IE_P_PER_CU
+#define IE_P_PER_CU 6
+#endif
+
+// Resident workgroups of encode4p_kernel<HIST> on this device (cached per process).
+static int encode4p_grid(bool hist, size_t lds) {
+    static int cached[2] = {0, 0};
+    int& c = cached[hist ? 1 : 0];
+    if (c) return c;
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hist) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4p_kernel<true>, 256, lds);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4p_kernel<false>, 256, lds);
+    per = std::min(per, IE_P_PER_CU);
+    c = std::max(1, per) * std::max(1, cus);
+    return c;
+}
+
 void launch_encode4w(const EncArgs& a, hipStream_t s) {
+    if (IE_ENC_P && !a.ticket) {
+        const size_t lds = kPLdsBytes + (a.hist ? 1024 * kWHistRep : 0);
+        const int grid = std::min(a.ntiles, encode4p_grid(a.hist != nullptr, lds));
+        if (a.hist) hipLaunchKernelGGL(encode4p_kernel<true>, dim3(grid), dim3(256), lds, s, a, a.tab);
+        else hipLaunchKernelGGL(encode4p_kernel<false>, dim3(grid), dim3(256), lds, s, a, a.tab);
+        return;
+    }
     if (a.hist) hipLaunchKernelGGL(encode4w_kernel<true>, dim3(a.ntiles), dim3(256), kWLdsBytes + 1024 * kWHistRep, s, a, a.tab);
     else hipLaunchKernelGGL(encode4w_kernel<false>, dim3(a.ntiles), dim3(256), kWLdsBytes, s, a, a.tab);
 }
