@@ -110,6 +110,7 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.ie_huffman_decode.argtypes = [vp, u8p, C.c_size_t, C.c_uint64, vp, u8p, C.c_size_t, C.POINTER(C.c_size_t)]
     L.ie_last_decode_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.ie_set_exact_parse.argtypes = [vp, C.c_int]
+    L.ie_set_spec_warm.argtypes = [vp, C.c_int]
     L.ie_last_decode_spec.argtypes = [vp]
     L.ie_malloc.argtypes = [vp, C.c_size_t, C.POINTER(C.c_void_p)]
     L.ie_free.argtypes = [vp, vp]
@@ -443,7 +444,8 @@ class Codec:
         """Record decodes parse exactly (composed transfer tables) instead of speculatively first
         (ie_set_exact_parse); a speculative parse may start each chunk's walk ``warm`` (<= 8)
         chunks early."""
-        self._chk(self.L.ie_set_exact_parse(self.h, 1 if exact else -min(8, max(0, int(warm)))))
+        self._chk(self.L.ie_set_spec_warm(self.h, int(warm)))
+        self._chk(self.L.ie_set_exact_parse(self.h, 1 if exact else 0))
 
     def last_decode_spec(self) -> bool:
         """True when the last record decode was completed by the speculative parse."""

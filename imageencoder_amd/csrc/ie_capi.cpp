@@ -41,6 +41,7 @@ struct ie_ctx {
 
     uint64_t* d_frame_start = nullptr;  // [cap_frames]
     uint64_t* d_chain_end = nullptr;    // [cap_frames]
+    unsigned* d_claim = nullptr;        // [cap_frames + 1] the persistent encoder's tile claim counters
     size_t cap_frames = 0;
     unsigned* d_err = nullptr;          // [0] look-back timeouts (cumulative)
     uint32_t* d_wave_fix = nullptr;     // [cap_tiles * waves per tile] fix-up requests of the last launch
@@ -113,8 +114,8 @@ struct ie_ctx {
     int last_chunks = 0;               // chunks of the last record decode
     int last_groups = 0;               // and their groups
     int last_spec = 0;                 // 1: the last record decode was the speculative parse
-    int spec_parse = 0;                // ie_set_exact_parse(ctx, <= 0): speculative record parse first
-    int spec_warm = 0;                 // ie_set_exact_parse(ctx, -w): w warm-up chunks (<= 8)
+    int spec_parse = 0;                // ie_set_exact_parse(ctx, 0): speculative record parse first
+    int spec_warm = 0;                 // ie_set_spec_warm(ctx, w): w warm-up chunks (<= 8)
     unsigned long long* d_first = nullptr;  // [256]
     ie_pipe* pipe = nullptr;           // streamed host path of image batches (created on first use)
     // P-frame videos (ie_encode_gop): reconstructed frames (two, alternating), the prediction
@@ -357,6 +358,14 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
         }
         T->rec_bits = 4 + bl * (1 + nn);
     }
+    if (n == 4) {  // every coefficient's FP64 row and its S, rq, qd, contiguous (encode4p_kernel's DMA)
+        for (int i = 0; i < nn * nn; i++) T->rows4[i] = T->P[i];
+        for (int k = 0; k < nn; k++) {
+            T->rows4[nn * nn + k] = T->S[k];
+            T->rows4[nn * nn + nn + k] = T->rq[k];
+            T->rows4[nn * nn + 2 * nn + k] = T->qd[k];
+        }
+    }
     {  // the fix-up's structural rows, contiguous (encode_kernel copies them to LDS)
         const int h = n / 2, ks[3] = {h, h * n, h * n + h};
         for (int si = 0; si < 3; si++) {
@@ -432,6 +441,9 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
         const size_t cap = std::max<size_t>(nframes, 64);
         HIPCHK(c, hipMalloc(&c->d_frame_start, cap * sizeof(uint64_t)));
         HIPCHK(c, hipMalloc(&c->d_chain_end, cap * sizeof(uint64_t)));
+        if (c->d_claim) HIPCHK(c, hipFree(c->d_claim));
+        HIPCHK(c, hipMalloc(&c->d_claim, (cap + 1) * ie::kClaimStride * sizeof(unsigned)));
+        HIPCHK(c, hipMemsetAsync(c->d_claim, 0, (cap + 1) * ie::kClaimStride * sizeof(unsigned), c->stream));
         c->cap_frames = cap;
     }
     return IE_OK;
@@ -595,6 +607,7 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     a.ticket_base = c->ticket_base;
     a.tag = c->tag;
     a.frame_start = c->d_frame_start;
+    a.claim = c->d_claim;
     a.chain_end = L.chain_end ? L.chain_end : c->d_chain_end;
     a.err = c->d_err;
     a.wave_fix = c->d_wave_fix;
@@ -1303,8 +1316,13 @@ int ie_last_decode_info(ie_ctx* c, int* chunks, int* levels) {
 
 int ie_set_exact_parse(ie_ctx* c, int exact) {
     if (!c) return IE_EINVAL;
-    c->spec_parse = exact > 0 ? 0 : 1;
-    c->spec_warm = exact < 0 ? std::min(8, -exact) : 0;
+    c->spec_parse = exact != 0 ? 0 : 1;  // any nonzero value: the exact parse
+    return IE_OK;
+}
+
+int ie_set_spec_warm(ie_ctx* c, int warm) {
+    if (!c) return IE_EINVAL;
+    c->spec_warm = warm < 0 ? 0 : (warm > 8 ? 8 : warm);  // clamped before use: no negation
     return IE_OK;
 }
 
@@ -1510,6 +1528,7 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_state);
     (void)hipFree(c->d_ticket);
     (void)hipFree(c->d_frame_start);
+    (void)hipFree(c->d_claim);
     (void)hipFree(c->d_chain_end);
     (void)hipFree(c->d_err);
     (void)hipFree(c->d_wave_fix);

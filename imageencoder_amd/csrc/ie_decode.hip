@@ -114,7 +114,7 @@ __device__ __forceinline__ uint64_t huf_walk(const HufArgs& a, const uint16_t* l
 // workgroup's, wgsum[g] = the workgroup's total (no separate scan launch).
 __global__ __launch_bounds__(kTPB) void huf_walk_kernel(HufArgs a) {
     __shared__ uint16_t l1[1 << kHufL1];
-    __shared__ uint32_t scratch[8];
+    __shared__ alignas(8) uint32_t scratch[8];
     huf_l1(a.lut, l1);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t c = 0;
@@ -153,7 +153,7 @@ __device__ __forceinline__ uint64_t huf_wg_prefix(const uint32_t* wgsum, int g, 
 
 __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
     __shared__ uint16_t l1[1 << kHufL1];
-    __shared__ uint32_t scratch[8];
+    __shared__ alignas(8) uint32_t scratch[8];
     huf_l1(a.lut, l1);
     const uint64_t pre = huf_wg_prefix(a.wgsum, int(blockIdx.x), scratch);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
 
 // total receives the symbol count (device, 1 word): the sum of the walk's workgroup totals.
 __global__ __launch_bounds__(kTPB) void huf_total_kernel(const uint32_t* wgsum, int nwg, uint64_t* total) {
-    __shared__ uint32_t scratch[8];
+    __shared__ alignas(8) uint32_t scratch[8];
     const uint64_t t = huf_wg_prefix(wgsum, nwg, scratch);
     if (threadIdx.x == 0) *total = t;
 }
@@ -836,7 +836,7 @@ __global__ __launch_bounds__(kTPB) void rec_spec_kernel(RecParseArgs a) {
 template <int N>
 __global__ __launch_bounds__(kTPB) void rec_count_kernel(RecParseArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t Lall[];
-    __shared__ uint32_t scratch[8];
+    __shared__ alignas(8) uint32_t scratch[8];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int seg = a.seg;
     const int k0 = (blockIdx.x * 4 + wv) * seg;  // this wave's first chunk

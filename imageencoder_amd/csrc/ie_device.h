@@ -32,6 +32,9 @@ struct EncTables {
     float lim_min4j;
     int dc_exact4j;
     uint32_t mfma_w[64][4];
+    // 4x4: P[16][16] then S, rq, qd of every coefficient, contiguous (the fix-up's LDS copy, staged
+    // by DMA: 152 lanes x 16 bytes)
+    double rows4[16 * 16 + 3 * 16];
     // the structural coefficients' rows P[k_s][*] (s = 0..2), then S, rq, qd of the three: the
     // fix-up's LDS copy, one contiguous block (3*NN + 9 doubles)
     double srow[3 * 64 + 9];
@@ -102,7 +105,12 @@ struct EncArgs {
     // optional (segmented launches): per-frame byte histograms [nframes][256] of the stream bytes
     // [0, ceil(end/8)) -- header included -- ADDED to by the launch (the Huffman pass's counts)
     uint32_t* hist;
+    // persistent encoder (encode4p_kernel): per-chain claim counters [nchains] then the exit counter,
+    // kClaimStride words apart (a 128-byte line each: atomics on one line serialise), all zero
+    // before the launch and left zero by its last workgroup
+    unsigned* claim;
 };
+constexpr int kClaimStride = 32;
 
 constexpr int kStamps = 64;  // encode_kernel: [0, 16) by thread 0; encode4w_kernel: [4 waves][16] by each wave's lane 0
 // chain-state words per tile (the host allocates; ie_common.hpp kGran must not exceed it)

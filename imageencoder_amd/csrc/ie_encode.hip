@@ -531,10 +531,11 @@ __device__ __forceinline__ void emit_block2(uint32_t* img, uint32_t p, const uin
 // Every triple is ORed in, without a wave-wide "any lane still has one" exit per field (past Lw
 // the coefficients are zero): the v_cmp + branch per field cost more than the skipped fields save
 // unless every lane of the wave has a short record (measured -2 % on C2).
-// 4x4 RLE records when every bl of the matrix is <= 11 (EncArgs::tri, from the host's record
-// bound): the header, Lw and z0 in one field of 4 + 2*bl bits, then the coefficients THREE at a
-// time (3*bl <= 33 bits, within scatter_bits' 64-bit window): 6 ORed fields per block instead of
-// 9.  Past Lw the packed coefficients are zero, so a trailing triple only ORs zeros.
+// 4x4 RLE records when every bl of the matrix is <= 10 (EncArgs::tri: the host's launch_chain
+// sets it when (rec_bits - 4) / 17 <= 10): the header, Lw and z0 in one field of 4 + 2*bl <= 24
+// bits, then the coefficients THREE at a time (3*bl <= 30 bits: the field is built in a 32-bit
+// v), each ORed through scatter_bits' 64-bit window: 6 fields per block instead of 9.  Past Lw
+// the packed coefficients are zero, so a trailing triple only ORs zeros.
 __device__ __forceinline__ void emit_block3(uint32_t* img, uint32_t p, const uint32_t (&zp)[8], uint32_t blw) {
     const uint32_t bl = blw & 0xFFu, lw = blw >> 8;
     auto z = [&](int k) -> uint32_t {  // low bl bits of zig-zag coefficient k
@@ -1873,8 +1874,43 @@ __device__ __forceinline__ float round_block_lean4j(const float (&t)[16], uint32
     return emax;
 }
 
+// Tile claims of the persistent encoder.  Tiles of a chain are handed out in chain order by that
+// chain's counter (segmented launches: one chain per frame, tile = k * nframes + frame, the
+// interleave of tile_geo; otherwise one chain, tile = k); a workgroup stays on its chain until it
+// is exhausted, then moves to the next chain with tiles left.  A tile's look-back waits only on
+// earlier tiles of its chain, claimed before it by workgroups that are running (a workgroup claims
+// its next tile while it works on the current one, and no chain of such waits can close: DESIGN
+// §3), so the order needs no residency guarantee.  One wave calls it (wave-uniform result).
+__device__ __forceinline__ int claim_resolve(unsigned* cnt, int nch, int tpc, bool seg, int* c, unsigned k) {
+    const int lane = lane_id();
+    for (;;) {
+        const int kk = __builtin_amdgcn_readfirstlane(int(k));
+        if (kk < tpc) return seg ? kk * nch + *c : kk;
+        if (nch == 1) return -1;
+        int found = -1;  // the first chain after *c with tiles left, 64 chains per look
+        for (int j0 = 1; j0 < nch && found < 0; j0 += 64) {
+            const int j = j0 + lane;
+            const int cc = (*c + j) % nch;
+            const bool left = j < nch && __hip_atomic_load(&cnt[kClaimStride * cc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unsigned(tpc);
+            const uint64_t m = __ballot(left);
+            if (m) found = __builtin_amdgcn_readlane(cc, __ffsll((unsigned long long)m) - 1);
+        }
+        if (found < 0) return -1;
+        *c = found;
+        unsigned kn = 0;
+        if (lane == 0) kn = atomicAdd(&cnt[kClaimStride * found], 1u);
+        k = kn;
+    }
+}
+
 #ifndef IE_P_WAVES
 #define IE_P_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD)
+#endif
+#ifndef IE_P_MFMA
+#define IE_P_MFMA 1  // 0: (A/B builds) the transform on the VALU as in encode4w_kernel
+#endif
+#ifndef IE_P_PERSIST
+#define IE_P_PERSIST 0  // 1: (A/B builds) the persistent grid with per-chain tile claims
 #endif
 
 template <bool HIST>
@@ -1882,7 +1918,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
     constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
     constexpr int GW = 16 * NS, BW = 64 * NS, TG = 4 * GW;  // groups / blocks per wave, groups per tile
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint32_t* const reg = smem + wv * kWReg;  // this wave's pixels, later its two slot images
     uint32_t* const task = smem + 4 * kWReg + wv * kWTask;
@@ -1899,9 +1935,38 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
     // and the ~40 argument words held in scalar registers for the kernel's whole life (spills).
     using KArgs = const __attribute__((address_space(4))) EncArgs;
     KArgs* ka = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
-    // static tile order (ticket mode runs encode4w_kernel: launch_encode4w)
+    // tile order: a grid of one workgroup per tile runs them in blockIdx order (dispatch order, as
+    // encode4w_kernel); a smaller (persistent) grid claims them (claim_resolve).  Ticket mode runs
+    // encode4w_kernel (launch_encode4w).
+    const bool dyn = IE_P_PERSIST && G < a_.ntiles;
+    const bool seg = a_.segmented != 0;
+    const int nch = seg ? a_.nframes : 1, tpc = seg ? a_.tiles_per_frame : a_.ntiles;
+    unsigned* const cnt = a_.claim;
+    int chain = int(blockIdx.x) % nch;  // the chain this workgroup claims from (wave 0's copy counts)
     int t = int(blockIdx.x);
-    if (t >= a_.ntiles) return;
+    if (dyn) {
+        if (wv == 0) {
+            unsigned k = 0;
+            if ((tid & 63) == 0) k = atomicAdd(&cnt[kClaimStride * chain], 1u);
+            const int tt = claim_resolve(cnt, nch, tpc, seg, &chain, k);
+            if (tid == 0) misc0[12] = uint32_t(tt);
+        }
+        lds_barrier();
+        t = __builtin_amdgcn_readfirstlane(int(misc0[12]));
+    }
+    // (every workgroup of a claiming grid counts its exit; the last one leaves the counters zero)
+    auto leave = [&]() {
+        if (dyn && tid == 0) {
+            const unsigned e = atomicAdd(&cnt[kClaimStride * nch], 1u);
+            if (e == unsigned(G) - 1u) {
+                for (int i = 0; i <= nch; i++) __hip_atomic_store(&cnt[kClaimStride * i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    };
+    if (t < 0 || t >= a_.ntiles) {
+        leave();
+        return;
+    }
     // each wave's pixel rows of tile tt into its own region (row r of the wave's block j at
     // reg[r BW + j]: a lane's 16 bytes are its group's row)
     auto issue_pixels = [&](KArgs& a, int tt) {
@@ -1915,17 +1980,25 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         }
     };
     issue_pixels(*ka, t);
+    // the FP64 rows (waves 0-2: 2432 bytes) and the matrix-pipe A fragments (wave 3; read back per
+    // slot: a register copy held across the tile loop measured as spills) by DMA too: no register
+    // round trip, one wait for everything
+    {
+        const int lane0 = tid & 63;
+        static_assert(kWRows * 8 == 2 * 1024 + 24 * 16, "rows: two full waves and 24 lanes of 16 bytes");
+        if (wv < 2 || (wv == 2 && lane0 < 24))
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->rows4[wv * 128 + 2 * lane0]),
+                                             (__attribute__((address_space(3))) void*)(srow + wv * 128), 16, 0, 0);
+        else if (wv == 3)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->mfma_w[lane0][0]),
+                                             (__attribute__((address_space(3))) void*)(wl), 16, 0, 0);
+    }
     if constexpr (HIST)
         for (int i = tid; i < HWORDS; i += TPB) hl[i] = 0u;
-    for (int i = tid; i < kWRows; i += TPB)
-        srow[i] = (i < NN * NN) ? tab->P[i] : (i < NN * NN + NN) ? tab->S[i - NN * NN]
-                : (i < NN * NN + 2 * NN) ? tab->rq[i - NN * NN - NN] : tab->qd[i - NN * NN - 2 * NN];
-    // the matrix-pipe A fragments (constant for the whole launch; read back per slot: a register
-    // copy held across the tile loop measured as spills)
-    wl[tid] = tab->mfma_w[tid >> 2][tid & 3];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA above and the first tile's pixels)
     const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
     const bool deep = a_.deep_lb != 0;
-    lds_barrier();  // srow (and the HIST bins) visible; the pixel DMA stays in flight
+    lds_barrier();  // the rows, the A fragments (and the HIST bins) visible
 
     for (int iter = 0;; iter++) {
         asm volatile("" : "+s"(ka));
@@ -1944,7 +2017,9 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         WSTAMP(0);
         WRTSTAMP(14);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
+        if (wv == 0 && lane == 0) misc[13] = 0u;  // the next tile's claim: not yet made (read after barrier 2)
         WSTAMP(1);
+        asm volatile("; PHASE p1" ::: "memory");
 
         // -------------------------------------------------------- transform + quantise, 4 slots
         // (the table pointer is re-derived every tile so that the FP32 stage's 36 constants are
@@ -1967,20 +2042,34 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
 #pragma unroll
         for (int b = 0; b < NS; b++) {
             __builtin_amdgcn_sched_barrier(0);
-            const v16i32 Jc = slot_mfma(b);
-            float Jf[16], x[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) Jf[k] = float(Jc[k]);
-            quot4j(Jf, x, tb->plan4j, FloatOp());
             uint32_t sf;
-            const float emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
-            const uint32_t fb = (emax >= lim_min) ? 8u : sf;
+            float emax, lmin;
+            if (IE_P_MFMA) {
+                const v16i32 Jc = slot_mfma(b);
+                float Jf[16], x[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) Jf[k] = float(Jc[k]);
+                quot4j(Jf, x, tb->plan4j, FloatOp());
+                emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
+                lmin = lim_min;
+            } else {  // (A/B builds) the VALU transform of encode4w_kernel
+                uint32_t rows[N][1];
+#pragma unroll
+                for (int r = 0; r < N; r++) rows[r][0] = reg[r * BW + 64 * b + lane];
+                float x[NN];
+                block_pixels<N, 1>(rows, 0, x);
+                quotients<N>(tab, x);
+                emax = round_block_lean4(tab, x, zp[b], &sf);
+                lmin = tab->lim_min;
+            }
+            const uint32_t fb = (emax >= lmin) ? 8u : sf;
             if (64 * b + lane < nbw) flags |= fb << (4 * b);
 #pragma unroll
             for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
             asm volatile("" : "+v"(flags));
         }
         WSTAMP(2);
+        asm volatile("; PHASE p2" ::: "memory");
 
         // -------------------------------------------------------- FP64 fix-up (encode4w_kernel's)
         auto block_px = [&](int b, int owner) {
@@ -2084,6 +2173,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
             if (lane == 0) a.wave_fix[size_t(t) * (TPB / 64) + wv] = wsum;
         }
         WSTAMP(3);
+        asm volatile("; PHASE p3" ::: "memory");
 
         // -------------------------------------------------------- sizing + the wave's offsets
         uint32_t blw[NS], rb[NS];
@@ -2123,9 +2213,10 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         const uint32_t S1 = T[0], S2 = S1 + T[1], S3 = S2 + T[2], Tw = S3 + T[3];
         if (lane == 0) misc[wv] = Tw;
         WSTAMP(4);
+        asm volatile("; PHASE p4" ::: "memory");
         lds_barrier();  // ---- the tile's bit count and this wave's place in it
         WSTAMP(5);
-        const int t_next = t + G;
+        asm volatile("; PHASE p5" ::: "memory");
 
         uint32_t A = 0, W = 0;
 #pragma unroll
@@ -2156,19 +2247,29 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
             asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // (a zero vector hoisted out of the tile loop was spilled)
             for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(reg + 4 * q) = u32x4{z, z, z, z};
         };
-        auto emit_slot = [&](int b) {  // slot b at its place in its pair's image
+        // The wave's whole image fits its region (the last record's trailing zero fields reach at
+        // most rec_bits past its start, plus the 64-bit window): all four slots are emitted before
+        // the position barrier -- beside wave 0's look-back -- and stored in one pass after it.
+        // Otherwise slot pairs in turn (pair 1 after pair 0 is stored).
+        const bool whole = Tw + uint32_t(a.rec_bits) + 64u <= 32u * kWReg;
+        auto emit_slot = [&](int b) {  // slot b at its place in the (whole or pair) image
             if (rb[b]) {
-                const uint32_t p = reg_bit0 + (Sb[b] - Sb[b & 2]) + off[b];
+                const uint32_t p = reg_bit0 + (whole ? Sb[b] : Sb[b] - Sb[b & 2]) + off[b];
                 if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
                 else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
             }
         };
-        zero_img(S2);
+        zero_img(whole ? Tw : S2);
         wave_sync();
         emit_slot(0);
         emit_slot(1);
+        if (whole) {
+            emit_slot(2);
+            emit_slot(3);
+        }
         wave_sync();
         WSTAMP(6);
+        asm volatile("; PHASE p6" ::: "memory");
         if (lane == 0 && Tw) misc[4 + wv] = reg[0];  // the wave's first 32 bits
 
         // -------------------------------------------------------- look-back (wave 0)
@@ -2247,11 +2348,37 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
             }
         }
         WSTAMP(7);
+        asm volatile("; PHASE p7" ::: "memory");
         lds_barrier();  // ---- the tile's position
         WSTAMP(8);
+        asm volatile("; PHASE p8" ::: "memory");
 
         // -------------------------------------------------------- store, slot pair by slot pair
-        const bool more = t_next < a.ntiles;
+        // The next tile is claimed only now (wave 0: the atomic here, resolved after its first
+        // store, published in misc[13] with bit 31 set; the other waves read it when they have
+        // stored): a claim made a whole tile ahead let a tile start up to a tile's time after its
+        // successor had, whose look-back then waited for it (measured 2x slower).
+        unsigned kclaim = 0;
+        if (dyn && wv == 0 && lane == 0) kclaim = atomicAdd(&cnt[kClaimStride * chain], 1u);
+        bool claimed = !dyn || wv != 0;
+        auto resolve_claim = [&]() {
+            if (!claimed) {
+                const int tn = claim_resolve(cnt, nch, tpc, seg, &chain, kclaim);
+                if (lane == 0) misc[13] = 0x80000000u | uint32_t(tn);
+                claimed = true;
+            }
+        };
+        auto next_tile = [&]() -> int {
+            if (!dyn) return a.ntiles;
+            uint32_t v;
+            for (;;) {  // (wave 0 sets it right after its first store: a short wait at most)
+                v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&misc[13], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (v & 0x80000000u) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            return v == 0xFFFFFFFFu ? -1 : int(v & 0x7FFFFFFFu);
+        };
+        int t_next = -1;
         if (Tw) {
             const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[8]))) |
                                   (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[9]))) << 32);
@@ -2275,9 +2402,11 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                 if (wv == 0 && chain_pos == 0)
                     for (uint32_t i = lane; i < uint32_t(start_bit >> 5); i += 64) hc(i, out[i]);
             }
-            store_pair(0u, S2);
+            store_pair(0u, whole ? Tw : S2);
+            resolve_claim();
             WSTAMP(9);
-            if (Tw > S2) {
+            asm volatile("; PHASE p9" ::: "memory");
+            if (!whole && Tw > S2) {
                 wave_sync();  // pair 0's image has been read
                 zero_img(Tw - S2);
                 wave_sync();
@@ -2292,7 +2421,8 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
             // every read of this wave's region is complete (the stores consumed it): the next
             // tile's pixels may land there now
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (more) issue_pixels(a, t_next);
+            t_next = next_tile();
+            if (t_next >= 0 && t_next < a.ntiles) issue_pixels(a, t_next);
             if (lane == 0) {
                 if (e && (wv < wlast || chain_last)) {  // the wave's last, partial word
                     const uint32_t v = bswap32((prev << (32u - e)) | (nexthead >> e));
@@ -2309,10 +2439,14 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                 }
             }
             WSTAMP(10);
+            asm volatile("; PHASE p10" ::: "memory");
             WRTSTAMP(15);
-        } else if (more) {
-            issue_pixels(a, t_next);
+        } else {
+            resolve_claim();
+            t_next = next_tile();
+            if (t_next >= 0 && t_next < a.ntiles) issue_pixels(a, t_next);
         }
+        const bool more = t_next >= 0 && t_next < a.ntiles;
         if constexpr (HIST) {
             lds_barrier();  // every wave's bytes counted
             uint32_t c = 0;
@@ -2325,6 +2459,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         if (!more) break;
         t = t_next;
     }
+    leave();
 }
 
 #ifndef IE_ENC_P
@@ -2355,7 +2490,7 @@ static int encode4p_grid(bool hist, size_t lds) {
 void launch_encode4w(const EncArgs& a, hipStream_t s) {
     if (IE_ENC_P && !a.ticket) {
         const size_t lds = kPLdsBytes + (a.hist ? 1024 * kWHistRep : 0);
-        const int grid = std::min(a.ntiles, encode4p_grid(a.hist != nullptr, lds));
+        const int grid = IE_P_PERSIST ? std::min(a.ntiles, encode4p_grid(a.hist != nullptr, lds)) : a.ntiles;
         if (a.hist) hipLaunchKernelGGL(encode4p_kernel<true>, dim3(grid), dim3(256), lds, s, a, a.tab);
         else hipLaunchKernelGGL(encode4p_kernel<false>, dim3(grid), dim3(256), lds, s, a, a.tab);
         return;

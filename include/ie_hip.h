@@ -285,16 +285,20 @@ int ie_decode_gop(ie_ctx* ctx, const uint8_t* in, size_t len, uint64_t start_bit
  * offset; the tables are composed G at a time, level after level). */
 int ie_last_decode_info(ie_ctx* ctx, int* chunks, int* levels);
 
-/* Record-parse mode of ie_decode_frames / ie_decode_gop.  By default (exact != 0) the exact parse
- * over composed transfer tables.  exact = 0: a call first parses speculatively -- every chunk's
- * entry is where a walk from its predecessor's first bit left it, and the counting walks, each from
- * its predecessor's speculative exit, verify every exit; on any mismatch (periodic content, e.g.
- * gradients) nothing is written and the exact parse runs.  Faster only on flat content (DESIGN.md
- * §7).  exact < 0: speculative with -exact (<= 8) warm-up chunks -- a chunk's walk starts that
- * many chunks earlier (the count pass's LDS bounds it further for long chunks).
+/* Record-parse mode of ie_decode_frames / ie_decode_gop.  By default (exact != 0, any nonzero
+ * value) the exact parse over composed transfer tables.  exact = 0: a call first parses
+ * speculatively -- every chunk's entry is where a walk from its predecessor's first bit left it,
+ * and the counting walks, each from its predecessor's speculative exit, verify every exit; on any
+ * mismatch (periodic content, e.g. gradients) nothing is written and the exact parse runs.  Faster
+ * only on flat content.
+ * ie_set_spec_warm: the speculative parse's warm-up chunks (clamped to [0, 8], default 0) -- a
+ * chunk's walk starts that many chunks earlier (the count pass's LDS bounds it further for long
+ * chunks).  (Round 4 briefly encoded the warm-up as a negative `exact`; that meaning is gone: a
+ * negative `exact` is nonzero, i.e. the exact parse, as before it.)
  * ie_last_decode_spec returns 1 when the last record decode was completed by the speculative
  * parse, 0 when by the exact one. */
 int ie_set_exact_parse(ie_ctx* ctx, int exact);
+int ie_set_spec_warm(ie_ctx* ctx, int warm);
 int ie_last_decode_spec(ie_ctx* ctx);
 
 #ifdef __cplusplus

@@ -595,7 +595,7 @@ def test_decode_speculative_equals_exact(codec, n, kind):
 @pytest.mark.parametrize("n", [4, 8])
 @pytest.mark.parametrize("warm", [1, 8])
 def test_decode_speculative_warm(codec, n, warm):
-    """Speculative parse with warm-up chunks (ie_set_exact_parse(ctx, -warm)): noise frames make
+    """Speculative parse with warm-up chunks (ie_set_spec_warm(ctx, warm)): noise frames make
     the longest chunks (8x8: C = 8192 bits), where warm = 8 would exceed the count pass's LDS
     unless the host clamps it; the pixels equal the exact parse's either way."""
     import torch

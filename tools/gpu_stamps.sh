@@ -1,7 +1,10 @@
-# encode4w per-wave phase stamps (IE_PROFILE build) of one NF-frame 4K launch, NF in $NFS
+# encode4w/4p per-wave phase stamps (IE_PROFILE builds) of one NF-frame 4K launch, NF in $NFS, for
+# every variant library named in $VARS (imageencoder_amd/lib/var_NAME; default: prof)
 R=${GRAFT_REPO_ROOT:-/root/repo}
 mkdir -p $R/gpurun_out
+for v in ${VARS:-prof}; do
 for nf in ${NFS:-1 16}; do
-  IE_LIB=$R/imageencoder_amd/lib/var_prof/libie_hip.so IE_STAMPS=$R/gpurun_out/st$nf.bin NF=$nf timeout -k 10 120 python3 $R/tools/stamp_run.py || exit 1
-  echo "== NF $nf"; python3 $R/tools/stamps_w.py $R/gpurun_out/st$nf.bin || exit 1
+  IE_LIB=$R/imageencoder_amd/lib/var_$v/libie_hip.so IE_STAMPS=$R/gpurun_out/st_${v}_$nf.bin NF=$nf timeout -k 10 120 python3 $R/tools/stamp_run.py || exit 1
+  echo "== $v NF $nf"; python3 $R/tools/stamps_w.py $R/gpurun_out/st_${v}_$nf.bin || exit 1
+done
 done

@@ -5,7 +5,9 @@ import sys
 import numpy as np
 
 names = ["start", "-", "load", "quant", "fix", "size", "scan", "emit", "lookback", "store"]
-raw16 = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 16).astype(np.int64)
+# kStamps (ie_device.h) words per tile; encode_kernel's thread 0 writes the first 16 (the rest
+# belong to encode4w/4p's per-wave stamps, tools/stamps_w.py)
+raw16 = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 64)[:, :16].astype(np.int64)
 raw = raw16[:, :10].copy()
 ghz = float(sys.argv[2]) if len(sys.argv) > 2 else 2.4
 dbg = raw[:, 1]
