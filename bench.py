@@ -12,8 +12,10 @@ A "step" is one pass of the encoder over one batch of distinct synthetic frames 
   c4 (default at N>1)  1920x1080 gop=1 video, 4x4: 64 frames per GPU (512 at N=8), sharded over
                        the ranks and assembled into ONE stream on rank 0 (all_gather of the bit
                        counts, per-rank bit re-shift, RCCL point-to-point gather); encode and
-                       gather are both timed, the gather of one sub-batch overlapping the encode
-                       of the next (imageencoder_amd/dist.py PipelinedGather)
+                       gather are both timed.  At N>1 each rank's frames go in K=2 sub-batches so
+                       that the gather of the first overlaps the encode of the second
+                       (imageencoder_amd/dist.py PipelinedGather); at N=1 there is nothing to
+                       gather and the 64 frames are one launch (K=1)
   c5                   3840x2160, 4x4, Huffman post-pass on every image (device histogram +
                        host tree build + device re-encode)
 
@@ -47,24 +49,23 @@ sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")  # data files (matrices, manifest of md5s)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROUND = "r04"  # profiles/<ROUND>_traffic_<workload>.json: this round's counter passes (tools/gpu_traffic.sh)
+ROUND = "r05"  # profiles/<ROUND>_traffic_<workload>.json: this round's counter passes (tools/gpu_traffic.sh)
 # the dominant kernel of each workload's timed launch (launch_encode: 4x4 FAST over whole 16-byte
-# groups runs encode4w_kernel; 8x8 runs encode_kernel<8>)
-KERNEL = {"c2": "encode4w_kernel<false>", "c3": "encode_kernel<8,false>", "c4": "encode4w_kernel<false>",
-          "c5": "encode4w_kernel<true>"}
+# groups runs encode4p_kernel; 8x8 runs encode_kernel<8>)
+KERNEL = {"c2": "encode4p_kernel<false>", "c3": "encode_kernel<8,false>", "c4": "encode4p_kernel<false>",
+          "c5": "encode4p_kernel<true>"}
 
 WORKLOADS = {
     "c2": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=False,
                golden="synU4k_4x4"),
     "c3": dict(w=3840, h=2160, n=8, matrix="matrix8_1.txt", batch=16, resident=64, gen="U", huffman=False,
                golden="synU4k_8x8"),
-    # c4: batch = frames per GPU per step, split into `chunks` pipelined sub-batches (1: each rank's
-    # launch is all 64 of its 1080p frames, 8 128 tiles, 5.3 rounds of the chip's resident tiles --
-    # 0.260 of HBM against 0.234 for two 32-frame launches and 0.197 for four 16-frame ones; the
-    # step at N = 1 is within 1 %, and at N > 1 rank 0's ingress of the other ranks' streams, not
-    # the encode the gather could overlap, sets it)
+    # c4: batch = frames per GPU per step, split into `chunks` pipelined sub-batches: None = 1 at one
+    # GPU (one launch of 64 1080p frames, 8 128 tiles: 0.260 of HBM against 0.234 for two 32-frame
+    # launches, round 4) and 2 above, where the first sub-batch's gather overlaps the second's encode
+    # (rank 0's ingress of the other ranks' streams, not the encode, sets the multi-GPU step)
     "c4": dict(w=1920, h=1080, n=4, matrix="matrix.txt", batch=64, resident=128, gen="U", huffman=False,
-               chunks=1, golden="vidU1080x3_4x4"),
+               chunks=None, golden="vidU1080x3_4x4"),
     "c5": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=True,
                golden="synU4k_4x4_huff"),
 }
@@ -89,7 +90,7 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="frames per launch (default: the workload's)")
     p.add_argument("--resident", type=int, default=None, help="distinct resident frames (default: the workload's)")
     p.add_argument("--chunks", type=int, default=None,
-                   help="C4: pipelined sub-batches per step (default: the workload's, 2)")
+                   help="C4: pipelined sub-batches per step (default: 1 at one GPU, 2 at more)")
     p.add_argument("--no-single-frame", dest="single_frame", action="store_false",
                    help="skip timing one-image launches (configs[1] taken literally: one 4K frame per launch)")
     return p.parse_args()
@@ -520,7 +521,7 @@ def main():
         parallelism = f"independent images sharded x{world} (no collective)"
         cpu_frame = frames[0].cpu().numpy() if rank == 0 else None
     else:  # c4: one gop=1 video stream, frames sharded over ranks, RCCL gather to rank 0
-        K = args.chunks or cfg["chunks"]
+        K = args.chunks or cfg["chunks"] or (1 if world == 1 else 2)
         m = max(B // K, 1)  # frames per rank per chunk
         nloc = m * K
         F = nloc * world
@@ -608,9 +609,14 @@ def main():
                 check.update({"golden": cfg["golden"], "md5": md5(got), "expected_md5": g["md5"]})
                 check["bit_exact"] = bool(ok and md5(got) == g["md5"])
         B = nloc
-        workload = (f"c4: {F} x {w}x{h} gop=1 video ({nloc} frames per GPU in {K} pipelined sub-batches of {m}), "
-                    f"{n}x{n} {cfg['matrix']} RLE, ONE stream assembled on rank 0 (all_gather of sizes + bit "
-                    f"re-shift + P2P gather, overlapped with the next sub-batch's encode)")
+        if world > 1:
+            workload = (f"c4: {F} x {w}x{h} gop=1 video ({nloc} frames per GPU in {K} sub-batches of {m}), "
+                        f"{n}x{n} {cfg['matrix']} RLE, ONE stream assembled on rank 0 (all_gather of sizes + bit "
+                        f"re-shift + P2P gather" + (", each sub-batch's gather overlapped with the next one's encode)"
+                                                   if K > 1 else ", after the encode: one sub-batch, no overlap)"))
+        else:
+            workload = (f"c4: {F} x {w}x{h} gop=1 video, {n}x{n} {cfg['matrix']} RLE, ONE stream: all {nloc} frames "
+                        f"in {'one launch' if K == 1 else f'{K} launches'} on one GPU (nothing to gather)")
         parallelism = (f"frame-sharded x{world} + {'RCCL' if not gloo else 'gloo (rehearsal)'} gather" if world > 1
                        else "one GPU, whole batch in one launch (no collective)")
         cpu_frame = frames[0, 0].cpu().numpy() if rank == 0 else None

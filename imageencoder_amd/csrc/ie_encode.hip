@@ -491,16 +491,33 @@ __device__ __forceinline__ uint32_t size_block(uint32_t (&zp)[N * N / 2], int rl
 }
 
 // OR the low `len` bits of v (MSB first) into the LDS bit image at bit p (len + p%32 <= 64).
+#ifndef IE_SCATTER
+#define IE_SCATTER 2  // 2: left-aligned field, funnel-shifted into the word pair (-2.7 % against 0, the 64-bit shift); 1: no LDS write (profiling)
+#endif
 __device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t v, uint32_t len) {
-    const uint32_t s = p & 31u;
-    const uint64_t x = uint64_t(v) << (64u - len - s);
     // The image is the dynamic LDS area at LDS byte address 0 (the encode kernels allocate no static
     // LDS; tools/asmcheck.py checks their group_segment_fixed_size): the word pair's byte address
     // straight from p, the second word through the instruction's offset field.
     (void)img;
     const uint32_t a = (p >> 3) & ~3u;
-    asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a), "v"(uint32_t(x >> 32)), "v"(uint32_t(x))
-                 : "memory");
+    const uint32_t s = p & 31u;
+    uint32_t hi, lo;
+    if (IE_SCATTER >= 2) {
+        const uint32_t u = v << (32u - len);  // the field left-aligned (len <= 32)
+        hi = u >> s;
+        lo = __builtin_amdgcn_alignbit(u, 0u, s);  // u << (32 - s), 0 for s = 0
+    } else {
+        const uint64_t x = uint64_t(v) << (64u - len - s);
+        hi = uint32_t(x >> 32);
+        lo = uint32_t(x);
+    }
+    // (one ds_or_b64 at a 4-byte-aligned address -- no alignment requirement assumed -- faulted the
+    // GPU: the two words stay separate ds_or_b32)
+    if (IE_SCATTER == 1) {
+        asm volatile("" ::"v"(a), "v"(hi), "v"(lo) : "memory");
+    } else {
+        asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a), "v"(hi), "v"(lo) : "memory");
+    }
 }
 
 // Branch-free variant: every pair is written (past Lw the packed coefficients are zero, so
@@ -1909,6 +1926,15 @@ __device__ __forceinline__ int claim_resolve(unsigned* cnt, int nch, int tpc, bo
 #ifndef IE_P_MFMA
 #define IE_P_MFMA 1  // 0: (A/B builds) the transform on the VALU as in encode4w_kernel
 #endif
+#ifndef IE_P_ABL
+#define IE_P_ABL 0  // (profiling builds) phases left out: 1 FP64 fix-up, 2 emission, 4 look-back, 8 store, 16 transform
+#endif
+#ifndef IE_P_LATEPROBE
+#define IE_P_LATEPROBE 0
+#endif
+#ifndef IE_P_CNTBAR
+#define IE_P_CNTBAR 0  // 1: (A/B builds) a workgroup barrier for the tile's count, not wave 0's polling
+#endif
 #ifndef IE_P_PERSIST
 #define IE_P_PERSIST 0  // 1: (A/B builds) the persistent grid with per-chain tile claims
 #endif
@@ -1995,6 +2021,10 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
     }
     if constexpr (HIST)
         for (int i = tid; i < HWORDS; i += TPB) hl[i] = 0u;
+    if ((tid & 63) == 0) {  // the waves' count flags of both misc copies
+        misc0[16 + wv] = 0u;
+        misc0[32 + 16 + wv] = 0u;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA above and the first tile's pixels)
     const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
     const bool deep = a_.deep_lb != 0;
@@ -2044,7 +2074,13 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
             __builtin_amdgcn_sched_barrier(0);
             uint32_t sf;
             float emax, lmin;
-            if (IE_P_MFMA) {
+            if (IE_P_ABL & 16) {  // (profiling) no transform: quotients = pixels / 64
+                float x[NN];
+#pragma unroll
+                for (int k = 0; k < NN; k++) x[k] = float((reg[(k >> 2) * BW + 64 * b + lane] >> (8 * (k & 3))) & 0xFFu) * 0.015625f;
+                emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
+                lmin = lim_min;
+            } else if (IE_P_MFMA) {
                 const v16i32 Jc = slot_mfma(b);
                 float Jf[16], x[16];
 #pragma unroll
@@ -2078,7 +2114,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
             for (int r = 0; r < N; r++) px.w[r] = reg[r * BW + 64 * b + owner];
             return px;
         };
-        if (__ballot(flags != 0)) {
+        if (!(IE_P_ABL & 1) && __ballot(flags != 0)) {
             const uint32_t sf = flags & 0x7777u;
             const uint32_t cnt = __popc(sf);
             uint32_t pre = 0, total = 0;
@@ -2102,8 +2138,9 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                     const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
                     const BlockPx<N> px = block_px(b, owner);
                     const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
-                    const int y = exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                    srow[NN * NN + 2 * NN + k], px);
+                    const int y = (IE_P_ABL & 32) ? int(px.w[0] & 1u)  // (profiling) no FP64 arithmetic (a small value: records stay in bound)
+                                                  : exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                                      srow[NN * NN + 2 * NN + k], px);
                     res[lane] = uint32_t(y) & 0xFFFFu;
                 }
                 wave_sync();
@@ -2211,20 +2248,33 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         off[2] = e23 & 0xFFFFu;
         off[3] = e23 >> 16;
         const uint32_t S1 = T[0], S2 = S1 + T[1], S3 = S2 + T[2], Tw = S3 + T[3];
-        if (lane == 0) misc[wv] = Tw;
+        // The tile's bit count: wave 0 alone waits for the four waves' counts (their flags in
+        // misc[16..19], cleared before the tile) and publishes it; the other waves go on to their
+        // emission and learn their place in the tile after the position barrier.  (A launch too
+        // small to fill the chip -- deep look-back -- keeps a workgroup barrier here: all four
+        // waves read predecessor windows.)
+        if (lane == 0) {
+            misc[wv] = Tw;
+            __hip_atomic_store(&misc[16 + wv], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         WSTAMP(4);
         asm volatile("; PHASE p4" ::: "memory");
-        lds_barrier();  // ---- the tile's bit count and this wave's place in it
+        if (deep || IE_P_CNTBAR) {
+            lds_barrier();
+        } else if (wv == 0) {
+            for (;;) {
+                const u32x4 f = *reinterpret_cast<const volatile u32x4*>(misc + 16);
+                if (__builtin_amdgcn_readfirstlane(f.x & f.y & f.z & f.w)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
         WSTAMP(5);
         asm volatile("; PHASE p5" ::: "memory");
 
-        uint32_t A = 0, W = 0;
+        uint32_t A = 0;  // (wave 0, or every wave in deep mode; the others after the position barrier)
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
-            A += v;
-            W += (w < wv) ? v : 0u;
-        }
+        for (int w = 0; w < 4; w++) A += __builtin_amdgcn_readfirstlane(misc[w]);
         if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);
         constexpr int DW = 2;
         Probe pr[DW];
@@ -2234,7 +2284,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
             if (deep) {
 #pragma unroll
                 for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
-            } else if (wv == 0) {
+            } else if (wv == 0 && !IE_P_LATEPROBE) {
                 pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
             }
         }
@@ -2253,7 +2303,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         // Otherwise slot pairs in turn (pair 1 after pair 0 is stored).
         const bool whole = Tw + uint32_t(a.rec_bits) + 64u <= 32u * kWReg;
         auto emit_slot = [&](int b) {  // slot b at its place in the (whole or pair) image
-            if (rb[b]) {
+            if (!(IE_P_ABL & 2) && rb[b]) {
                 const uint32_t p = reg_bit0 + (whole ? Sb[b] : Sb[b] - Sb[b & 2]) + off[b];
                 if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
                 else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
@@ -2263,6 +2313,9 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         wave_sync();
         emit_slot(0);
         emit_slot(1);
+        // (A/B builds) the first probe issued half-way through the emission: predecessors that
+        // started just before this tile have had that much longer to publish their counts
+        if (IE_P_LATEPROBE && !deep && wv == 0 && chain_pos != 0) pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
         if (whole) {
             emit_slot(2);
             emit_slot(3);
@@ -2329,7 +2382,8 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                 }
                 if (!done) {
                     const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr[0];
-                    excl = lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
+                    excl = (IE_P_ABL & 4) ? uint64_t(chain_pos) * 30000u
+                                          : lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
                 }
                 const bool have = uint32_t(pr[0].gt >> 56) == a.tag;
                 const bool split = ((start_bit + excl) & 31) != 0;
@@ -2352,6 +2406,16 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         lds_barrier();  // ---- the tile's position
         WSTAMP(8);
         asm volatile("; PHASE p8" ::: "memory");
+        uint32_t W = 0;
+        A = 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
+            A += v;
+            W += (w < wv) ? v : 0u;
+        }
+        // every wave is past the previous tile: its count flags (the other copy) are free again
+        if (lane == 0) misc0[((iter + 1) & 1) * 32 + 16 + wv] = 0u;
 
         // -------------------------------------------------------- store, slot pair by slot pair
         // The next tile is claimed only now (wave 0: the atomic here, resolved after its first
@@ -2391,7 +2455,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                 if constexpr (HIST) hc(gw, v);
             };
             auto store_pair = [&](uint32_t S0, uint32_t n) {
-                if (!n) return;
+                if (!n || (IE_P_ABL & 8)) return;
                 const uint64_t Xb = Xw + S0;
                 const uint32_t nw = uint32_t(((Xb + n) >> 5) - (Xb >> 5));
                 if constexpr (HIST) store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane, hc);

@@ -76,6 +76,7 @@ for path in args.libs:
         if r != 0:
             raise RuntimeError(L.ie_last_error(hnd))
 
+    print(f"running {path}", flush=True)  # (a fault names its variant)
     run(sizes=True)
     torch.cuda.synchronize()
     fb = C.c_uint64(0)

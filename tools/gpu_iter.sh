@@ -16,5 +16,6 @@ if [ "${BENCH:-1}" = 1 ]; then
 fi
 if [ -n "$AB" ]; then
   libs="imageencoder_amd/lib/libie_hip.so"; for v in $AB; do libs="$libs imageencoder_amd/lib/var_$v/libie_hip.so"; done
-  timeout -k 10 300 python tools/ab.py --rounds ${ROUNDS:-7} $ABARGS $libs 2>&1 | tail -8
+  timeout -k 10 300 python tools/ab.py --rounds ${ROUNDS:-7} $ABARGS $libs > $O/ab.log 2>&1; rc=$?
+  grep -v "^running" $O/ab.log | tail -12; [ $rc -eq 0 ] || { grep "^running" $O/ab.log | tail -1; exit $rc; }
 fi
