@@ -240,6 +240,10 @@ struct TrkOp {
         return lin(x, double(c), &y, -1, 0, std::fabs(double(c)) * x.E + y.E, x.integ && y.integ && is_int(c), false);
     }
     Trk addc(const Trk& x, float c) const { return lin(x, 1, nullptr, 0, double(c), x.E, x.integ && is_int(c), false); }
+    // x * c + k (one rounding, constant k)
+    Trk fmac(const Trk& x, float c, float k) const {
+        return lin(x, double(c), nullptr, 0, double(k), std::fabs(double(c)) * x.E, x.integ && is_int(c) && is_int(k), false);
+    }
 };
 
 inline double Cf(int i) { return i == 0 ? 0.5 : M_SQRT1_2; }  // algo.cpp:294-297
@@ -333,7 +337,7 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
     }
     TrkOp op{nn};
     // the matrix-pipe form: the sixteen J exact (pixels - 128), then quot4j's FP32 stage
-    std::vector<Trk> bj(nn);
+    std::vector<Trk> bj(nn), bh(nn);
     if (n == 4) {
         std::vector<Trk> xs(b), J(nn);
         for (int k = 0; k < nn; k++) xs[k].c0 = -128.0;
@@ -341,6 +345,7 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
         for (int k = 0; k < nn; k++)
             if (!J[k].integ || J[k].E != 0.0) return false;  // the integer stage must be exact
         ie::quot4j(J.data(), bj.data(), T->plan4j, op);
+        ie::quot4j<true>(J.data(), bh.data(), T->plan4j, op);
     }
     if (n == 4) ie::quot4(b.data(), T->plan4, op);
     else ie::quot8(b.data(), T->dct, T->g, op);
@@ -410,6 +415,38 @@ bool build_tables(int n, const uint16_t* q, ie::EncTables* T) {
     };
     limits(b, T->lim, T->thr, &T->lim_min, &T->dc_exact, T->g[0]);
     if (n == 4) limits(bj, T->lim4j, nullptr, &T->lim_min4j, &T->dc_exact4j, T->plan4j.G[0][0]);
+    if (n == 4) {  // t + 1/2: the tie test on fract(t + 1/2), limits rounded outward
+        T->dc_exact4h = 0;
+        T->dlo_max4h = 0.0f;
+        T->dhi_min4h = 1.0f;
+        for (int k = 0; k < nn; k++) {
+            const Trk& t = bh[k];
+            double dev = 0.0, sa = 0.0;
+            for (int m = 0; m < nn; m++) {
+                dev += std::fabs(t.a[m] - sq[k] * T->P[k * nn + m]);
+                sa += t.a[m];
+            }
+            // (the map's value at x = 128 is the 1/2 itself)
+            const double bound = t.E + 128.0 * dev + std::fabs(t.c0 + 128.0 * sa - 0.5) + 1e-9;
+            // DC: exact in quot4j (dc_exact4j) stays exact with the 1/2 added (J0 * G (a power of two)
+            // has at most 12 significant bits; the tracked fmac does not see that)
+            if (k == 0 && T->dc_exact4j) {
+                T->dlo4h[k] = -1.0f;  // never flagged
+                T->dhi4h[k] = 2.0f;
+                T->dc_exact4h = 1;
+                continue;
+            }
+            const double d = 2.0 * bound;
+            T->dlo4h[k] = std::nextafter(float(d), 1.0f);          // >= d
+            T->dhi4h[k] = std::nextafter(float(1.0 - d), 0.0f);    // <= 1 - d
+            const int h = n / 2;
+            const bool structural = (k == h) || (k == h * n) || (k == h * n + h);
+            if (!structural) {
+                T->dlo_max4h = std::max(T->dlo_max4h, T->dlo4h[k]);
+                T->dhi_min4h = std::min(T->dhi_min4h, T->dhi4h[k]);
+            }
+        }
+    }
     return ok;
 }
 

@@ -163,14 +163,17 @@ __host__ __device__ inline void dct4j_ints(const T* x, T* J, const Op& op) {
     }
 }
 
-template <class T, class Op, class Plan = Dct4JPlan>
+// HALF: every quotient is formed as t + 1/2 (the first product's addend, no extra operation): the
+// rounding then takes floor and fract of it (encode4p_kernel, round_half4).
+template <bool HALF = false, class T, class Op, class Plan = Dct4JPlan>
 __host__ __device__ inline void quot4j(const T* J, T* t, const Plan& P, const Op& op) {
 #pragma unroll
     for (int u = 0; u < 4; u++)
 #pragma unroll
         for (int v = 0; v < 4; v++) {
             const int k = 4 * u + v;
-            T acc = op.mul(J[4 * dct4j_b(u, 0) + dct4j_b(v, 0)], P.G[k][0]);
+            T acc = HALF ? op.fmac(J[4 * dct4j_b(u, 0) + dct4j_b(v, 0)], P.G[k][0], 0.5f)
+                         : op.mul(J[4 * dct4j_b(u, 0) + dct4j_b(v, 0)], P.G[k][0]);
             int m = 1;
 #pragma unroll
             for (int a = 0; a < dct4j_nb(u); a++)
@@ -200,6 +203,7 @@ struct FloatOp {
     __device__ __forceinline__ float fma(float a, float c, float b) const { return __builtin_fmaf(a, c, b); }
     __device__ __forceinline__ float fms(float a, float c, float b) const { return __builtin_fmaf(a, c, -b); }
     __device__ __forceinline__ float addc(float a, float c) const { return a + c; }
+    __device__ __forceinline__ float fmac(float a, float c, float k) const { return __builtin_fmaf(a, c, k); }
 };
 
 }  // namespace ie

@@ -31,6 +31,12 @@ struct EncTables {
     float lim4j[16];
     float lim_min4j;
     int dc_exact4j;
+    // the same stage forming t + 1/2 (quot4j<true>): coefficient k is near a rounding tie when
+    // fract(t + 1/2) <= dlo4h[k] or >= dhi4h[k] (2 x its tracked bound, rounded outward); the
+    // non-structural coefficients share the loosest pair (dlo_max4h, dhi_min4h)
+    float dlo4h[16], dhi4h[16];
+    float dlo_max4h, dhi_min4h;
+    int dc_exact4h;
     uint32_t mfma_w[64][4];
     // 4x4: P[16][16] then S, rq, qd of every coefficient, contiguous (the fix-up's LDS copy, staged
     // by DMA: 152 lanes x 16 bytes)

@@ -453,6 +453,35 @@ __device__ __forceinline__ uint32_t pk_sign_i16(uint32_t w) {  // per half: h >>
 // packed-int16 instruction.  Returns bl | Lw << 8 and the record length in bits.  In the RLE
 // truncation case (L == N*N, z[N*N-2] == 0: the reference drops the last coefficient,
 // Block.cpp:388-390) z[N*N-1] is cleared, so every coefficient at or past Lw is zero.
+// 4x4 form with 32-bit masks throughout (the 64-bit nz mask cost 64-bit compares and moves), the
+// pair masks merged by shift-or and the widest value by one three-input op per word.
+__device__ __forceinline__ uint32_t size_block4(uint32_t (&zp)[8], int rle, uint32_t* bits) {
+    uint32_t M = 0, mo = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t w = zp[j];
+        M = (pk_min1_u16(w) << (2 * j)) | M;  // v_lshl_or_b32
+        mo = (w ^ pk_sign_i16(w)) | mo;  // one v_bitop3 (the compiler's table: a hand-written one had the operands swapped)
+    }
+    const uint32_t nz = (M & 0x5555u) | ((M >> 15) & 0xAAAAu);  // bit kz: z[kz] != 0
+    mo = (mo | (mo >> 16)) & 0xFFFFu;
+    const int maxb = 33 - __clz(mo);
+    const int L = 32 - __clz(nz);                       // 0 for nz == 0
+    const int ffsL = L ? 32 - __clz(uint32_t(L)) : 1;  // utils.hpp:210-216, with ffs(0) == 1
+    const int bl = max(maxb, ffsL);
+    int lw;
+    if (!rle) {
+        lw = 16;
+    } else if (L == 16 && !((nz >> 14) & 1u)) {
+        lw = 32 - __clz(nz & 0x7FFFu);  // drop the last element (Block.cpp:388-390)
+        zp[7] &= 0xFFFFu;
+    } else {
+        lw = L;
+    }
+    *bits = __umul24(uint32_t(bl), uint32_t(lw + rle)) + 4u;
+    return uint32_t(bl) | (uint32_t(lw) << 8);
+}
+
 template <int N>
 __device__ __forceinline__ uint32_t size_block(uint32_t (&zp)[N * N / 2], int rle, uint32_t* bits) {
     constexpr int NN = N * N;
@@ -486,7 +515,7 @@ __device__ __forceinline__ uint32_t size_block(uint32_t (&zp)[N * N / 2], int rl
     } else {
         lw = L;
     }
-    *bits = 4u + uint32_t(bl) * uint32_t(lw + rle);
+    *bits = __umul24(uint32_t(bl), uint32_t(lw + rle)) + 4u;  // (a 64-bit v_mad otherwise)
     return uint32_t(bl) | (uint32_t(lw) << 8);
 }
 
@@ -1920,6 +1949,64 @@ __device__ __forceinline__ int claim_resolve(unsigned* cnt, int nch, int tpc, bo
     }
 }
 
+// Rounding of quotients formed as t + 1/2 (quot4j<true>): rint(t) = floor(t + 1/2) away from ties
+// (one v_cvt_flr_i32_f32), and t is within the bound of a tie exactly when f = fract(t + 1/2) is
+// within it of 0 or 1 -- the thirteen ordinary coefficients by one min and one max over their f,
+// the structural three one by one (sflags bits 0-2).  Returns whether an ordinary coefficient may
+// be at a tie.  At an exact tie floor(t + 1/2) need not be the reference's value: every tie is
+// flagged and re-evaluated.  DC (dcx: exact, q[0] a power of two): std::round's half away from
+// zero from t + 1/2 directly.
+struct HalfLims {
+    float lo0, hi0, lo1, hi1, lo2, hi2, lo, hi;
+};
+__device__ __forceinline__ bool round_half4(const float (&tp)[16], uint32_t (&zp)[8], uint32_t* sflags, bool dcx,
+                                            const HalfLims& L) {
+    constexpr int S0 = Structural<4>::k[0], S1 = Structural<4>::k[1], S2 = Structural<4>::k[2];
+    float fmin = 1.0f, fmax = 0.0f;
+    uint32_t sf = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        int r[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int k = ZigZag<4>::idx[2 * j + h];
+            const float x = tp[k];
+            const float f = __builtin_amdgcn_fractf(x);
+            asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r[h]) : "v"(x));  // (floorf + a conversion would be two)
+            if (k == 0) {
+                // t >= 0: floor(t + 1/2); t < 0: -floor(1/2 - t) = -floor(1 - (t + 1/2))
+                const int neg = -int(floorf(1.0f - x));
+                r[h] = dcx ? (x >= 0.5f ? r[h] : neg) : r[h];
+                fmin = dcx ? fmin : fminf(fmin, f);
+                fmax = dcx ? fmax : fmaxf(fmax, f);
+            } else if (k == S0) {
+                sf |= (f <= L.lo0 || f >= L.hi0) ? 1u : 0u;
+            } else if (k == S1) {
+                sf |= (f <= L.lo1 || f >= L.hi1) ? 2u : 0u;
+            } else if (k == S2) {
+                sf |= (f <= L.lo2 || f >= L.hi2) ? 4u : 0u;
+            } else {
+                fmin = fminf(fmin, f);
+                fmax = fmaxf(fmax, f);
+            }
+        }
+        zp[j] = __builtin_amdgcn_perm(uint32_t(r[1]), uint32_t(r[0]), 0x05040100u);
+        asm volatile("" : "+v"(zp[j]));
+    }
+    *sflags = sf;
+    return fmin <= L.lo || fmax >= L.hi;
+}
+
+#ifndef IE_P_SIZE4
+#define IE_P_SIZE4 1
+#endif
+#ifndef IE_P_DPPFIX
+#define IE_P_DPPFIX 1
+#endif
+#ifndef IE_P_RHALF
+#define IE_P_RHALF 0  // 1: (A/B builds) floor / fract of t + 1/2 (round_half4): +1.5 % VALU, slower
+#endif
+
 #ifndef IE_P_WAVES
 #define IE_P_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD)
 #endif
@@ -2057,9 +2144,12 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         using KTab = const __attribute__((address_space(4))) EncTables;
         KTab* tb = (KTab*)(tab);  // constant address space: scalar loads
         asm volatile("" : "+s"(tb));
-        const bool dcx = tb->dc_exact4j != 0;
+        const bool dcx = IE_P_RHALF ? tb->dc_exact4h != 0 : tb->dc_exact4j != 0;
         const float lim_s0 = tb->lim4j[Structural<4>::k[0]], lim_s1 = tb->lim4j[Structural<4>::k[1]],
                     lim_s2 = tb->lim4j[Structural<4>::k[2]], lim_min = tb->lim_min4j;
+        constexpr int K0 = Structural<4>::k[0], K1 = Structural<4>::k[1], K2 = Structural<4>::k[2];
+        const HalfLims hl4{tb->dlo4h[K0], tb->dhi4h[K0], tb->dlo4h[K1], tb->dhi4h[K1],
+                           tb->dlo4h[K2], tb->dhi4h[K2], tb->dlo_max4h, tb->dhi_min4h};
         uint32_t zp[NS][NP];
         uint32_t flags = 0;  // 4 bits per slot: structural s (bits 0-2), whole block (bit 3)
         auto slot_mfma = [&](int b) {
@@ -2080,6 +2170,14 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                 for (int k = 0; k < NN; k++) x[k] = float((reg[(k >> 2) * BW + 64 * b + lane] >> (8 * (k & 3))) & 0xFFu) * 0.015625f;
                 emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
                 lmin = lim_min;
+            } else if (IE_P_MFMA && IE_P_RHALF) {
+                const v16i32 Jc = slot_mfma(b);
+                float Jf[16], x[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) Jf[k] = float(Jc[k]);
+                quot4j<true>(Jf, x, tb->plan4j, FloatOp());
+                emax = round_half4(x, zp[b], &sf, dcx, hl4) ? 1.0f : 0.0f;
+                lmin = 0.5f;
             } else if (IE_P_MFMA) {
                 const v16i32 Jc = slot_mfma(b);
                 float Jf[16], x[16];
@@ -2117,12 +2215,20 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
         if (!(IE_P_ABL & 1) && __ballot(flags != 0)) {
             const uint32_t sf = flags & 0x7777u;
             const uint32_t cnt = __popc(sf);
-            uint32_t pre = 0, total = 0;
+            uint32_t pre, total;
+            if (IE_P_DPPFIX) {  // the lanes' request counts placed by one DPP wave scan
+                const uint32_t incl = wave_incl_scan_dpp(cnt);
+                pre = incl - cnt;
+                total = __builtin_amdgcn_readlane(incl, 63);
+            } else {  // (A/B builds) a 4-plane ballot prefix
+                pre = 0;
+                total = 0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {  // cnt <= 12
-                const uint64_t bm = __ballot((cnt >> k) & 1u);
-                pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
-                total += uint32_t(__popcll(bm)) << k;
+                for (int k = 0; k < 4; k++) {  // cnt <= 12
+                    const uint64_t bm = __ballot((cnt >> k) & 1u);
+                    pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+                    total += uint32_t(__popcll(bm)) << k;
+                }
             }
             for (uint32_t r0 = 0; r0 < total; r0 += 64) {
                 uint32_t m = sf, i = pre - r0;
@@ -2227,7 +2333,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
-            blw[b] = size_block<N>(zp[b], a.rle, &rb[b]);
+            blw[b] = IE_P_SIZE4 ? size_block4(zp[b], a.rle, &rb[b]) : size_block<N>(zp[b], a.rle, &rb[b]);
             rb[b] = valid ? rb[b] : 0u;
             asm volatile("" : "+v"(blw[b]), "+v"(rb[b]));
 #pragma unroll
