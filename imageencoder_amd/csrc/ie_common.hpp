@@ -206,10 +206,11 @@ constexpr int kLbAhead = IE_LB_AHEAD;
 // first probe are issued at once, before it is evaluated.
 template <int kLbAhead = ie::kLbAhead>
 __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
-                                  unsigned* err, unsigned* rounds = nullptr, bool deep = false) {
+                                  unsigned* err, unsigned* rounds = nullptr, bool deep = false,
+                                  int width0 = kProbe0) {
     const int lane = lane_id();
     uint64_t excl = 0;
-    int d0 = 0, width = kProbe0;
+    int d0 = 0, width = width0;  // (the first probe's width)
     unsigned spins = 0;
     Probe ahead[kLbAhead];  // windows d0 + 64, d0 + 128, ... already in flight
     int nahead = 0;

@@ -2632,6 +2632,565 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
     leave();
 }
 
+// =============================================================================================
+// encode4q_kernel -- encode4p_kernel's tile, SOFTWARE-PIPELINED over a persistent grid.
+//   * Grid = the workgroups the chip holds at once (occupancy API, capped at IE_Q_PER_CU per CU);
+//     workgroup w takes tiles w, w + G, w + 2G, ... in that order (static: no claim atomics).  A
+//     tile's look-back waits only on tiles of earlier rounds or of earlier workgroups of its own
+//     round -- all resident -- so the order cannot deadlock.
+//   * Two pixel/image buffers per wave: tile k+1's pixels land by DMA while tile k is worked on.
+//   * Deferred back end: iteration k runs front(k) (transform, FP64 fix-up, sizing, the count),
+//     then back(k-1) (look-back, position barrier, store), then the DMA of tile k+1, then
+//     emit(k).  A tile's look-back thus runs a whole front stage after its predecessors
+//     published their counts (and after the round before published its inclusive prefixes), and
+//     the probe it evaluates (issued when the iteration starts) has had that long to return.
+//     Only a tile with a wave image too large for the buffer (slot pairs in turn) runs its back
+//     end at once.
+//   * Tile boundary word: the word holding a tile's first bits and its predecessor's last is
+//     written by whichever of the two reaches it second, found by ONE 64-bit exchange on the
+//     successor's granule 3 (atomics on one address are ordered: exactly one of the two sees the
+//     other's half) -- no tile waits for its predecessor's tail.
+// =============================================================================================
+#ifndef IE_ENC_Q
+#define IE_ENC_Q 1  // 0: (A/B builds) large 4x4 FAST batches on encode4p_kernel
+#endif
+#ifndef IE_Q_PER_CU
+#define IE_Q_PER_CU 4
+#endif
+#ifndef IE_Q_PROBE
+#define IE_Q_PROBE 64  // first look-back window of a deferred back end (predecessors)
+#endif
+constexpr int kQMisc = 3 * 32;  // three copies of encode4w_kernel's misc words (tile k: copy k % 3)
+constexpr int kQLdsBytes = (8 * kWReg + 4 * kWTask + kQMisc + kPWfrag) * 4 + kWRows * 8;
+static_assert(kGran >= 4, "encode4q_kernel's boundary exchange uses granule 3");
+
+// One side of a tile-boundary word: role 1 = the tile ending in it, 2 = the tile starting in it;
+// part = that tile's bits of the word (before the byte swap).  Returns the old granule.
+__device__ __forceinline__ uint64_t boundary_swap(uint64_t* st, int succ, uint32_t tag, uint32_t role, uint32_t part) {
+    const uint64_t v = (uint64_t(tag) << 56) | (uint64_t(role) << 48) | part;
+    return __hip_atomic_exchange(&st[kGran * succ + 3], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The second side writes the word.
+__device__ __forceinline__ void boundary_finish(uint32_t* out, uint64_t word, uint64_t old, uint32_t tag, uint32_t role,
+                                                uint32_t part) {
+    if (uint32_t(old >> 56) == tag && uint32_t((old >> 48) & 0xFFu) == 3u - role) out[word] = bswap32(part | uint32_t(old));
+}
+
+__global__ __launch_bounds__(256, IE_Q_PER_CU) void encode4q_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
+    constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
+    constexpr int GW = 16 * NS, BW = 64 * NS, TG = 4 * GW;  // groups / blocks per wave, groups per tile
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int tid0 = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+    uint32_t* const task = smem + 8 * kWReg + wv * kWTask;
+    uint32_t* const res = task + 64;
+    uint32_t* const misc0 = smem + 8 * kWReg + 4 * kWTask;  // [3][32]
+    uint32_t* const wl = misc0 + kQMisc;                    // [64][4]: the matrix-pipe A fragments
+    double* const srow = reinterpret_cast<double*>(wl + kPWfrag);
+    const int G = int(gridDim.x);
+    const int wg = int(blockIdx.x);
+    using KArgs = const __attribute__((address_space(4))) EncArgs;
+    KArgs* ka = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+    // tiles by per-chain claims (encode4p_kernel's counters and claim_resolve), made two tiles
+    // ahead: tile k+2 is claimed when iteration k starts and resolved when tile k+1's pixels are
+    // requested; misc copy k % 3 word 13 holds tile k (-1: none)
+    const bool seg = a_.segmented != 0;
+    const int nch = seg ? a_.nframes : 1, tpc = seg ? a_.tiles_per_frame : a_.ntiles;
+    unsigned* const cnt = a_.claim;
+    int chain = wg % nch;  // (wave 0's copy counts)
+    bool claiming = true;
+    // wave wv's buffer par (0/1): pixels [4 rows][BW], then the tile's wave image
+    auto bufp = [&](int par) { return smem + (par * 4 + wv) * kWReg; };
+    auto issue_pixels = [&](KArgs& a, int tt, int par) {
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const TileGeo gg = tile_geo<4, 4, TG>(a, tt, tid);
+        if (gg.nblk) {
+            uint32_t* const reg = bufp(par);
+            const uint8_t* base = a.y + size_t(gg.frame) * a.frame_pitch + size_t(gg.byi) * N * a.stride + size_t(gg.bx0) * N;
+#pragma unroll
+            for (int r = 0; r < N; r++)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
+                                                 (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, 0);
+        }
+    };
+    {
+        const int lane0 = tid0 & 63;
+        static_assert(kWRows * 8 == 2 * 1024 + 24 * 16, "rows: two full waves and 24 lanes of 16 bytes");
+        if (wv < 2 || (wv == 2 && lane0 < 24))
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->rows4[wv * 128 + 2 * lane0]),
+                                             (__attribute__((address_space(3))) void*)(srow + wv * 128), 16, 0, 0);
+        else if (wv == 3)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->mfma_w[lane0][0]),
+                                             (__attribute__((address_space(3))) void*)(wl), 16, 0, 0);
+    }
+    if ((tid0 & 63) == 0) {  // the waves' count flags of the three misc copies
+#pragma unroll
+        for (int c = 0; c < 3; c++) misc0[32 * c + 16 + wv] = 0u;
+    }
+    if (wv == 0) {  // the first two tiles: two positions of the workgroup's chain by one atomic
+        unsigned k0 = 0;
+        if ((tid0 & 63) == 0) k0 = atomicAdd(&cnt[kClaimStride * chain], 2u);
+        const int k0u = __builtin_amdgcn_readfirstlane(int(k0));
+        int ta = -1, tb2 = -1;
+        if (k0u + 1 < tpc) {
+            ta = seg ? k0u * nch + chain : k0u;
+            tb2 = seg ? (k0u + 1) * nch + chain : k0u + 1;
+        } else {  // (the chain ends here: the next chains by claim_resolve)
+            ta = claim_resolve(cnt, nch, tpc, seg, &chain, k0);
+            if (ta >= 0) {
+                unsigned kn = 0;
+                if ((tid0 & 63) == 0) kn = atomicAdd(&cnt[kClaimStride * chain], 1u);
+                tb2 = claim_resolve(cnt, nch, tpc, seg, &chain, kn);
+            }
+        }
+        claiming = tb2 >= 0;
+        if ((tid0 & 63) == 0) {
+            misc0[13] = uint32_t(ta);
+            misc0[32 + 13] = uint32_t(tb2);
+        }
+    }
+    const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
+    lds_barrier();  // the first two tiles known
+    {
+        const int ta = __builtin_amdgcn_readfirstlane(int(misc0[13])), tb2 = __builtin_amdgcn_readfirstlane(int(misc0[32 + 13]));
+        if (ta >= 0) issue_pixels(*ka, ta, 0);
+        if (tb2 >= 0) issue_pixels(*ka, tb2, 1);
+    }
+    // (every workgroup counts its exit; the last one leaves the claim counters zero)
+    auto leave = [&]() {
+        if (tid0 == 0) {
+            const unsigned e = atomicAdd(&cnt[kClaimStride * nch], 1u);
+            if (e == unsigned(G) - 1u) {
+                for (int c = 0; c <= nch; c++) __hip_atomic_store(&cnt[kClaimStride * c], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    };
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();  // the rows, the A fragments visible
+
+    // the front stage's results (one tile at a time; function scope for back()'s slot-pair case)
+    uint32_t zp[NS][NP], blw[NS], rb[NS], off[NS];
+    uint32_t S2 = 0, S3 = 0;
+
+    // -------------------------------------------------------- the back end of tile tt
+    // (position: wave 0's look-back; every wave's store; the tile-boundary exchanges)
+    // now: the tile of this iteration (its image may be in slot pairs: zp of slots 2-3 live)
+    int qst = 0;  // (profiling builds) the tile whose stamp row this iteration fills
+#define QSTAMP(i)                                                                                         \
+    do {                                                                                                  \
+        if (IE_PROFILE && a.stamps && (threadIdx.x & 63) == 0) a.stamps[size_t(qst) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define QRTSTAMP(i)                                                                                       \
+    do {                                                                                                  \
+        if (IE_PROFILE && a.stamps && (threadIdx.x & 63) == 0) a.stamps[size_t(qst) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    auto back = [&](int tt, int kk, bool now, const Probe& p0) {
+        asm volatile("" : "+s"(ka));
+        KArgs& a = *ka;
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63;
+        const TileGeo gb = tile_geo<4, 4, TG>(a, tt, tid);
+        const int bframe = gb.frame, btif = gb.tif, bstep = gb.step, bpos = gb.chain_pos;
+        const int bng = min(TG, a.groups_per_frame - btif * TG);
+        const int wlast = (bng - 1) / GW;  // the tile's last non-empty wave
+        uint32_t* const bm = misc0 + (kk % 3) * 32;
+        uint32_t* const breg = bufp(kk & 1);
+        const bool chain_last = a.segmented ? (btif == a.tiles_per_frame - 1) : (tt == a.ntiles - 1);
+        uint32_t* const out = a.out + (a.segmented ? uint64_t(bframe) * a.out_pitch_words : 0ull);
+        if (wv == 0) {
+            uint32_t A = 0;
+#pragma unroll
+            for (int w = 0; w < 4; w++) A += __builtin_amdgcn_readfirstlane(bm[w]);
+            uint64_t excl = 0;
+            uint32_t ptail = 0, pend = 0;
+            if (bpos == 0) {
+                const uint32_t s = uint32_t(start_bit & 31);
+                ptail = s ? (bswap32(out[start_bit >> 5]) >> (32 - s)) : 0u;
+            } else {
+                const Probe q = now ? probe_issue(a.st, tt, bpos, bstep, 0, IE_Q_PROBE) : p0;
+                QSTAMP(12);
+                unsigned rounds = 0;
+                excl = lookback_wave<IE_W_AHEAD>(q, a.st, tt, bpos, bstep, a.tag, a.err, IE_PROFILE ? &rounds : nullptr, false, IE_Q_PROBE);
+                pend = ((start_bit + excl) & 31) != 0 ? 1u : 0u;  // the boundary word: exchanged
+                if (IE_PROFILE && a.stamps && lane == 0) a.stamps[size_t(qst) * kStamps + 13] = rounds;
+            }
+            QSTAMP(5);
+            if (lane == 0) {
+                if (bpos != 0) publish(a.st, tt, 1, a.tag, excl + A);
+                bm[8] = uint32_t(excl);
+                bm[9] = uint32_t(excl >> 32);
+                bm[10] = ptail;
+                bm[11] = pend;
+                const uint64_t P = start_bit + excl;
+                if (btif == 0) a.frame_start[bframe] = P;
+                if (chain_last) a.chain_end[a.segmented ? bframe : 0] = P + A;
+            }
+        }
+        lds_barrier();  // ---- the tile's position
+        QSTAMP(6);
+        uint32_t W = 0, A = 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const uint32_t v = __builtin_amdgcn_readfirstlane(bm[w]);
+            A += v;
+            W += (w < wv) ? v : 0u;
+        }
+        const uint32_t bTw = __builtin_amdgcn_readfirstlane(bm[wv]);
+        if (!bTw) return;
+        const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(bm[8]))) |
+                              (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(bm[9]))) << 32);
+        const uint64_t Xw = start_bit + excl + W;
+        const bool pend = __builtin_amdgcn_readfirstlane(bm[11]) != 0u;
+        const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
+        uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(bm[10]) : 0u;
+        const bool whole = bTw + uint32_t(a.rec_bits) + 64u <= 32u * kWReg;
+        const uint64_t E = Xw + bTw;
+        const uint32_t e = uint32_t(E) & 31u;
+        // the boundary exchanges, issued before the stores (their round trip overlaps them)
+        const bool xs = wv == 0 && pend;                                 // this tile's first word
+        const bool xp = wv == wlast && e != 0u && !chain_last;           // its last word
+        const uint32_t s0 = uint32_t(Xw) & 31u;
+        const uint32_t head = __builtin_amdgcn_readfirstlane(bm[4 + wv]);
+        uint64_t oldS = 0, oldP = 0;
+        if (lane == 0 && xs) oldS = boundary_swap(a.st, tt, a.tag, 2u, head >> s0);
+        if (xp && whole) {
+            const uint32_t tw = slot_tail32(breg, bTw, prev);  // (= prev after the store)
+            if (lane == 0) oldP = boundary_swap(a.st, tt + bstep, a.tag, 1u, tw << (32u - e));
+        }
+        auto store_pair = [&](uint32_t S0, uint32_t n) {
+            if (!n) return;
+            const uint64_t Xb = Xw + S0;
+            const uint32_t nw = uint32_t(((Xb + n) >> 5) - (Xb >> 5));
+            store_slot(out, breg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
+            prev = slot_tail32(breg, n, prev);
+        };
+        if (whole) {
+            store_pair(0u, bTw);
+        } else if (now) {  // (slot pairs in turn: the zp of slots 2-3 are this iteration's)
+            store_pair(0u, S2);
+            if (bTw > S2) {
+                wave_sync();  // pair 0's image has been read
+                const uint32_t nq = (bTw - S2 + 127u) >> 7;
+                uint32_t z;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(breg + 4 * q) = u32x4{z, z, z, z};
+                wave_sync();
+                const uint32_t reg_bit0 = uint32_t(((kk & 1) * 4 + wv) * kWReg) * 32u;
+#pragma unroll
+                for (int b = 2; b < 4; b++) {
+                    if (rb[b]) {
+                        const uint32_t p = reg_bit0 + (b == 2 ? 0u : (S3 - S2)) + off[b];
+                        if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
+                        else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
+                    }
+                }
+                wave_sync();
+                store_pair(S2, bTw - S2);
+            }
+            if (lane == 0 && xp) oldP = boundary_swap(a.st, tt + bstep, a.tag, 1u, prev << (32u - e));
+        }
+        const uint32_t nexthead = (e && wv < wlast) ? bm[4 + wv + 1] : 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (every read of the buffer is done)
+        QSTAMP(7);
+        if (lane == 0) {
+            if (e && (wv < wlast || chain_last)) out[E >> 5] = bswap32((prev << (32u - e)) | (nexthead >> e));
+            if (xs) boundary_finish(out, Xw >> 5, oldS, a.tag, 2u, head >> s0);
+            if (xp) boundary_finish(out, E >> 5, oldP, a.tag, 1u, prev << (32u - e));
+        }
+    };
+
+    Probe prc{0, 0, 0};     // wave 0: the first look-back probe of the tile whose back end is deferred
+    bool deferred = false;  // the previous tile's back end is still to run
+    int t_prev = -1, klast = 0;
+    for (int k = 0;; k++) {
+        asm volatile("" : "+s"(ka));
+        KArgs& a = *ka;
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63;
+        uint32_t* const misc = misc0 + (k % 3) * 32;
+        const int t = __builtin_amdgcn_readfirstlane(int(misc[13]));
+        if (t < 0) break;
+        uint32_t* const reg = bufp(k & 1);
+        unsigned kc = 0;  // wave 0: the claim of tile k + 2, resolved at tile k+1's pixel request
+        if (wv == 0 && claiming && lane == 0) kc = atomicAdd(&cnt[kClaimStride * chain], 1u);
+        const TileGeo g = tile_geo<4, 4, TG>(a, t, tid);
+        const int frame = g.frame, tif = g.tif, chain_pos = g.chain_pos;
+        const int ng = min(TG, a.groups_per_frame - tif * TG);
+        const int nbw = 4 * min(GW, max(0, ng - GW * wv));  // blocks of this wave
+        qst = t;
+        QRTSTAMP(14);
+        QSTAMP(11);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's pixels (and every older access)
+        QSTAMP(0);
+        // the deferred tile's first probe, in flight during this tile's front stage
+        if (deferred && wv == 0) {
+            const int tp = t_prev;
+            const TileGeo gp = tile_geo<4, 4, TG>(a, tp, tid);
+            if (gp.chain_pos != 0) prc = probe_issue(a.st, tp, gp.chain_pos, gp.step, 0, IE_Q_PROBE);
+        }
+
+        // -------------------------------------------------------- front: transform + quantise
+        using KTab = const __attribute__((address_space(4))) EncTables;
+        KTab* tb = (KTab*)(tab);
+        asm volatile("" : "+s"(tb));
+        const bool dcx = tb->dc_exact4j != 0;
+        const float lim_s0 = tb->lim4j[Structural<4>::k[0]], lim_s1 = tb->lim4j[Structural<4>::k[1]],
+                    lim_s2 = tb->lim4j[Structural<4>::k[2]], lim_min = tb->lim_min4j;
+        uint32_t flags = 0;  // 4 bits per slot: structural s (bits 0-2), whole block (bit 3)
+#pragma unroll
+        for (int b = 0; b < NS; b++) {
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t sf;
+            v4i32 px;
+#pragma unroll
+            for (int r = 0; r < N; r++) px[r] = int(reg[r * BW + 64 * b + lane] ^ 0x80808080u);  // x - 128 as i8
+            const v4i32 wfrag = *reinterpret_cast<const v4i32*>(wl + 4 * lane);
+            const v16i32 Jc = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfrag, px, v16i32{}, 0, 0, 0);
+            float Jf[16], x[16];
+#pragma unroll
+            for (int kk = 0; kk < 16; kk++) Jf[kk] = float(Jc[kk]);
+            quot4j(Jf, x, tb->plan4j, FloatOp());
+            const float emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
+            const uint32_t fb = (emax >= lim_min) ? 8u : sf;
+            if (64 * b + lane < nbw) flags |= fb << (4 * b);
+#pragma unroll
+            for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
+            asm volatile("" : "+v"(flags));
+        }
+
+        QSTAMP(1);
+        // -------------------------------------------------------- FP64 fix-up (encode4p_kernel's)
+        auto block_px = [&](int b, int owner) {
+            BlockPx<N> px;
+#pragma unroll
+            for (int r = 0; r < N; r++) px.w[r] = reg[r * BW + 64 * b + owner];
+            return px;
+        };
+        if (__ballot(flags != 0)) {
+            const uint32_t sf = flags & 0x7777u;
+            const uint32_t cnt = __popc(sf);
+            const uint32_t incl = wave_incl_scan_dpp(cnt);
+            const uint32_t pre = incl - cnt, total = __builtin_amdgcn_readlane(incl, 63);
+            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+                uint32_t m = sf, i = pre - r0;
+                while (m) {
+                    const int bit = __ffs(m) - 1;
+                    m &= m - 1;
+                    if (i < 64u) task[i] = (uint32_t(lane) << 4) | uint32_t(bit);
+                    i++;
+                }
+                wave_sync();
+                if (uint32_t(lane) < total - r0) {
+                    const uint32_t tk = task[lane];
+                    const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
+                    const BlockPx<N> px = block_px(b, owner);
+                    const int kc = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
+                    const int y = exact_coef_row<N>(srow + kc * NN, srow[NN * NN + kc], srow[NN * NN + NN + kc],
+                                                    srow[NN * NN + 2 * NN + kc], px);
+                    res[lane] = uint32_t(y) & 0xFFFFu;
+                }
+                wave_sync();
+                i = pre - r0;
+#pragma unroll
+                for (int b = 0; b < NS; b++)
+#pragma unroll
+                    for (int ss = 0; ss < 3; ss++) {
+                        if ((sf >> (4 * b + ss)) & 1u) {
+                            const int zw = Structural<N>::zpos(ss) >> 1;
+                            if (i < 64u) zp[b][zw] = __builtin_amdgcn_perm(res[i], zp[b][zw], 0x05040100u);  // res low -> high half
+                            i++;
+                        }
+                    }
+                wave_sync();
+            }
+            const uint32_t wf = flags & 0x8888u;
+            if (__ballot(wf != 0)) {
+                const uint32_t nb = __popc(wf);
+                uint32_t pb = 0, tbk = 0;
+#pragma unroll
+                for (int kk = 0; kk < 3; kk++) {  // nb <= 4
+                    const uint64_t bm = __ballot((nb >> kk) & 1u);
+                    pb += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << kk;
+                    tbk += uint32_t(__popcll(bm)) << kk;
+                }
+                for (uint32_t r0 = 0; r0 < tbk; r0 += 4) {
+                    uint32_t m = wf, j = pb - r0;
+                    while (m) {
+                        const int b = (__ffs(m) - 1) >> 2;
+                        m &= m - 1;
+                        if (j < 4u) task[j] = (uint32_t(lane) << 4) | uint32_t(b);
+                        j++;
+                    }
+                    wave_sync();
+                    if (uint32_t(lane >> 4) < tbk - r0) {
+                        const uint32_t tk = task[lane >> 4];
+                        const int b = int(tk & 3u), owner = int(tk >> 4), kc = lane & 15;
+                        const BlockPx<N> px = block_px(b, owner);
+                        const int y = exact_coef_row<N>(srow + kc * NN, srow[NN * NN + kc], srow[NN * NN + NN + kc],
+                                                        srow[NN * NN + 2 * NN + kc], px);
+                        res[lane] = uint32_t(y) & 0xFFFFu;
+                    }
+                    wave_sync();
+                    m = wf;
+                    j = pb - r0;
+                    while (m) {
+                        const int b = (__ffs(m) - 1) >> 2;
+                        m &= m - 1;
+                        if (j < 4u) {
+                            const uint32_t* rr = res + 16 * j;
+#pragma unroll
+                            for (int jj = 0; jj < NP; jj++) {
+                                const uint32_t w = rr[ZigZag<N>::idx[2 * jj]] | (rr[ZigZag<N>::idx[2 * jj + 1]] << 16);
+#pragma unroll
+                                for (int bb = 0; bb < NS; bb++) zp[bb][jj] = (b == bb) ? w : zp[bb][jj];
+                            }
+                        }
+                        j++;
+                    }
+                    wave_sync();
+                }
+            }
+        }
+        {  // statistics: FP64 requests of this wave (one store)
+            const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan_dpp(uint32_t(__popc(flags))), 63);
+            if (lane == 0) a.wave_fix[size_t(t) * (TPB / 64) + wv] = wsum;
+        }
+
+        QSTAMP(2);
+        // -------------------------------------------------------- sizing + the wave's offsets
+        const uint32_t k0 = uint32_t(tif * TG + GW * wv) * 4u;  // the wave's first block (frame raster order)
+#pragma unroll
+        for (int b = 0; b < NS; b++) {
+            const bool valid = 64 * b + lane < nbw;
+            if (a.coef && valid) {
+                int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + k0 + 64 * b + lane) * NN;
+#pragma unroll
+                for (int kk = 0; kk < NN; kk++) {
+                    const int kz = ZigZagInv<N>::pos[kk];
+                    dst[kk] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            blw[b] = size_block4(zp[b], a.rle, &rb[b]);
+            rb[b] = valid ? rb[b] : 0u;
+            asm volatile("" : "+v"(blw[b]), "+v"(rb[b]));
+#pragma unroll
+            for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const uint32_t s01 = rb[0] | (rb[1] << 16), s23 = rb[2] | (rb[3] << 16);
+        const uint32_t i01 = wave_incl_scan_dpp(s01), i23 = wave_incl_scan_dpp(s23);
+        const uint32_t t01 = __builtin_amdgcn_readlane(i01, 63), t23 = __builtin_amdgcn_readlane(i23, 63);
+        const uint32_t e01 = i01 - s01, e23 = i23 - s23;
+        off[0] = e01 & 0xFFFFu;
+        off[1] = e01 >> 16;
+        off[2] = e23 & 0xFFFFu;
+        off[3] = e23 >> 16;
+        const uint32_t S1 = t01 & 0xFFFFu;
+        S2 = S1 + (t01 >> 16);
+        S3 = S2 + (t23 & 0xFFFFu);
+        const uint32_t Tw = S3 + (t23 >> 16);
+        QSTAMP(3);
+        // the tile's count: wave 0 waits for the four waves' (flag = k + 1 in this copy), publishes
+        // it, and decides whether every wave image fits its buffer (else the back end runs at once)
+        if (lane == 0) {
+            misc[wv] = Tw;
+            __hip_atomic_store(&misc[16 + wv], uint32_t(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (wv == 0) {
+            for (;;) {
+                const u32x4 f = *reinterpret_cast<const volatile u32x4*>(misc + 16);
+                const uint32_t want = uint32_t(k + 1);
+                if (__builtin_amdgcn_readfirstlane((f.x == want) & (f.y == want) & (f.z == want) & (f.w == want))) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            uint32_t A = 0, big = 0;
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
+                A += v;
+                big |= (v + uint32_t(a.rec_bits) + 64u > 32u * kWReg) ? 1u : 0u;
+            }
+            if (lane == 0) {
+                chain_publish_count(a.st, t, chain_pos, a.tag, A);
+                misc[12] = big;
+            }
+        }
+
+        QSTAMP(4);
+        if (k == 0) lds_barrier();  // (the decision below visible; later iterations: back()'s barrier)
+        else if (deferred) back(t_prev, k - 1, false, prc);
+        else lds_barrier();
+        const bool now = __builtin_amdgcn_readfirstlane(misc[12]) != 0u;
+        // the buffer of tile k-1 is free (its stores have read it): tile k+1's pixels into it;
+        // wave 0 resolves the claim of tile k+2
+        if (k >= 1) {
+            const int tn = __builtin_amdgcn_readfirstlane(int(misc0[((k + 1) % 3) * 32 + 13]));
+            if (tn >= 0) issue_pixels(a, tn, (k + 1) & 1);
+        }
+        if (wv == 0) {
+            int t2 = -1;
+            if (claiming) {
+                t2 = claim_resolve(cnt, nch, tpc, seg, &chain, kc);
+                claiming = t2 >= 0;
+            }
+            if (lane == 0) misc0[((k + 2) % 3) * 32 + 13] = uint32_t(t2);
+        }
+
+        // -------------------------------------------------------- emit (whole image, or slot pair 0)
+        const uint32_t reg_bit0 = uint32_t(((k & 1) * 4 + wv) * kWReg) * 32u;
+        const uint32_t Sb[NS] = {0u, S1, S2, S3};
+        const bool whole = Tw + uint32_t(a.rec_bits) + 64u <= 32u * kWReg;
+        {
+            const uint32_t nq = ((whole ? Tw : S2) + 127u) >> 7;  // 16-byte groups
+            uint32_t z;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+            for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(reg + 4 * q) = u32x4{z, z, z, z};
+        }
+        wave_sync();
+        QSTAMP(8);
+#pragma unroll
+        for (int b = 0; b < NS; b++) {
+            if ((b < 2 || whole) && rb[b]) {
+                const uint32_t p = reg_bit0 + Sb[b] + off[b];
+                if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
+                else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
+            }
+        }
+        wave_sync();
+        if (lane == 0 && Tw) misc[4 + wv] = reg[0];  // the wave's first 32 bits
+        QSTAMP(9);
+        if (now) {
+            back(t, k, true, prc);
+            deferred = false;
+        } else {
+            deferred = true;
+        }
+        t_prev = t;
+        klast = k;
+        QSTAMP(10);
+        QRTSTAMP(15);
+    }
+    if (deferred) {  // the last tile's back end (no front stage left to overlap its look-back)
+        if (wv == 0) {
+            const int tp = t_prev;
+            KArgs& a = *ka;
+            int tid = threadIdx.x;
+            asm volatile("" : "+v"(tid));
+            const TileGeo gp = tile_geo<4, 4, TG>(a, tp, tid);
+            if (gp.chain_pos != 0) prc = probe_issue(a.st, tp, gp.chain_pos, gp.step, 0, IE_Q_PROBE);
+        }
+        back(t_prev, klast, false, prc);
+    }
+    leave();
+#undef QSTAMP
+#undef QRTSTAMP
+}
+
 #ifndef IE_ENC_P
 #define IE_ENC_P 1  // 0: 4x4 FAST batch launches run encode4w_kernel (A/B builds)
 #endif
@@ -2657,7 +3216,32 @@ static int encode4p_grid(bool hist, size_t lds) {
     return c;
 }
 
+// Resident workgroups of encode4q_kernel on this device (cached per process): the grid of its
+// static tile order, which must be resident at once.
+static int encode4q_grid() {
+    static int c = 0;
+    if (c) return c;
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4q_kernel, 256, kQLdsBytes);
+    per = std::min(per, IE_Q_PER_CU);
+    c = std::max(1, per) * std::max(1, cus);
+    return c;
+}
+
 void launch_encode4w(const EncArgs& a, hipStream_t s) {
+    // large segmented launches without the histogram may run the pipelined persistent encoder (two
+    // or more tiles per workgroup; a smaller launch has nothing to overlap and keeps one tile per
+    // workgroup; one long chain -- a concatenated stream -- would make its deferred look-backs
+    // walk a whole round of the grid)
+    // (opt-in, IE_PIPELINED=1, read per launch: measured slower than encode4p_kernel)
+    const char* pe = getenv("IE_PIPELINED");
+    const bool pipelined = pe && atoi(pe) != 0;
+    if (IE_ENC_Q && pipelined && !a.ticket && !a.hist && !a.deep_lb && a.segmented && a.ntiles >= 2 * encode4q_grid()) {
+        hipLaunchKernelGGL(encode4q_kernel, dim3(encode4q_grid()), dim3(256), kQLdsBytes, s, a, a.tab);
+        return;
+    }
     if (IE_ENC_P && !a.ticket) {
         const size_t lds = kPLdsBytes + (a.hist ? 1024 * kWHistRep : 0);
         const int grid = IE_P_PERSIST ? std::min(a.ntiles, encode4p_grid(a.hist != nullptr, lds)) : a.ntiles;

@@ -101,6 +101,7 @@ BUDGETS = {
     "_ZN2ie15encode4w_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
     "_ZN2ie15encode4p_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
     "_ZN2ie15encode4p_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 32),
+    "_ZN2ie15encode4q_kernelENS_7EncArgsEPKNS_9EncTablesE": (4, 0),
 }
 # Persistent kernels: the host sizes the grid as (workgroups per CU) x CUs with workgroups per CU
 # = min(occupancy API, PERSIST[name]); every one of them must be resident at once (static tile
@@ -109,6 +110,7 @@ BUDGETS = {
 PERSIST = {
     "_ZN2ie15encode4p_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": 6,
     "_ZN2ie15encode4p_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": 6,
+    "_ZN2ie15encode4q_kernelENS_7EncArgsEPKNS_9EncTablesE": 4,
 }
 
 
@@ -131,7 +133,7 @@ def main(paths):
         # the encoder's bit image is addressed from LDS byte 0 (scatter_bits' inline ds_or): its
         # kernels must allocate no static LDS, so the dynamic area starts there
         for name, size in static_lds(p).items():
-            if ("encode_kernel" in name or "encode4w_kernel" in name or "encode4p_kernel" in name) and size != 0:
+            if ("encode_kernel" in name or "encode4w_kernel" in name or "encode4p_kernel" in name or "encode4q_kernel" in name) and size != 0:
                 rc = 1
                 print(f"{p}: {name} allocates {size} B of static LDS (scatter_bits assumes 0)", file=sys.stderr)
         bad, kernels = scan(p)
