@@ -1877,6 +1877,28 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
 //     parity, so a wave that runs ahead into its next tile never overwrites what a slower wave of
 //     the same workgroup still reads; the tile's two barriers order everything else.
 // =============================================================================================
+// Tile boundary word (encode4p_kernel, encode4q_kernel): the word holding a tile's first bits and
+// its predecessor's last is written by whichever of the two reaches it second, found by ONE 64-bit
+// exchange on the successor's granule 3 (atomics on one address are ordered: exactly one of the
+// two sees the other's half) -- no tile waits for its predecessor's tail.
+static_assert(kGran >= 4, "the boundary exchange uses granule 3");
+// One side of a tile-boundary word: role 1 = the tile ending in it, 2 = the tile starting in it;
+// part = that tile's bits of the word (before the byte swap).  Returns the old granule.
+__device__ __forceinline__ uint64_t boundary_swap(uint64_t* st, int succ, uint32_t tag, uint32_t role, uint32_t part) {
+    const uint64_t v = (uint64_t(tag) << 56) | (uint64_t(role) << 48) | part;
+    return __hip_atomic_exchange(&st[kGran * succ + 3], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Whether this side is the second (then *w = the whole word, byte-swapped for the store).
+__device__ __forceinline__ bool boundary_second(uint64_t old, uint32_t tag, uint32_t role, uint32_t part, uint32_t* w) {
+    *w = bswap32(part | uint32_t(old));
+    return uint32_t(old >> 56) == tag && uint32_t((old >> 48) & 0xFFu) == 3u - role;
+}
+// The second side writes the word.
+__device__ __forceinline__ void boundary_finish(uint32_t* out, uint64_t word, uint64_t old, uint32_t tag, uint32_t role,
+                                                uint32_t part) {
+    if (uint32_t(old >> 56) == tag && uint32_t((old >> 48) & 0xFFu) == 3u - role) out[word] = bswap32(part | uint32_t(old));
+}
+
 constexpr int kPMisc = 64;  // two copies of encode4w_kernel's 32 misc words
 constexpr int kPWfrag = 256;  // the matrix-pipe A fragments [64 lanes][4 words]
 constexpr int kPLdsBytes = (4 * kWReg + 4 * kWTask + kPMisc + kPWfrag) * 4 + kWRows * 8;
@@ -2018,6 +2040,9 @@ __device__ __forceinline__ bool round_half4(const float (&tp)[16], uint32_t (&zp
 #endif
 #ifndef IE_P_LATEPROBE
 #define IE_P_LATEPROBE 0
+#endif
+#ifndef IE_P_XCHG
+#define IE_P_XCHG 0  // 1: (A/B builds) the boundary words by exchange (measured neutral on C2: 90.8 vs 90.0 us)
 #endif
 #ifndef IE_P_CNTBAR
 #define IE_P_CNTBAR 0  // 1: (A/B builds) a workgroup barrier for the tile's count, not wave 0's polling
@@ -2491,10 +2516,10 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                     excl = (IE_P_ABL & 4) ? uint64_t(chain_pos) * 30000u
                                           : lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
                 }
-                const bool have = uint32_t(pr[0].gt >> 56) == a.tag;
+                const bool have = (!IE_P_XCHG || deep) && uint32_t(pr[0].gt >> 56) == a.tag;
                 const bool split = ((start_bit + excl) & 31) != 0;
                 ptail = have ? uint32_t(pr[0].gt) : 0u;
-                pend = (!have && split) ? 1u : 0u;
+                pend = (!have && split) ? 1u : 0u;  // (IE_P_XCHG: the boundary word by exchange)
             }
             if (lane == 0) {
                 if (chain_pos != 0) publish(a.st, t, 1, a.tag, excl + A);
@@ -2572,6 +2597,22 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                 if (wv == 0 && chain_pos == 0)
                     for (uint32_t i = lane; i < uint32_t(start_bit >> 5); i += 64) hc(i, out[i]);
             }
+            const uint64_t E = Xw + Tw;
+            const uint32_t e = uint32_t(E) & 31u;
+            // (IE_P_XCHG) the tile's boundary words by exchange, issued before the stores so that
+            // their round trips overlap them: the first (wave 0, pend) and the last (wave wlast)
+            // (a launch too small to fill the chip -- deep -- keeps the published tails: its tiles end
+            // together, and the exchange's round trip would sit at every one's end)
+            const bool xs = IE_P_XCHG && !deep && wv == 0 && pend;
+            const bool xp = IE_P_XCHG && !deep && wv == wlast && e != 0u && !chain_last;
+            const uint32_t s0 = uint32_t(Xw) & 31u;
+            const uint32_t headS = xs ? (uint32_t(__builtin_amdgcn_readfirstlane(misc[4])) >> s0) : 0u;
+            uint64_t oldS = 0, oldP = 0;
+            if (xs && lane == 0) oldS = boundary_swap(a.st, t, a.tag, 2u, headS);
+            if (xp && whole) {
+                const uint32_t tw = slot_tail32(reg, Tw, prev);  // (= prev after the store)
+                if (lane == 0) oldP = boundary_swap(a.st, t + step, a.tag, 1u, tw << (32u - e));
+            }
             store_pair(0u, whole ? Tw : S2);
             resolve_claim();
             WSTAMP(9);
@@ -2585,8 +2626,7 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                 wave_sync();
                 store_pair(S2, Tw - S2);
             }
-            const uint64_t E = Xw + Tw;
-            const uint32_t e = uint32_t(E) & 31u;
+            if (xp && !whole && lane == 0) oldP = boundary_swap(a.st, t + step, a.tag, 1u, prev << (32u - e));
             const uint32_t nexthead = (e && wv < wlast) ? misc[4 + wv + 1] : 0u;
             // every read of this wave's region is complete (the stores consumed it): the next
             // tile's pixels may land there now
@@ -2599,13 +2639,22 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
                     out[E >> 5] = v;
                     count(E >> 5, v);
                 }
-                if (wv == wlast) publish(a.st, t, 2, a.tag, prev);  // the tile's last 32 bits
-                if (wv == 0 && pend) {  // the first word, with the predecessor's tail
+                if ((!IE_P_XCHG || deep) && wv == wlast) publish(a.st, t, 2, a.tag, prev);  // the tile's last 32 bits
+                if ((!IE_P_XCHG || deep) && wv == 0 && pend) {  // the first word, with the predecessor's tail
                     const uint32_t pt = wait_tail(a.st, t - step, a.tag, a.err);
                     const uint32_t s = uint32_t(Xw) & 31u;
                     const uint32_t v = bswap32((pt << (32u - s)) | (misc[4] >> s));
                     out[Xw >> 5] = v;
                     count(Xw >> 5, v);
+                }
+                uint32_t v;
+                if (xs && boundary_second(oldS, a.tag, 2u, headS, &v)) {
+                    out[Xw >> 5] = v;
+                    count(Xw >> 5, v);
+                }
+                if (xp && boundary_second(oldP, a.tag, 1u, prev << (32u - e), &v)) {
+                    out[E >> 5] = v;
+                    count(E >> 5, v);
                 }
             }
             WSTAMP(10);
@@ -2662,19 +2711,6 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
 #endif
 constexpr int kQMisc = 3 * 32;  // three copies of encode4w_kernel's misc words (tile k: copy k % 3)
 constexpr int kQLdsBytes = (8 * kWReg + 4 * kWTask + kQMisc + kPWfrag) * 4 + kWRows * 8;
-static_assert(kGran >= 4, "encode4q_kernel's boundary exchange uses granule 3");
-
-// One side of a tile-boundary word: role 1 = the tile ending in it, 2 = the tile starting in it;
-// part = that tile's bits of the word (before the byte swap).  Returns the old granule.
-__device__ __forceinline__ uint64_t boundary_swap(uint64_t* st, int succ, uint32_t tag, uint32_t role, uint32_t part) {
-    const uint64_t v = (uint64_t(tag) << 56) | (uint64_t(role) << 48) | part;
-    return __hip_atomic_exchange(&st[kGran * succ + 3], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// The second side writes the word.
-__device__ __forceinline__ void boundary_finish(uint32_t* out, uint64_t word, uint64_t old, uint32_t tag, uint32_t role,
-                                                uint32_t part) {
-    if (uint32_t(old >> 56) == tag && uint32_t((old >> 48) & 0xFFu) == 3u - role) out[word] = bswap32(part | uint32_t(old));
-}
 
 __global__ __launch_bounds__(256, IE_Q_PER_CU) void encode4q_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
     constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;

@@ -23,14 +23,18 @@ ap.add_argument("--frames", type=int, default=16)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--kind", default="U")
-ap.add_argument("--op", default="encode", choices=["encode", "counted"],
-                help="counted: time ie_encode_images_counted (the encoder with the fused byte histogram)")
+ap.add_argument("--op", default="encode", choices=["encode", "counted", "frames"],
+                help="counted: time ie_encode_images_counted (the encoder with the fused byte histogram); "
+                     "frames: ie_encode_frames, one concatenated stream (the C4 shape with --w 1920 --h 1080 "
+                     "--frames 64)")
+ap.add_argument("--w", type=int, default=3840)
+ap.add_argument("--h", type=int, default=2160)
 ap.add_argument("libs", nargs="+")
 args = ap.parse_args()
 
 n = args.n
 q = np.ascontiguousarray(np.asarray(O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n), dtype=np.uint16).ravel())
-w, h, nf = 3840, 2160, args.frames
+w, h, nf = args.w, args.h, args.frames
 y = (synth.uniform_device(w, h, nf, 3, "cuda", torch) if args.kind == "U"
      else torch.from_numpy(synth.frames(args.kind, w, h, nf, seed=3)).cuda())
 stream = torch.cuda.Stream()  # a real stream handle (the default stream's handle is 0 = the ctx's own)
@@ -64,7 +68,17 @@ for path in args.libs:
         L.ie_encode_images_counted.argtypes = [vp, vp, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
                                                C.c_int, vp, C.c_size_t, C.c_uint64]
 
+    if args.op == "frames":
+        L.ie_encode_frames.argtypes = [vp, vp, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                       vp, C.c_size_t, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+
     def run(L=L, hnd=hnd, out=out, pitch=pitch, eb=eb, sizes=False):
+        if args.op == "frames":  # (eb[0] = the stream's end bit; compared over the whole stream)
+            r = L.ie_encode_frames(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, nf, 1, 0, C.c_void_p(out.data_ptr()),
+                                   pitch * nf, 165, None, eb.ctypes.data_as(C.POINTER(C.c_uint64)))
+            if r != 0:
+                raise RuntimeError(L.ie_last_error(hnd))
+            return
         if args.op == "counted" and not sizes:
             r = L.ie_encode_images_counted(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, nf, 1, 0,
                                            C.c_void_p(out.data_ptr()), pitch, 165)
@@ -88,7 +102,10 @@ for path in args.libs:
 ref = variants[0]
 for v in variants:
     ok = np.array_equal(v["eb"], ref["eb"])
-    if ok:
+    if ok and args.op == "frames":
+        nb = (int(v["eb"][0]) + 7) // 8
+        ok = torch.equal(v["out"][:nb], ref["out"][:nb])
+    elif ok:
         for f in range(nf):
             nb = (int(v["eb"][f]) + 7) // 8
             a = v["out"][f * v["pitch"]: f * v["pitch"] + nb]
