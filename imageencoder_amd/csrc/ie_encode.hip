@@ -2032,6 +2032,9 @@ __device__ __forceinline__ bool round_half4(const float (&tp)[16], uint32_t (&zp
 #ifndef IE_P_WAVES
 #define IE_P_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD)
 #endif
+#ifndef IE_P_WAVES_HIST
+#define IE_P_WAVES_HIST 6  // the counting instantiation (5: 89 VGPRs; measured 124.7 against 119.4 us)
+#endif
 #ifndef IE_P_MFMA
 #define IE_P_MFMA 1  // 0: (A/B builds) the transform on the VALU as in encode4w_kernel
 #endif
@@ -2052,7 +2055,7 @@ __device__ __forceinline__ bool round_half4(const float (&tp)[16], uint32_t (&zp
 #endif
 
 template <bool HIST>
-__global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
+__global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void encode4p_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
     constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
     constexpr int GW = 16 * NS, BW = 64 * NS, TG = 4 * GW;  // groups / blocks per wave, groups per tile
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -2672,8 +2675,13 @@ __global__ __launch_bounds__(256, IE_P_WAVES) void encode4p_kernel(EncArgs a_, c
 #pragma unroll
             for (int r = 0; r < HR; r++) c += hl[tid * HR + r];
             if (c) atomicAdd(&a.hist[size_t(frame) * 256 + tid], c);
+            if (more) {  // (the next tile adds after two barriers; a zero vector held across the tile
+                         // loop was spilled: 16 B per lane stored per tile, ~30 MB per C5 launch)
+                uint32_t z;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
 #pragma unroll
-            for (int r = 0; r < HR; r++) hl[tid * HR + r] = 0u;  // (the next tile adds after two barriers)
+                for (int r = 0; r < HR; r++) hl[tid * HR + r] = z;
+            }
         }
         if (!more) break;
         t = t_next;

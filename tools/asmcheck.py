@@ -100,7 +100,7 @@ BUDGETS = {
     "_ZN2ie15encode4w_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
     "_ZN2ie15encode4w_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
     "_ZN2ie15encode4p_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
-    "_ZN2ie15encode4p_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 32),
+    "_ZN2ie15encode4p_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
     "_ZN2ie15encode4q_kernelENS_7EncArgsEPKNS_9EncTablesE": (4, 0),
 }
 # Persistent kernels: the host sizes the grid as (workgroups per CU) x CUs with workgroups per CU

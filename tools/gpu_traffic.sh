@@ -3,7 +3,7 @@
 # four workloads' bench runs -> gpurun_out/traffic/<ROUND>_traffic_<wl>.json + *_kernel_stats.csv.
 # Each GPU step has its own limit; a failing step ends the script.
 R=${GRAFT_REPO_ROOT:-/root/repo}
-ROUND=${ROUND:-r04}
+ROUND=${ROUND:-r05}
 O=$R/gpurun_out/traffic; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 BOPT="--steps 6 --warmup 1 --no-cpu --no-single-frame --no-e2e --no-decode --no-gop --no-check"
