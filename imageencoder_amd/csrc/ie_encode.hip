@@ -1334,6 +1334,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     return v;
 }
 
+#ifndef IE_STORE2
+#define IE_STORE2 1  // 0: (A/B builds) the quad loop reads each word by itself (4-way LDS bank conflicts)
+#endif
 // One slot image I (bit 0 at absolute stream bit X) to the output words, by one wave: words
 // [r0, nw) counted from floor(X / 32), word r = alignbit(I[r - 1], I[r], X % 32) with I[-1] =
 // prev (the 32 bits before X); the partial word nw is left to whoever writes the next bits.
@@ -1347,13 +1350,41 @@ __device__ __forceinline__ void store_slot(uint32_t* __restrict__ out, const uin
         const uint32_t am = I[max(r, 1u) - 1u];
         return bswap32(__builtin_amdgcn_alignbit(r ? am : prev, I[r], s));
     };
-    const uint32_t hd = min(nw - r0, uint32_t((4u - uint32_t((w0 + r0) & 3u)) & 3u));
+    uint32_t hd = min(nw - r0, uint32_t((4u - uint32_t((w0 + r0) & 3u)) & 3u));
+    if (IE_STORE2 && r0 + hd == 0u) hd = min(nw, 4u);  // (the quad loop needs I[r - 1]: word -1 is prev)
     if (uint32_t(lane) < hd) {
         const uint32_t v = word(r0 + lane);
         out[w0 + r0 + lane] = v;
         cnt(w0 + r0 + lane, v);
     }
     const uint32_t rq = r0 + hd, nq = (nw - rq) >> 2;
+    if (IE_STORE2) {
+        // output quad q = words rq + 4q .. +3 (16-byte aligned in out) needs I[rq + 4q - 1 ..
+        // rq + 4q + 3]: five words at offset d of the two 16-byte LDS quads from (rq - 1) / 4 + q,
+        // read whole (consecutive lanes, consecutive quads: no bank conflicts), d wave-uniform
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const uint32_t d = (rq - 1u) & 3u;
+        const v4u* I4 = reinterpret_cast<const v4u*>(I) + ((rq - 1u) >> 2);
+        uint32_t* const ob = out + (w0 + rq);
+        auto quads = [&](auto dc) {
+            constexpr uint32_t D = decltype(dc)::value;
+            for (uint32_t q = lane; q < nq; q += 64) {
+                const v4u A = I4[q], B = I4[q + 1];
+                const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+                const v4u v = {bswap32(__builtin_amdgcn_alignbit(W[D], W[D + 1], s)), bswap32(__builtin_amdgcn_alignbit(W[D + 1], W[D + 2], s)),
+                               bswap32(__builtin_amdgcn_alignbit(W[D + 2], W[D + 3], s)), bswap32(__builtin_amdgcn_alignbit(W[D + 3], W[D + 4], s))};
+                __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(ob + 4u * q));
+                cnt(w0 + rq + 4u * q, v.x);
+                cnt(w0 + rq + 4u * q + 1u, v.y);
+                cnt(w0 + rq + 4u * q + 2u, v.z);
+                cnt(w0 + rq + 4u * q + 3u, v.w);
+            }
+        };
+        if (d == 0u) quads(std::integral_constant<uint32_t, 0>{});
+        else if (d == 1u) quads(std::integral_constant<uint32_t, 1>{});
+        else if (d == 2u) quads(std::integral_constant<uint32_t, 2>{});
+        else quads(std::integral_constant<uint32_t, 3>{});
+    } else
     for (uint32_t q = lane; q < nq; q += 64) {
         const uint32_t r = rq + 4u * q;
         const uint32_t am = I[max(r, 1u) - 1u];
