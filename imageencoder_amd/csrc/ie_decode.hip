@@ -151,16 +151,31 @@ __device__ __forceinline__ uint64_t huf_wg_prefix(const uint32_t* wgsum, int g, 
     return s64[0] + s64[1] + s64[2] + s64[3];
 }
 
+// The emitting walk: every chunk again from its entry, its symbols into LDS at the chunk's place
+// in the workgroup's output, then the workgroup's output copied out whole (consecutive lanes,
+// consecutive bytes) -- a lane writing its own chunk's bytes straight to memory touches 64 lines
+// per store instruction.  A workgroup whose output exceeds the buffer writes from the walk.
+#ifndef IE_HUF_EMIT_LDS
+#define IE_HUF_EMIT_LDS 40960
+#endif
 __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
     __shared__ uint16_t l1[1 << kHufL1];
     __shared__ alignas(8) uint32_t scratch[8];
+    __shared__ uint8_t sym[IE_HUF_EMIT_LDS > 0 ? IE_HUF_EMIT_LDS : 1];
     huf_l1(a.lut, l1);
     const uint64_t pre = huf_wg_prefix(a.wgsum, int(blockIdx.x), scratch);
+    const uint32_t tot = a.wgsum[blockIdx.x];
+    const bool staged = IE_HUF_EMIT_LDS > 0 && tot <= uint32_t(IE_HUF_EMIT_LDS);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= a.nchunks) return;
-    const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
-    uint32_t c;
-    huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, a.out + pre + a.base[k], true);
+    if (k < a.nchunks) {
+        const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
+        uint32_t c;
+        if (staged) huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, sym + a.base[k], true);
+        else huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, a.out + pre + a.base[k], true);
+    }
+    if (!staged) return;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += kTPB) a.out[pre + i] = sym[i];
 }
 
 // total receives the symbol count (device, 1 word): the sum of the walk's workgroup totals.
