@@ -2391,7 +2391,11 @@ int finish_decode(ie_ctx* c, uint8_t* out, const uint8_t* dpix, bool out_dev, in
 // parse buffers it needs: fills a's chunking fields and scratch pointers, *levels = composition
 // levels.  The record stream's own fields (words, nbits, start_bit, dstart, total, end_out) are
 // the caller's.
-int plan_records(ie_ctx* c, uint64_t span, uint64_t nblocks, ie::RecParseArgs& a, size_t* spec_at_out, int* levels_out) {
+#ifndef IE_GOP_CAPC
+#define IE_GOP_CAPC 1  // 0: (A/B builds) gop decode chunks sized by the I-frame bound alone
+#endif
+int plan_records(ie_ctx* c, uint64_t span, uint64_t nblocks, ie::RecParseArgs& a, size_t* spec_at_out, int* levels_out,
+                 uint64_t cmax = uint64_t(1) << 15) {
     const int n = c->n;
     int r;
     // chunking: about R records per chunk (IE_DEC_R; default 24 for 4x4, 28 for 8x8: measured
@@ -2407,7 +2411,7 @@ int plan_records(ie_ctx* c, uint64_t span, uint64_t nblocks, ie::RecParseArgs& a
     const uint64_t recs = rs ? std::max<uint64_t>(1, strtoull(rs, nullptr, 10)) : (n == 4 ? 24 : 28);
     const uint64_t want = std::max<uint64_t>((nblocks + recs - 1) / recs, 1);
     uint64_t C = (span + want - 1) / want;
-    C = std::min<uint64_t>(std::max<uint64_t>((C + 31) / 32 * 32, 256), uint64_t(1) << 15);
+    C = std::min<uint64_t>(std::max<uint64_t>((C + 31) / 32 * 32, 256), std::max<uint64_t>(cmax / 32 * 32, 256));
     const uint64_t nch = std::max<uint64_t>((span + C - 1) / C, 1);
     // levels: ceil(n / G) composites per level until at most G remain (G^4 chunks at most)
     size_t tab_rows = 0;
@@ -2685,7 +2689,12 @@ int ie_decode_gop(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_bit, 
     // scratch do not depend on where a frame ends
     ie::RecParseArgs pa{};
     int levels = 0;
-    if ((r = plan_records(c, rec_bound, nblocks, pa, nullptr, &levels))) return r;
+    // (gop > 1: the plan is sized by the I-frame bound, but a P-frame's records are a few bits each
+    // -- at most kRecPosCap records per chunk (5 bits each at least with RLE: 4 header bits and
+    // one value bit) keeps its chunks on the listed-positions decode instead of the re-walk)
+    const uint64_t min_rec = use_rle ? 5u : uint64_t(4 + n * n);
+    const uint64_t cmax = (gop > 1 && IE_GOP_CAPC) ? uint64_t(ie::kRecPosCap) * min_rec : (uint64_t(1) << 15);
+    if ((r = plan_records(c, rec_bound, nblocks, pa, nullptr, &levels, cmax))) return r;
     pa.words = reinterpret_cast<const uint32_t*>(c->d_in);
     pa.nbits = nbits;
     pa.rle = use_rle ? 1 : 0;

@@ -36,6 +36,23 @@ for gop in (1, F):
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / k
     res[gop] = (t, int(end), [int(v) for v in fb])
+# decode (ie_decode_gop, device-resident stream and frames) of both streams
+dec_t = {}
+dout = torch.zeros(F * h * w, dtype=torch.uint8, device="cuda")
+for gop in ((1, F) if w % 16 == 0 and h % 16 == 0 else ()):  # (P-frames decode at multiples of 16 only)
+    _, end = c.encode_gop(dy, w, h, out, gop, mer, nframes=F)
+    nb = (int(end) + 7) // 8
+    c.decode_gop(out, w, h, dout, gop, mer, nframes=F, length=nb)  # warm-up
+    torch.cuda.synchronize()
+    k = 10
+    t0 = time.perf_counter()
+    for _ in range(k):
+        c.decode_gop(out, w, h, dout, gop, mer, nframes=F, length=nb)
+    torch.cuda.synchronize()
+    dec_t[gop] = (time.perf_counter() - t0) / k
+if dec_t:
+    print(f"decode_gop {w}x{h} x{F}: gop=1 {dec_t[1] * 1e3:.3f} ms ({dec_t[1] / F * 1e6:.1f} us/frame), "
+          f"gop={F} {dec_t[F] * 1e3:.3f} ms ({dec_t[F] / F * 1e6:.1f} us/frame)")
 # the stream zeroing is part of each timed call above; time it alone to subtract it
 torch.cuda.synchronize()
 t0 = time.perf_counter()
