@@ -52,8 +52,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ROUND = "r05"  # profiles/<ROUND>_traffic_<workload>.json: this round's counter passes (tools/gpu_traffic.sh)
 # the dominant kernel of each workload's timed launch (launch_encode: 4x4 FAST over whole 16-byte
 # groups runs encode4p_kernel; 8x8 runs encode_kernel<8>)
-KERNEL = {"c2": "encode4p_kernel<false>", "c3": "encode_kernel<8,false>", "c4": "encode4p_kernel<false>",
-          "c5": "encode4p_kernel<true>"}
+KERNEL = {"c2": "encode4p_kernel<false, 4>", "c3": "encode_kernel<8,false>", "c4": "encode4p_kernel<false, 4>",
+          "c5": "encode4p_kernel<true, 4>"}
 
 WORKLOADS = {
     "c2": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=False,

@@ -648,7 +648,7 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     a.chain_end = L.chain_end ? L.chain_end : c->d_chain_end;
     a.err = c->d_err;
     a.wave_fix = c->d_wave_fix;
-    c->last_fix_words = (L.mode == IE_MODE_EXACT) ? 0 : g.ntiles * (ie::encode_threads_per_tile() / 64);
+    c->last_fix_words = 0;  // (set after the launch: its kernel's waves per tile)
     if (L.hist) HIPCHK(c, hipMemsetAsync(L.hist, 0, size_t(L.nframes) * 256 * sizeof(uint32_t), c->stream));
     uint64_t* d_stamps = nullptr;
     if (stamp_file) {
@@ -657,7 +657,8 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     }
     a.stamps = d_stamps;
     a.deep_lb = small ? 1 : 0;
-    ie::launch_encode(a, c->n, L.mode == IE_MODE_EXACT, c->stream, bpt);
+    const int fix_per_tile = ie::launch_encode(a, c->n, L.mode == IE_MODE_EXACT, c->stream, bpt);
+    c->last_fix_words = (L.mode == IE_MODE_EXACT) ? 0 : g.ntiles * fix_per_tile;
     HIPCHK(c, hipGetLastError());
     if (d_stamps) {
         std::vector<uint64_t> hs(size_t(g.ntiles) * ie::kStamps);

@@ -122,7 +122,8 @@ constexpr int kStamps = 64;  // encode_kernel: [0, 16) by thread 0; encode4w_ker
 // chain-state words per tile (the host allocates; ie_common.hpp kGran must not exceed it)
 constexpr int kStateWordsPerTile = 16;
 // bpt: blocks per thread, encode_blocks_per_thread(n, ntiles at the default) for the launch
-void launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s, int bpt);
+// returns the FP64-statistics words per tile the launched kernel writes (EncArgs::wave_fix)
+int launch_encode(const EncArgs& a, int n, bool exact, hipStream_t s, int bpt);
 int encode_blocks_per_thread(int n);  // the batch default (4x4: 4, 8x8: 1)
 int encode_small_tiles();             // a launch of fewer tiles does not fill the chip (deep look-back)
 void launch_word_scatter(const uint32_t* src, uint32_t* dst, uint64_t pitch_words, int n, hipStream_t s);  // horizontally adjacent blocks per lane (Geo<N>::BPT)

@@ -1418,12 +1418,12 @@ __device__ __forceinline__ uint32_t slot_tail32(const uint32_t* I, uint32_t n, u
 // boundaries, [tile][wave][12] (tools/stamps_w.py)
 #define WSTAMP(i)                                                                                                   \
     do {                                                                                                            \
-        if (IE_PROFILE && a.stamps && lane == 0) a.stamps[size_t(t) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (IE_PROFILE && a.stamps && lane == 0 && wv < 4) a.stamps[size_t(t) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 // the chip-wide 100 MHz clock (comparable across CUs and XCDs) at the wave's start (14) and end (15)
 #define WRTSTAMP(i)                                                                                                 \
     do {                                                                                                            \
-        if (IE_PROFILE && a.stamps && lane == 0) a.stamps[size_t(t) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (IE_PROFILE && a.stamps && lane == 0 && wv < 4) a.stamps[size_t(t) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
 // HIST (ie_encode_images_counted): every stored byte also counted into a per-tile LDS histogram
@@ -1932,6 +1932,19 @@ __device__ __forceinline__ void boundary_finish(uint32_t* out, uint64_t word, ui
 
 constexpr int kPMisc = 64;  // two copies of encode4w_kernel's 32 misc words
 constexpr int kPWfrag = 256;  // the matrix-pipe A fragments [64 lanes][4 words]
+// encode4p_kernel's misc words per copy by waves per tile: [0, WPT) wave bit counts, H the waves'
+// head words, E the tile's exclusive prefix (2), PT the tail before the chain start, PD the pending
+// first word, C12 / CL the claim words, F the count flags, D the deep look-back sums (2 per wave),
+// FD their found flags; S the copy's size (4 waves: encode4w_kernel's layout)
+template <int WPT> struct PMisc {
+    static constexpr int H = WPT, E = 2 * WPT, PT = 2 * WPT + 2, PD = 2 * WPT + 3, C12 = 2 * WPT + 4,
+                         CL = 2 * WPT + 5, F = 4 * WPT, D = 4 * WPT + WPT + 2 - (WPT == 4 ? 4 : 0),
+                         FD = D + 2 * WPT, S = WPT == 4 ? 32 : 96;
+    static_assert(FD + WPT <= S && F % 4 == 0 && CL < F, "misc layout");
+};
+template <int WPT> constexpr int p_lds_bytes() {
+    return (WPT * 4 * 64 * (16 / WPT) + WPT * kWTask + 2 * PMisc<WPT>::S + kPWfrag) * 4 + kWRows * 8;
+}
 constexpr int kPLdsBytes = (4 * kWReg + 4 * kWTask + kPMisc + kPWfrag) * 4 + kWRows * 8;
 
 typedef int v4i32 __attribute__((ext_vector_type(4)));
@@ -2085,18 +2098,24 @@ __device__ __forceinline__ bool round_half4(const float (&tp)[16], uint32_t (&zp
 #define IE_P_PERSIST 0  // 1: (A/B builds) the persistent grid with per-chain tile claims
 #endif
 
-template <bool HIST>
-__global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void encode4p_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
-    constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
-    constexpr int GW = 16 * NS, BW = 64 * NS, TG = 4 * GW;  // groups / blocks per wave, groups per tile
+// WPT: waves per tile -- 4 (four slots of 64 blocks per lane), or 8 for launches too small to fill
+// the chip (two slots per lane: twice the waves per tile, half the work per wave; the tile, its
+// chain element and its stream layout are the same)
+template <bool HIST, int WPT>
+__global__ __launch_bounds__(64 * WPT, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void encode4p_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
+    static_assert(WPT == 4 || (WPT == 8 && !HIST), "4 waves per tile, or 8 without the histogram");
+    constexpr int N = 4, NN = 16, NP = 8, TPB = 64 * WPT, NS = 16 / WPT, PS = NS / 2;  // PS: slots per pair
+    constexpr int GW = 16 * NS, BW = 64 * NS, TG = WPT * GW;  // groups / blocks per wave, groups per tile
+    constexpr int RW = 4 * BW;  // words per wave region
+    using ML = PMisc<WPT>;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int tid = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint32_t* const reg = smem + wv * kWReg;  // this wave's pixels, later its two slot images
-    uint32_t* const task = smem + 4 * kWReg + wv * kWTask;
+    uint32_t* const reg = smem + wv * RW;  // this wave's pixels, later its slot images
+    uint32_t* const task = smem + WPT * RW + wv * kWTask;
     uint32_t* const res = task + 64;
-    uint32_t* const misc0 = smem + 4 * kWReg + 4 * kWTask;  // [2][32]
-    uint32_t* const wl = misc0 + kPMisc;  // [64][4]: the matrix-pipe A fragment of every lane
+    uint32_t* const misc0 = smem + WPT * RW + WPT * kWTask;  // [2][ML::S]
+    uint32_t* const wl = misc0 + 2 * ML::S;  // [64][4]: the matrix-pipe A fragment of every lane
     uint32_t* const hl = wl + kPWfrag;    // HIST: the tile's byte histogram
     constexpr int HR = kWHistRep, HWORDS = 256 * HR;
     double* const srow = reinterpret_cast<double*>(hl + (HIST ? HWORDS : 0));
@@ -2121,10 +2140,10 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
             unsigned k = 0;
             if ((tid & 63) == 0) k = atomicAdd(&cnt[kClaimStride * chain], 1u);
             const int tt = claim_resolve(cnt, nch, tpc, seg, &chain, k);
-            if (tid == 0) misc0[12] = uint32_t(tt);
+            if (tid == 0) misc0[ML::C12] = uint32_t(tt);
         }
         lds_barrier();
-        t = __builtin_amdgcn_readfirstlane(int(misc0[12]));
+        t = __builtin_amdgcn_readfirstlane(int(misc0[ML::C12]));
     }
     // (every workgroup of a claiming grid counts its exit; the last one leaves the counters zero)
     auto leave = [&]() {
@@ -2142,7 +2161,9 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
     // each wave's pixel rows of tile tt into its own region (row r of the wave's block j at
     // reg[r BW + j]: a lane's 16 bytes are its group's row)
     auto issue_pixels = [&](KArgs& a, int tt) {
-        const TileGeo gg = tile_geo<4, 4, TG>(a, tt, tid);
+        const int l0 = tid & 63;
+        if (l0 >= GW) return;  // (8 waves per tile: a wave's 32 groups, one per lane)
+        const TileGeo gg = tile_geo<4, 4, TG>(a, tt, GW * wv + l0);
         if (gg.nblk) {
             const uint8_t* base = a.y + size_t(gg.frame) * a.frame_pitch + size_t(gg.byi) * N * a.stride + size_t(gg.bx0) * N;
 #pragma unroll
@@ -2168,8 +2189,8 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
     if constexpr (HIST)
         for (int i = tid; i < HWORDS; i += TPB) hl[i] = 0u;
     if ((tid & 63) == 0) {  // the waves' count flags of both misc copies
-        misc0[16 + wv] = 0u;
-        misc0[32 + 16 + wv] = 0u;
+        misc0[ML::F + wv] = 0u;
+        misc0[ML::S + ML::F + wv] = 0u;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA above and the first tile's pixels)
     const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
@@ -2184,7 +2205,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const int lane = tid & 63;
-        uint32_t* const misc = misc0 + (iter & 1) * 32;
+        uint32_t* const misc = misc0 + (iter & 1) * ML::S;
         const TileGeo g = tile_geo<4, 4, TG>(a, t, tid);
         const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
         const int ng = min(TG, a.groups_per_frame - tif * TG);
@@ -2193,7 +2214,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
         WSTAMP(0);
         WRTSTAMP(14);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
-        if (wv == 0 && lane == 0) misc[13] = 0u;  // the next tile's claim: not yet made (read after barrier 2)
+        if (wv == 0 && lane == 0) misc[ML::CL] = 0u;  // the next tile's claim: not yet made (read after barrier 2)
         WSTAMP(1);
         asm volatile("; PHASE p1" ::: "memory");
 
@@ -2399,20 +2420,23 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
             for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
             __builtin_amdgcn_sched_barrier(0);
         }
-        const uint32_t s01 = rb[0] | (rb[1] << 16), s23 = rb[2] | (rb[3] << 16);
-        const uint32_t i01 = wave_incl_scan_dpp(s01), i23 = wave_incl_scan_dpp(s23);
-        const uint32_t t01 = __builtin_amdgcn_readlane(i01, 63), t23 = __builtin_amdgcn_readlane(i23, 63);
-        const uint32_t e01 = i01 - s01, e23 = i23 - s23;
         uint32_t T[NS], off[NS];
-        T[0] = t01 & 0xFFFFu;
-        T[1] = t01 >> 16;
-        T[2] = t23 & 0xFFFFu;
-        T[3] = t23 >> 16;
-        off[0] = e01 & 0xFFFFu;
-        off[1] = e01 >> 16;
-        off[2] = e23 & 0xFFFFu;
-        off[3] = e23 >> 16;
-        const uint32_t S1 = T[0], S2 = S1 + T[1], S3 = S2 + T[2], Tw = S3 + T[3];
+#pragma unroll
+        for (int h = 0; h < NS / 2; h++) {  // two slots per 32-bit scan (16-bit halves)
+            const uint32_t sv = rb[2 * h] | (rb[2 * h + 1] << 16);
+            const uint32_t iv = wave_incl_scan_dpp(sv);
+            const uint32_t tv = __builtin_amdgcn_readlane(iv, 63), ev = iv - sv;
+            T[2 * h] = tv & 0xFFFFu;
+            T[2 * h + 1] = tv >> 16;
+            off[2 * h] = ev & 0xFFFFu;
+            off[2 * h + 1] = ev >> 16;
+        }
+        uint32_t Sb[NS];  // slot starts in the wave image
+        Sb[0] = 0u;
+#pragma unroll
+        for (int b = 1; b < NS; b++) Sb[b] = Sb[b - 1] + T[b - 1];
+        const uint32_t Tw = Sb[NS - 1] + T[NS - 1];
+        const uint32_t S2 = NS == 4 ? Sb[2] : Sb[1];  // the end of slot pair 0 (8 waves: slot 0)
         // The tile's bit count: wave 0 alone waits for the four waves' counts (their flags in
         // misc[16..19], cleared before the tile) and publishes it; the other waves go on to their
         // emission and learn their place in the tile after the position barrier.  (A launch too
@@ -2420,7 +2444,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
         // waves read predecessor windows.)
         if (lane == 0) {
             misc[wv] = Tw;
-            __hip_atomic_store(&misc[16 + wv], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&misc[ML::F + wv], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         WSTAMP(4);
         asm volatile("; PHASE p4" ::: "memory");
@@ -2428,8 +2452,13 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
             lds_barrier();
         } else if (wv == 0) {
             for (;;) {
-                const u32x4 f = *reinterpret_cast<const volatile u32x4*>(misc + 16);
-                if (__builtin_amdgcn_readfirstlane(f.x & f.y & f.z & f.w)) break;
+                uint32_t all = 1u;
+#pragma unroll
+                for (int q = 0; q < WPT / 4; q++) {
+                    const u32x4 f = *reinterpret_cast<const volatile u32x4*>(misc + ML::F + 4 * q);
+                    all &= f.x & f.y & f.z & f.w;
+                }
+                if (__builtin_amdgcn_readfirstlane(all)) break;
                 __builtin_amdgcn_s_sleep(1);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -2439,7 +2468,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
 
         uint32_t A = 0;  // (wave 0, or every wave in deep mode; the others after the position barrier)
 #pragma unroll
-        for (int w = 0; w < 4; w++) A += __builtin_amdgcn_readfirstlane(misc[w]);
+        for (int w = 0; w < WPT; w++) A += __builtin_amdgcn_readfirstlane(misc[w]);
         if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);
         constexpr int DW = 2;
         Probe pr[DW];
@@ -2454,8 +2483,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
             }
         }
 
-        const uint32_t reg_bit0 = uint32_t(wv * kWReg) * 32u;
-        const uint32_t Sb[NS] = {0u, S1, S2, S3};
+        const uint32_t reg_bit0 = uint32_t(wv * RW) * 32u;
         auto zero_img = [&](uint32_t bits) {
             const uint32_t nq = (bits + 127u) >> 7;  // 16-byte groups
             uint32_t z;
@@ -2466,29 +2494,29 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
         // most rec_bits past its start, plus the 64-bit window): all four slots are emitted before
         // the position barrier -- beside wave 0's look-back -- and stored in one pass after it.
         // Otherwise slot pairs in turn (pair 1 after pair 0 is stored).
-        const bool whole = Tw + uint32_t(a.rec_bits) + 64u <= 32u * kWReg;
+        const bool whole = Tw + uint32_t(a.rec_bits) + 64u <= 32u * RW;
         auto emit_slot = [&](int b) {  // slot b at its place in the (whole or pair) image
             if (!(IE_P_ABL & 2) && rb[b]) {
-                const uint32_t p = reg_bit0 + (whole ? Sb[b] : Sb[b] - Sb[b & 2]) + off[b];
+                const uint32_t p = reg_bit0 + (whole ? Sb[b] : Sb[b] - Sb[(b / PS) * PS]) + off[b];
                 if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
                 else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
             }
         };
         zero_img(whole ? Tw : S2);
         wave_sync();
-        emit_slot(0);
-        emit_slot(1);
+#pragma unroll
+        for (int b = 0; b < PS; b++) emit_slot(b);
         // (A/B builds) the first probe issued half-way through the emission: predecessors that
         // started just before this tile have had that much longer to publish their counts
         if (IE_P_LATEPROBE && !deep && wv == 0 && chain_pos != 0) pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
         if (whole) {
-            emit_slot(2);
-            emit_slot(3);
+#pragma unroll
+            for (int b = PS; b < NS; b++) emit_slot(b);
         }
         wave_sync();
         WSTAMP(6);
         asm volatile("; PHASE p6" ::: "memory");
-        if (lane == 0 && Tw) misc[4 + wv] = reg[0];  // the wave's first 32 bits
+        if (lane == 0 && Tw) misc[ML::H + wv] = reg[0];  // the wave's first 32 bits
 
         // -------------------------------------------------------- look-back (wave 0)
         const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
@@ -2520,9 +2548,9 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
                 for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
             }
             if (lane == 0) {
-                misc[18 + 2 * wv] = uint32_t(sm);
-                misc[19 + 2 * wv] = uint32_t(sm >> 32);
-                misc[26 + wv] = found ? 1u : 0u;
+                misc[ML::D + 2 * wv] = uint32_t(sm);
+                misc[ML::D + 2 * wv + 1] = uint32_t(sm >> 32);
+                misc[ML::FD + wv] = found ? 1u : 0u;
             }
             lds_barrier();
         }
@@ -2536,11 +2564,11 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
                 bool done = false;
                 if (deep) {
 #pragma unroll
-                    for (int w = 0; w < 4; w++) {
+                    for (int w = 0; w < WPT; w++) {
                         if (!done) {
-                            excl += uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[18 + 2 * w]))) |
-                                    (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[19 + 2 * w]))) << 32);
-                            done = __builtin_amdgcn_readfirstlane(misc[26 + w]) != 0;
+                            excl += uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::D + 2 * w]))) |
+                                    (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::D + 2 * w + 1]))) << 32);
+                            done = __builtin_amdgcn_readfirstlane(misc[ML::FD + w]) != 0;
                         }
                     }
                     if (!done) excl = 0;
@@ -2557,10 +2585,10 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
             }
             if (lane == 0) {
                 if (chain_pos != 0) publish(a.st, t, 1, a.tag, excl + A);
-                misc[8] = uint32_t(excl);
-                misc[9] = uint32_t(excl >> 32);
-                misc[10] = ptail;
-                misc[11] = pend;
+                misc[ML::E] = uint32_t(excl);
+                misc[ML::E + 1] = uint32_t(excl >> 32);
+                misc[ML::PT] = ptail;
+                misc[ML::PD] = pend;
                 const uint64_t P = start_bit + excl;
                 if (tif == 0) a.frame_start[frame] = P;
                 if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
@@ -2574,13 +2602,13 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
         uint32_t W = 0;
         A = 0;
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
+        for (int w = 0; w < WPT; w++) {
             const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
             A += v;
             W += (w < wv) ? v : 0u;
         }
         // every wave is past the previous tile: its count flags (the other copy) are free again
-        if (lane == 0) misc0[((iter + 1) & 1) * 32 + 16 + wv] = 0u;
+        if (lane == 0) misc0[((iter + 1) & 1) * ML::S + ML::F + wv] = 0u;
 
         // -------------------------------------------------------- store, slot pair by slot pair
         // The next tile is claimed only now (wave 0: the atomic here, resolved after its first
@@ -2593,7 +2621,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
         auto resolve_claim = [&]() {
             if (!claimed) {
                 const int tn = claim_resolve(cnt, nch, tpc, seg, &chain, kclaim);
-                if (lane == 0) misc[13] = 0x80000000u | uint32_t(tn);
+                if (lane == 0) misc[ML::CL] = 0x80000000u | uint32_t(tn);
                 claimed = true;
             }
         };
@@ -2601,7 +2629,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
             if (!dyn) return a.ntiles;
             uint32_t v;
             for (;;) {  // (wave 0 sets it right after its first store: a short wait at most)
-                v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&misc[13], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&misc[ML::CL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
                 if (v & 0x80000000u) break;
                 __builtin_amdgcn_s_sleep(1);
             }
@@ -2609,12 +2637,12 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
         };
         int t_next = -1;
         if (Tw) {
-            const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[8]))) |
-                                  (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[9]))) << 32);
+            const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::E]))) |
+                                  (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::E + 1]))) << 32);
             const uint64_t Xw = start_bit + excl + W;
-            const bool pend = __builtin_amdgcn_readfirstlane(misc[11]) != 0u;
+            const bool pend = __builtin_amdgcn_readfirstlane(misc[ML::PD]) != 0u;
             const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
-            uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[10]) : 0u;
+            uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[ML::PT]) : 0u;
             const HistCountT<HR> hc{hl, chain_last ? (start_bit + excl + A + 7) / 8 : ~0ull, uint32_t(lane % HR)};
             auto count = [&](uint64_t gw, uint32_t v) {
                 if constexpr (HIST) hc(gw, v);
@@ -2640,7 +2668,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
             const bool xs = IE_P_XCHG && !deep && wv == 0 && pend;
             const bool xp = IE_P_XCHG && !deep && wv == wlast && e != 0u && !chain_last;
             const uint32_t s0 = uint32_t(Xw) & 31u;
-            const uint32_t headS = xs ? (uint32_t(__builtin_amdgcn_readfirstlane(misc[4])) >> s0) : 0u;
+            const uint32_t headS = xs ? (uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::H])) >> s0) : 0u;
             uint64_t oldS = 0, oldP = 0;
             if (xs && lane == 0) oldS = boundary_swap(a.st, t, a.tag, 2u, headS);
             if (xp && whole) {
@@ -2655,13 +2683,13 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
                 wave_sync();  // pair 0's image has been read
                 zero_img(Tw - S2);
                 wave_sync();
-                emit_slot(2);
-                emit_slot(3);
+#pragma unroll
+                for (int b = PS; b < NS; b++) emit_slot(b);
                 wave_sync();
                 store_pair(S2, Tw - S2);
             }
             if (xp && !whole && lane == 0) oldP = boundary_swap(a.st, t + step, a.tag, 1u, prev << (32u - e));
-            const uint32_t nexthead = (e && wv < wlast) ? misc[4 + wv + 1] : 0u;
+            const uint32_t nexthead = (e && wv < wlast) ? misc[ML::H + wv + 1] : 0u;
             // every read of this wave's region is complete (the stores consumed it): the next
             // tile's pixels may land there now
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2677,7 +2705,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
                 if ((!IE_P_XCHG || deep) && wv == 0 && pend) {  // the first word, with the predecessor's tail
                     const uint32_t pt = wait_tail(a.st, t - step, a.tag, a.err);
                     const uint32_t s = uint32_t(Xw) & 31u;
-                    const uint32_t v = bswap32((pt << (32u - s)) | (misc[4] >> s));
+                    const uint32_t v = bswap32((pt << (32u - s)) | (misc[ML::H] >> s));
                     out[Xw >> 5] = v;
                     count(Xw >> 5, v);
                 }
@@ -3284,8 +3312,8 @@ static int encode4p_grid(bool hist, size_t lds) {
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hist) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4p_kernel<true>, 256, lds);
-    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4p_kernel<false>, 256, lds);
+    if (hist) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4p_kernel<true, 4>, 256, lds);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4p_kernel<false, 4>, 256, lds);
     per = std::min(per, IE_P_PER_CU);
     c = std::max(1, per) * std::max(1, cus);
     return c;
@@ -3305,7 +3333,11 @@ static int encode4q_grid() {
     return c;
 }
 
-void launch_encode4w(const EncArgs& a, hipStream_t s) {
+#ifndef IE_P_W8
+#define IE_P_W8 0  // 1: (A/B builds) launches too small to fill the chip run 8 waves per tile (one 4K frame: 16.9 against 16.3 us)
+#endif
+// Returns the FP64-statistics words per tile the launched kernel writes (its waves per tile).
+int launch_encode4w(const EncArgs& a, hipStream_t s) {
     // large segmented launches without the histogram may run the pipelined persistent encoder (two
     // or more tiles per workgroup; a smaller launch has nothing to overlap and keeps one tile per
     // workgroup; one long chain -- a concatenated stream -- would make its deferred look-backs
@@ -3315,17 +3347,22 @@ void launch_encode4w(const EncArgs& a, hipStream_t s) {
     const bool pipelined = pe && atoi(pe) != 0;
     if (IE_ENC_Q && pipelined && !a.ticket && !a.hist && !a.deep_lb && a.segmented && a.ntiles >= 2 * encode4q_grid()) {
         hipLaunchKernelGGL(encode4q_kernel, dim3(encode4q_grid()), dim3(256), kQLdsBytes, s, a, a.tab);
-        return;
+        return 4;
+    }
+    if (IE_ENC_P && IE_P_W8 && !a.ticket && !a.hist && a.deep_lb) {
+        hipLaunchKernelGGL((encode4p_kernel<false, 8>), dim3(a.ntiles), dim3(512), p_lds_bytes<8>(), s, a, a.tab);
+        return 8;
     }
     if (IE_ENC_P && !a.ticket) {
-        const size_t lds = kPLdsBytes + (a.hist ? 1024 * kWHistRep : 0);
+        const size_t lds = p_lds_bytes<4>() + (a.hist ? 1024 * kWHistRep : 0);
         const int grid = IE_P_PERSIST ? std::min(a.ntiles, encode4p_grid(a.hist != nullptr, lds)) : a.ntiles;
-        if (a.hist) hipLaunchKernelGGL(encode4p_kernel<true>, dim3(grid), dim3(256), lds, s, a, a.tab);
-        else hipLaunchKernelGGL(encode4p_kernel<false>, dim3(grid), dim3(256), lds, s, a, a.tab);
-        return;
+        if (a.hist) hipLaunchKernelGGL((encode4p_kernel<true, 4>), dim3(grid), dim3(256), lds, s, a, a.tab);
+        else hipLaunchKernelGGL((encode4p_kernel<false, 4>), dim3(grid), dim3(256), lds, s, a, a.tab);
+        return 4;
     }
     if (a.hist) hipLaunchKernelGGL(encode4w_kernel<true>, dim3(a.ntiles), dim3(256), kWLdsBytes + 1024 * kWHistRep, s, a, a.tab);
     else hipLaunchKernelGGL(encode4w_kernel<false>, dim3(a.ntiles), dim3(256), kWLdsBytes, s, a, a.tab);
+    return 4;
 }
 
 // The streamed host path's per-image header words: word i (read from page-locked host memory
@@ -3353,16 +3390,14 @@ int encode_small_tiles() {
 
 int encode_threads_per_tile() { return kEncTPB; }
 
-void launch_encode4w(const EncArgs& a, hipStream_t s);
+int launch_encode4w(const EncArgs& a, hipStream_t s);
 
-void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt) {
+int launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt) {
     EncArgs a = a0;
-    // 4x4 FAST over whole 16-byte groups: the wave-local encoder (encode4w_kernel)
+    // 4x4 FAST over whole 16-byte groups: the wave-local encoders (encode4p_kernel)
     if (IE_ENC_W && n == 4 && !exact && bpt == 4 && a.vec_ok && a.bx % 4 == 0 &&
-        a.groups_per_frame % 8 == 0 && a.rec_bits <= 252 && !a.ablate) {
-        launch_encode4w(a, s);
-        return;
-    }
+        a.groups_per_frame % 8 == 0 && a.rec_bits <= 252 && !a.ablate)
+        return launch_encode4w(a, s);
     a.img_words = image_words_for(n, bpt, a.rec_bits);
     if (n == 4 && a.img_words < fix_words<4>()) a.img_words = fix_words<4>();
     if (n == 8 && a.img_words < kFix8Words) a.img_words = kFix8Words;
@@ -3371,7 +3406,7 @@ void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt)
     const dim3 grid(a.ntiles), block(kEncTPB);
     if (a.hist) {  // segmented 4x4 FAST launches only (ie_encode_images_counted; 8x8 would spill)
         hipLaunchKernelGGL((encode_kernel<4, false, true>), grid, block, lds, s, a, a.tab);
-        return;
+        return kEncTPB / 64;
     }
     if (n == 4) {
         if (exact) hipLaunchKernelGGL((encode_kernel<4, true>), grid, block, lds, s, a, a.tab);
@@ -3380,6 +3415,7 @@ void launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt)
         if (exact) hipLaunchKernelGGL((encode_kernel<8, true>), grid, block, lds, s, a, a.tab);
         else hipLaunchKernelGGL((encode_kernel<8, false>), grid, block, lds, s, a, a.tab);
     }
+    return kEncTPB / 64;
 }
 
 }  // namespace ie

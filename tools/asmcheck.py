@@ -99,8 +99,9 @@ BUDGETS = {
     "_ZN2ie13encode_kernelILi8ELb0ELb0ELi1EEEvNS_7EncArgsEPKNS_9EncTablesE": (4, 0),
     "_ZN2ie15encode4w_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
     "_ZN2ie15encode4w_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
-    "_ZN2ie15encode4p_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
-    "_ZN2ie15encode4p_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
+    "_ZN2ie15encode4p_kernelILb0ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
+    "_ZN2ie15encode4p_kernelILb1ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
+    "_ZN2ie15encode4p_kernelILb0ELi8EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
     "_ZN2ie15encode4q_kernelENS_7EncArgsEPKNS_9EncTablesE": (4, 0),
 }
 # Persistent kernels: the host sizes the grid as (workgroups per CU) x CUs with workgroups per CU
@@ -108,8 +109,8 @@ BUDGETS = {
 # order), so the SGPR admission rule (MI355X_MICROARCH.md, Residency: 256-thread blocks per CU <=
 # floor(800 / (ceil(sgpr / 16) * 16 + 16))) must admit at least that many.
 PERSIST = {
-    "_ZN2ie15encode4p_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": 6,
-    "_ZN2ie15encode4p_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": 6,
+    "_ZN2ie15encode4p_kernelILb0ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": 6,
+    "_ZN2ie15encode4p_kernelILb1ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": 6,
     "_ZN2ie15encode4q_kernelENS_7EncArgsEPKNS_9EncTablesE": 4,
 }
 
