@@ -50,6 +50,9 @@ template <> struct ZigZagInv<8> {
                                     21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 };
 
+#ifndef IE_P_GEO  // encode4p_kernel: a tile's geometry fields in one scalar round trip (load_geo)
+#define IE_P_GEO 1
+#endif
 #ifndef IE_PROFILE
 #define IE_PROFILE 0
 #endif
@@ -633,6 +636,48 @@ __device__ __forceinline__ TileGeo tile_geo(const Args& a, int t, int tid) {
         g.bx0 = int(r - dq * uint32_t(a.gpr)) * BPT;
         g.nblk = min(BPT, a.bx - g.bx0);
     }
+    return g;
+}
+
+// The launch fields a tile's geometry and pixel loads need (EncArgs' first 27 words), read from
+// the kernel-argument segment in ONE scalar round trip (two s_load_dwordx16).  Read field by field,
+// the compiler sinks each load into the branch that uses it: a chain of ~6 dependent round trips
+// (≈1.1 µs under load, measured by stamps) before a tile's first pixel load and again at its start.
+struct GeoArgs {
+    const uint8_t* y;
+    uint64_t stride, frame_pitch;
+    int nframes, bx, by, gpr;
+    uint32_t gpr_magic;
+    int groups_per_frame, tiles_per_frame, ntiles;
+    FastDiv div_frames, div_tpf, div_gpr;
+    int segmented;
+};
+template <class KA>
+__device__ __forceinline__ GeoArgs load_geo(KA* ka) {
+    typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+    using P = const __attribute__((address_space(4))) u16v;
+    u16v A = ((P*)ka)[0], B = ((P*)ka)[1];
+    asm volatile("" : "+s"(A), "+s"(B));  // both loaded here, before any use
+    auto w = [&](size_t off) -> uint32_t { return off < 64 ? A[off / 4] : B[off / 4 - 16]; };
+    auto d = [&](size_t off) -> uint64_t { return uint64_t(w(off)) | (uint64_t(w(off + 4)) << 32); };
+    auto fd = [&](size_t off) { return FastDiv{w(off), w(off + 4), w(off + 8)}; };
+    static_assert(offsetof(EncArgs, segmented) + 4 <= 128, "geometry fields in the first 128 bytes");
+    GeoArgs g;
+    g.y = reinterpret_cast<const uint8_t*>(d(offsetof(EncArgs, y)));
+    g.stride = d(offsetof(EncArgs, stride));
+    g.frame_pitch = d(offsetof(EncArgs, frame_pitch));
+    g.nframes = int(w(offsetof(EncArgs, nframes)));
+    g.bx = int(w(offsetof(EncArgs, bx)));
+    g.by = int(w(offsetof(EncArgs, by)));
+    g.gpr = int(w(offsetof(EncArgs, gpr)));
+    g.gpr_magic = w(offsetof(EncArgs, gpr_magic));
+    g.groups_per_frame = int(w(offsetof(EncArgs, groups_per_frame)));
+    g.tiles_per_frame = int(w(offsetof(EncArgs, tiles_per_frame)));
+    g.ntiles = int(w(offsetof(EncArgs, ntiles)));
+    g.div_frames = fd(offsetof(EncArgs, div_frames));
+    g.div_tpf = fd(offsetof(EncArgs, div_tpf));
+    g.div_gpr = fd(offsetof(EncArgs, div_gpr));
+    g.segmented = int(w(offsetof(EncArgs, segmented)));
     return g;
 }
 
@@ -2135,6 +2180,7 @@ __global__ __launch_bounds__(64 * WPT, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void
     unsigned* const cnt = a_.claim;
     int chain = int(blockIdx.x) % nch;  // the chain this workgroup claims from (wave 0's copy counts)
     int t = int(blockIdx.x);
+    const GeoArgs ga0 = load_geo(ka);
     if (dyn) {
         if (wv == 0) {
             unsigned k = 0;
@@ -2154,13 +2200,15 @@ __global__ __launch_bounds__(64 * WPT, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void
             }
         }
     };
-    if (t < 0 || t >= a_.ntiles) {
+    if (t < 0 || t >= (IE_P_GEO ? ga0.ntiles : a_.ntiles)) {
         leave();
         return;
     }
+    // (profiling: the workgroup's entry on the chip-wide clock, wave 0's word 13)
+    if (IE_PROFILE && a_.stamps && (tid & 63) == 0 && wv < 4) a_.stamps[size_t(t) * kStamps + wv * 16 + 13] = __builtin_amdgcn_s_memrealtime();
     // each wave's pixel rows of tile tt into its own region (row r of the wave's block j at
     // reg[r BW + j]: a lane's 16 bytes are its group's row)
-    auto issue_pixels = [&](KArgs& a, int tt) {
+    auto issue_pixels = [&](const auto& a, int tt) {
         const int l0 = tid & 63;
         if (l0 >= GW) return;  // (8 waves per tile: a wave's 32 groups, one per lane)
         const TileGeo gg = tile_geo<4, 4, TG>(a, tt, GW * wv + l0);
@@ -2172,7 +2220,9 @@ __global__ __launch_bounds__(64 * WPT, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void
                                                  (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, 0);
         }
     };
-    issue_pixels(*ka, t);
+    if (IE_P_GEO) issue_pixels(ga0, t);
+    else issue_pixels(*ka, t);
+    if (IE_PROFILE == 2 && a_.stamps && (tid & 63) == 0 && wv < 4) a_.stamps[size_t(t) * kStamps + wv * 16 + 1] = __builtin_amdgcn_s_memrealtime();
     // the FP64 rows (waves 0-2: 2432 bytes) and the matrix-pipe A fragments (wave 3; read back per
     // slot: a register copy held across the tile loop measured as spills) by DMA too: no register
     // round trip, one wait for everything
@@ -2193,9 +2243,11 @@ __global__ __launch_bounds__(64 * WPT, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void
         misc0[ML::S + ML::F + wv] = 0u;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA above and the first tile's pixels)
+    if (IE_PROFILE && a_.stamps && (tid & 63) == 0 && wv < 4) a_.stamps[size_t(t) * kStamps + wv * 16 + 12] = __builtin_amdgcn_s_memrealtime();
     const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
     const bool deep = a_.deep_lb != 0;
     lds_barrier();  // the rows, the A fragments (and the HIST bins) visible
+    if (IE_PROFILE && a_.stamps && (tid & 63) == 0 && wv < 4) a_.stamps[size_t(t) * kStamps + wv * 16 + 11] = __builtin_amdgcn_s_memrealtime();
 
     for (int iter = 0;; iter++) {
         asm volatile("" : "+s"(ka));
@@ -2206,16 +2258,17 @@ __global__ __launch_bounds__(64 * WPT, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void
         asm volatile("" : "+v"(tid));
         const int lane = tid & 63;
         uint32_t* const misc = misc0 + (iter & 1) * ML::S;
-        const TileGeo g = tile_geo<4, 4, TG>(a, t, tid);
+        const GeoArgs ga = load_geo(ka);
+        const TileGeo g = IE_P_GEO ? tile_geo<4, 4, TG>(ga, t, tid) : tile_geo<4, 4, TG>(a, t, tid);
         const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
-        const int ng = min(TG, a.groups_per_frame - tif * TG);
+        const int ng = min(TG, (IE_P_GEO ? ga.groups_per_frame : a.groups_per_frame) - tif * TG);
         const int nbw = 4 * min(GW, max(0, ng - GW * wv));  // blocks of this wave
         const int wlast = (ng - 1) / GW;                    // the tile's last non-empty wave
         WSTAMP(0);
         WRTSTAMP(14);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
         if (wv == 0 && lane == 0) misc[ML::CL] = 0u;  // the next tile's claim: not yet made (read after barrier 2)
-        WSTAMP(1);
+        if (IE_PROFILE != 2) WSTAMP(1);
         asm volatile("; PHASE p1" ::: "memory");
 
         // -------------------------------------------------------- transform + quantise, 4 slots
