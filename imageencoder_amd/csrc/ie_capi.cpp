@@ -86,10 +86,27 @@ struct ie_ctx {
     int hist_count[2] = {};
     uint8_t* h_pack[2] = {};
     size_t cap_hpack[2] = {};
-    hipEvent_t ev_pack[2] = {};
+    hipEvent_t ev_pack[2] = {};    // the table copy out of pinned slot i (on tab_stream)
     bool pack_recorded[2] = {};
+    uint8_t* d_pack[2] = {};       // device table slots
+    size_t cap_dpack[2] = {};
+    hipEvent_t ev_packed[2] = {};  // the pack (and prefix copies) that read device slot i
+    bool packed_recorded[2] = {};
+    hipStream_t tab_stream = nullptr;
     int pack_slot = 0;
-    int fused_count = 0;  // > 0: the last encode (ie_encode_images_counted) left this many histograms in d_batch
+    int fused_count = 0;  // > 0: the last encode (ie_encode_images_counted) left this many histograms in d_chist
+    // the counted pipeline: the encoder's histograms (cleared by the first-occurrence pass that reads
+    // them: chist_zero), and per pinned slot the device n / first / unresolved the rare first_full
+    // pass of ie_huffman_hist_batch_wait needs, with the batch it reads
+    uint32_t* d_chist = nullptr;
+    size_t cap_chist = 0;  // (words)
+    bool chist_zero = false;
+    bool hist_skip_zero = false;  // one shot: encode() skips its histogram memset (set by the counted encode)
+    uint8_t* d_cslot[2] = {};
+    size_t cap_cslot[2] = {};
+    bool hist_fused[2] = {};
+    const uint8_t* hist_in[2] = {};
+    size_t hist_pitch[2] = {};
     // decoder scratch
     uint8_t* d_dec = nullptr;          // staged stream + padding
     size_t cap_dec = 0;
@@ -649,7 +666,8 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     a.err = c->d_err;
     a.wave_fix = c->d_wave_fix;
     c->last_fix_words = 0;  // (set after the launch: its kernel's waves per tile)
-    if (L.hist) HIPCHK(c, hipMemsetAsync(L.hist, 0, size_t(L.nframes) * 256 * sizeof(uint32_t), c->stream));
+    if (L.hist && !c->hist_skip_zero) HIPCHK(c, hipMemsetAsync(L.hist, 0, size_t(L.nframes) * 256 * sizeof(uint32_t), c->stream));
+    c->hist_skip_zero = false;  // (a re-launch clears)
     uint64_t* d_stamps = nullptr;
     if (stamp_file) {
         HIPCHK(c, hipMalloc(&d_stamps, size_t(g.ntiles) * ie::kStamps * sizeof(uint64_t)));
@@ -1561,6 +1579,10 @@ int ie_destroy(ie_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->own) (void)hipStreamSynchronize(c->own);
     if (c->stream && c->stream != c->own) (void)hipStreamSynchronize(c->stream);
+    if (c->tab_stream) {
+        (void)hipStreamSynchronize(c->tab_stream);
+        (void)hipStreamDestroy(c->tab_stream);
+    }
     (void)hipFree(c->d_tab);
     (void)hipHostFree(c->h_tab);
     (void)hipFree(c->d_state);
@@ -1578,11 +1600,15 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_hist);
     (void)hipFree(c->d_batch);
     (void)hipHostFree(c->h_batch);
+    (void)hipFree(c->d_chist);
     for (int i = 0; i < 2; i++) {
+        (void)hipFree(c->d_cslot[i]);
         if (c->h_hist[i]) (void)hipHostFree(c->h_hist[i]);
         if (c->h_pack[i]) (void)hipHostFree(c->h_pack[i]);
         if (c->ev_hist[i]) (void)hipEventDestroy(c->ev_hist[i]);
         if (c->ev_pack[i]) (void)hipEventDestroy(c->ev_pack[i]);
+        if (c->ev_packed[i]) (void)hipEventDestroy(c->ev_packed[i]);
+        (void)hipFree(c->d_pack[i]);
     }
     for (hipEvent_t e : c->stage_ev)
         if (e) (void)hipEventDestroy(e);
@@ -1859,12 +1885,20 @@ int ie_encode_images_counted(ie_ctx* c, const uint8_t* y, int w, int h, size_t s
     if (mode == IE_MODE_EXACT || c->n != 4 || !is_device_ptr(out))
         return ie_encode_images(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_pitch, start_bit,
                                 nullptr);
-    // the counts go where ie_huffman_hist_batch_ends_async expects them (d_batch, same layout)
+    // the counts go to d_chist, where ie_huffman_hist_batch_ends_async reads (and clears) them: the
+    // memset before the launch only when they are not known to be zero
     const size_t K = size_t(nframes);
     int r;
-    if ((r = ensure(c, c->d_batch, c->cap_batch, K * 256 * 12 + K * 8 + K * 4))) return r;
+    if (c->cap_chist < K * 256 || !c->d_chist) {
+        if ((r = ensure(c, c->d_chist, c->cap_chist, K * 256))) return r;
+        HIPCHK(c, hipMemsetAsync(c->d_chist, 0, c->cap_chist * sizeof(uint32_t), c->stream));
+        c->chist_zero = true;
+    }
+    c->hist_skip_zero = c->chist_zero;
+    c->chist_zero = false;
     r = encode(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_pitch * K, out_pitch, start_bit, 1,
-               nullptr, nullptr, nullptr, reinterpret_cast<uint32_t*>(c->d_batch));
+               nullptr, nullptr, nullptr, c->d_chist);
+    c->hist_skip_zero = false;
     if (r == IE_OK) c->fused_count = nframes;
     return r;
 }
@@ -2086,17 +2120,39 @@ int ie_huffman_hist_batch_ends_async(ie_ctx* c, const uint8_t* in, size_t in_pit
     const size_t hb = size_t(count) * 256 * sizeof(uint32_t), fb = size_t(count) * 256 * sizeof(uint64_t);
     const size_t nb = size_t(count) * sizeof(uint64_t), ub = size_t(count) * sizeof(unsigned);
     int r;
-    if (fused && c->cap_batch < hb + fb + nb + ub) return fail(c, IE_EINVAL, "fused histogram scratch lost");
-    if ((r = ensure(c, c->d_batch, c->cap_batch, hb + fb + nb + ub))) return r;
-    if ((r = ensure_pinned(c, c->h_hist[slot], c->cap_hhist[slot], hb + fb))) return r;
+    if ((r = ensure_pinned(c, c->h_hist[slot], c->cap_hhist[slot], hb + fb + ub))) return r;
     if (!c->ev_hist[slot]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_hist[slot], hipEventDisableTiming));
+    c->hist_fused[slot] = fused;
+    c->hist_in[slot] = in;
+    c->hist_pitch[slot] = in_pitch;
+    if (fused) {
+        // counts from the encoder (cleared as they are read), lengths from the end bits, results
+        // straight into the pinned slot: ONE launch, no memset, no copy
+        if ((r = ensure(c, c->d_cslot[slot], c->cap_cslot[slot], fb + nb + ub))) return r;
+        uint8_t* hp = nullptr;
+        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&hp), c->h_hist[slot], 0));
+        uint8_t* ds = c->d_cslot[slot];
+        if ((r = stage_mark(c, 0))) return r;
+        ie::launch_first_counted(in, in_pitch, end_bits, uint64_t(in_pitch), count, c->d_chist,
+                                 reinterpret_cast<uint64_t*>(ds + fb), reinterpret_cast<unsigned long long*>(ds),
+                                 reinterpret_cast<unsigned*>(ds + fb + nb), reinterpret_cast<uint32_t*>(hp),
+                                 reinterpret_cast<unsigned long long*>(hp + hb), reinterpret_cast<unsigned*>(hp + hb + fb),
+                                 c->stream);
+        HIPCHK(c, hipGetLastError());
+        c->chist_zero = true;
+        if ((r = stage_mark(c, 1))) return r;
+        HIPCHK(c, hipEventRecord(c->ev_hist[slot], c->stream));
+        c->hist_count[slot] = count;
+        return IE_OK;
+    }
+    if ((r = ensure(c, c->d_batch, c->cap_batch, hb + fb + nb + ub))) return r;
     uint32_t* dh = reinterpret_cast<uint32_t*>(c->d_batch);
     auto* df = reinterpret_cast<unsigned long long*>(c->d_batch + hb);
     auto* dn = reinterpret_cast<uint64_t*>(c->d_batch + hb + fb);
     auto* du = reinterpret_cast<unsigned*>(c->d_batch + hb + fb + nb);
     if ((r = stage_mark(c, 0))) return r;
-    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream, fused ? nullptr : dh, df);
-    ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream, !fused);
+    ie::launch_ends_to_bytes(end_bits, uint64_t(in_pitch), count, dn, c->stream, dh, df);
+    ie::launch_hist_batch(in, in_pitch, dn, uint64_t(in_pitch), count, dh, df, du, c->stream, true);
     HIPCHK(c, hipGetLastError());
     if ((r = stage_mark(c, 1))) return r;
     // histograms and first positions are contiguous on the device: one read-back
@@ -2110,10 +2166,36 @@ int ie_huffman_hist_batch_wait(ie_ctx* c, int slot, uint32_t* hist, uint64_t* fi
     if (!c || slot < 0 || slot > 1 || !hist || !first_pos) return IE_EINVAL;
     if (!c->ev_hist[slot] || !c->hist_count[slot]) return fail(c, IE_EINVAL, "no histogram pending in this slot");
     HIPCHK(c, hipEventSynchronize(c->ev_hist[slot]));
-    const size_t hb = size_t(c->hist_count[slot]) * 256 * sizeof(uint32_t);
+    const int K = c->hist_count[slot];
+    const size_t hb = size_t(K) * 256 * sizeof(uint32_t), fb = size_t(K) * 256 * sizeof(uint64_t);
+    const size_t nb = size_t(K) * sizeof(uint64_t);
     std::memcpy(hist, c->h_hist[slot], hb);
-    std::memcpy(first_pos, c->h_hist[slot] + hb, size_t(c->hist_count[slot]) * 256 * sizeof(uint64_t));
+    std::memcpy(first_pos, c->h_hist[slot] + hb, fb);
     c->hist_count[slot] = 0;
+    if (c->hist_fused[slot]) {
+        // a string whose first-occurrence scan stopped short (a value first seen past its first
+        // 64 chunks): the full pass over the batch, then the device's positions
+        const unsigned* un = reinterpret_cast<const unsigned*>(c->h_hist[slot] + hb + fb);
+        bool any = false;
+        uint64_t maxn = 0;
+        for (int k = 0; k < K; k++) any |= un[k] != 0u;
+        if (any) {
+            uint64_t* nn = reinterpret_cast<uint64_t*>(c->d_cslot[slot] + fb);
+            for (int k = 0; k < K; k++) {
+                uint64_t s = 0;
+                for (int b = 0; b < 256; b++) s += hist[256 * k + b];
+                maxn = std::max(maxn, s);
+            }
+            uint8_t* hp = nullptr;
+            HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&hp), c->h_hist[slot], 0));
+            ie::launch_first_full_batch(c->hist_in[slot], c->hist_pitch[slot], nn, maxn, K, reinterpret_cast<const uint32_t*>(hp),
+                                        reinterpret_cast<unsigned long long*>(c->d_cslot[slot]),
+                                        reinterpret_cast<const unsigned*>(c->d_cslot[slot] + fb + nb), c->stream);
+            HIPCHK(c, hipGetLastError());
+            HIPCHK(c, hipMemcpyAsync(first_pos, c->d_cslot[slot], fb, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
+    }
     return IE_OK;
 }
 
@@ -2122,7 +2204,6 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
                           uint8_t* out, size_t out_pitch, const uint64_t* start_bit, uint64_t* end_bit) {
     if (!c || !in || !n || count <= 0 || !code || !len || !out || !start_bit || (!prefix && prefix_pitch))
         return IE_EINVAL;
-    c->fused_count = 0;  // the staged tables overwrite the batch scratch
     if (!is_device_ptr(in) || !is_device_ptr(out))
         return fail(c, IE_EINVAL, "batched Huffman input and output must be device memory");
     if (reinterpret_cast<uintptr_t>(out) % 4 || out_pitch % 4)
@@ -2158,13 +2239,19 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
     const size_t o_ts = 0, o_n = o_ts + 8 * (K + 1), o_st = o_n + 8 * K, o_code = o_st + 8 * K;
     const size_t o_pre = o_code + 4 * 256 * K, o_len = o_pre + 4 * size_t(pw) * K, total = o_len + 256 * K;
     int r;
-    if ((r = ensure(c, c->d_batch, c->cap_batch, total))) return r;
-    // two pinned staging slots in turn: wait only for this slot's previous copy, not the stream
+    // two pinned staging slots and two device table slots in turn: wait only for this slot's
+    // previous copy, not the stream.  The copy runs on a side stream as soon as the tables exist
+    // (beside whatever the context's stream is running, e.g. the next batch's encode); the pack
+    // waits for it by event, and the copy into a device slot waits for the pack that last read it.
     const int ps = c->pack_slot;
     c->pack_slot ^= 1;
     if (c->pack_recorded[ps]) HIPCHK(c, hipEventSynchronize(c->ev_pack[ps]));
     if ((r = ensure_pinned(c, c->h_pack[ps], c->cap_hpack[ps], total))) return r;
+    if (c->cap_dpack[ps] < total && c->d_pack[ps]) HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((r = ensure(c, c->d_pack[ps], c->cap_dpack[ps], total))) return r;
     if (!c->ev_pack[ps]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_pack[ps], hipEventDisableTiming));
+    if (!c->ev_packed[ps]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_packed[ps], hipEventDisableTiming));
+    if (!c->tab_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->tab_stream, hipStreamNonBlocking));
     uint8_t* h = c->h_pack[ps];
     std::memcpy(h + o_ts, ts.data(), 8 * (K + 1));
     std::memcpy(h + o_n, n, 8 * K);
@@ -2180,10 +2267,12 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         std::memcpy(d, prefix + k * prefix_pitch, nbytes);
         if (sb % 8) d[nbytes - 1] &= uint8_t(0xFF00u >> (sb % 8));  // bits from start_bit on are the packer's
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_batch, h, total, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipEventRecord(c->ev_pack[ps], c->stream));
+    if (c->packed_recorded[ps]) HIPCHK(c, hipStreamWaitEvent(c->tab_stream, c->ev_packed[ps], 0));
+    HIPCHK(c, hipMemcpyAsync(c->d_pack[ps], h, total, hipMemcpyHostToDevice, c->tab_stream));
+    HIPCHK(c, hipEventRecord(c->ev_pack[ps], c->tab_stream));
     c->pack_recorded[ps] = true;
-    const uint8_t* d = c->d_batch;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_pack[ps], 0));
+    const uint8_t* d = c->d_pack[ps];
     // strings without bytes: the prefix alone
     for (size_t k = 0; k < K; k++)
         if (n[k] == 0)
@@ -2218,6 +2307,8 @@ int ie_huffman_pack_batch(ie_ctx* c, const uint8_t* in, size_t in_pitch, const u
         HIPCHK(c, hipGetLastError());
         if (c->use_ticket) c->ticket_base += ntiles;
     }
+    HIPCHK(c, hipEventRecord(c->ev_packed[ps], c->stream));  // (the table slot's readers are done)
+    c->packed_recorded[ps] = true;
     if (!end_bit) {
         if (ntiles) note_async(c, "Huffman batch pack");
         return IE_OK;

@@ -171,6 +171,12 @@ void launch_hist(const uint8_t* in, uint64_t n, uint32_t* hist, unsigned long lo
 // hist/first + 256*k
 // counts = false: hist already holds the counts (an encoder launch with EncArgs::hist); only the
 // first occurrences are computed
+// the counted pipeline's first-occurrence pass (ie_huffman.hip first_scan_counted_kernel)
+void launch_first_counted(const uint8_t* in, uint64_t pitch, const uint64_t* ends, uint64_t cap, int count,
+                          uint32_t* hist, uint64_t* n, unsigned long long* first, unsigned* unresolved, uint32_t* h_hist,
+                          unsigned long long* h_first, unsigned* h_unres, hipStream_t s);
+void launch_first_full_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count,
+                             const uint32_t* hist, unsigned long long* first, const unsigned* unresolved, hipStream_t s);
 void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count, uint32_t* hist,
                        unsigned long long* first, unsigned* unresolved, hipStream_t s, bool counts = true);
 

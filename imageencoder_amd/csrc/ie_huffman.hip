@@ -75,26 +75,60 @@ __device__ __forceinline__ void hist_body(const uint8_t* __restrict__ in, uint64
 // (every value appears within a few KiB) one or two chunks.  At most kFirstScanChunks chunks;
 // values still missing after that are left to first_full (unresolved[k] = 1).
 constexpr int kFirstScanChunks = 64;
-__device__ __forceinline__ void first_scan_body(const uint8_t* __restrict__ in, uint64_t n, const uint32_t* hist,
-                                                unsigned long long* first, unsigned* unresolved) {
+#ifndef IE_FIRST_Q
+#define IE_FIRST_Q 4
+#endif
+constexpr int kFirstScanQ = IE_FIRST_Q;  // chunks per round of first_scan
+// (hv: this thread's value's count; returns its first position, *unres = 1 if the scan stopped short)
+__device__ __forceinline__ unsigned long long first_scan_core(const uint8_t* __restrict__ in, uint64_t n, uint32_t hv,
+                                                              unsigned* unres) {
     __shared__ unsigned long long f[256];
     const int tid = threadIdx.x;
     f[tid] = ~0ull;
-    const int need = __syncthreads_count(hist[tid] != 0u);
+    const int need = __syncthreads_count(hv != 0u);
     int have = 0;
-    for (int ch = 0; ch < kFirstScanChunks && have < need; ch++) {
-        const uint64_t p = uint64_t(ch) * kHistTile + uint64_t(tid) * 16;
-        for (int e = 0; e < 16; e++)
-            if (p + e < n) {
-                const uint32_t b = in[p + e];
-                // (> and not "unset": another thread of this chunk may have set a later position)
-                if (f[b] > p + e) atomicMin(&f[b], (unsigned long long)(p + e));
+    // kFirstScanQ chunks per round, one 16-byte load each per thread, all in flight together (a
+    // round per chunk made the scan a chain of load round trips)
+    constexpr int Q = kFirstScanQ;
+    static_assert(kFirstScanChunks % Q == 0, "whole rounds");
+    const bool al = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+    for (int ch = 0; ch < kFirstScanChunks && have < need; ch += Q) {
+        uint4 v[Q];
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const uint64_t p = uint64_t(ch + q) * kHistTile + uint64_t(tid) * 16;
+            if (al && p + 16 <= n) {
+                v[q] = *reinterpret_cast<const uint4*>(in + p);
+            } else {
+                uint32_t w[4] = {0u, 0u, 0u, 0u};
+                for (int e = 0; e < 16; e++)
+                    if (p + e < n) w[e >> 2] |= uint32_t(in[p + e]) << (8 * (e & 3));
+                v[q] = make_uint4(w[0], w[1], w[2], w[3]);
             }
+        }
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const uint64_t p = uint64_t(ch + q) * kHistTile + uint64_t(tid) * 16;
+            const uint32_t w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+            for (int e = 0; e < 16; e++)
+                if (p + e < n) {
+                    const uint32_t b = (w[e >> 2] >> (8 * (e & 3))) & 0xFFu;
+                    // (> and not "unset": another thread of this round may have set a later position)
+                    if (f[b] > p + e) atomicMin(&f[b], (unsigned long long)(p + e));
+                }
+        }
         have = __syncthreads_count(f[tid] != ~0ull);
-        if (uint64_t(ch + 1) * kHistTile >= n) break;
+        if (uint64_t(ch + Q) * kHistTile >= n) break;
     }
-    first[tid] = f[tid];
-    if (tid == 0) *unresolved = (have < need) ? 1u : 0u;
+    *unres = (have < need) ? 1u : 0u;
+    return f[tid];
+}
+__device__ __forceinline__ void first_scan_body(const uint8_t* __restrict__ in, uint64_t n, const uint32_t* hist,
+                                                unsigned long long* first, unsigned* unresolved) {
+    unsigned u;
+    first[threadIdx.x] = first_scan_core(in, n, hist[threadIdx.x], &u);
+    if (threadIdx.x == 0) *unresolved = u;
 }
 
 // The values first_scan did not find: every byte of the string (past the scanned prefix) checks a
@@ -152,6 +186,49 @@ __global__ __launch_bounds__(kTPB) void first_full_batch_kernel(const uint8_t* _
                                                                 unsigned long long* first, const unsigned* unresolved) {
     const int k = blockIdx.y;
     first_full_body(in + uint64_t(k) * pitch, n[k], hist + 256 * k, first + 256 * k, unresolved + k);
+}
+
+// The first-occurrence pass of the counted pipeline (ie_encode_images_counted, then
+// ie_huffman_hist_batch_ends_async): string blockIdx.x's length from its end bit, its counts from
+// the encoder's histogram -- CLEARED here for the next counted encode (no memset launch) -- and the
+// counts, first positions and unresolved flag written straight into the caller's pinned read-back
+// slot h_* (no copy launch).  n / first / unresolved (device) keep what first_full needs for the
+// rare string whose scan stopped short (run by the host's wait, ie_huffman_hist_batch_wait).
+__global__ __launch_bounds__(kTPB) void first_scan_counted_kernel(const uint8_t* __restrict__ in, uint64_t pitch,
+                                                                  const uint64_t* __restrict__ ends, uint64_t cap,
+                                                                  uint32_t* hist, uint64_t* n_out,
+                                                                  unsigned long long* first, unsigned* unresolved,
+                                                                  uint32_t* h_hist, unsigned long long* h_first,
+                                                                  unsigned* h_unres) {
+    const int k = blockIdx.x, tid = threadIdx.x;
+    const uint64_t n = min<uint64_t>((ends[k] + 7) / 8, cap);
+    const uint32_t hv = hist[256 * k + tid];
+    hist[256 * k + tid] = 0u;
+    h_hist[256 * k + tid] = hv;
+    unsigned u;
+    const unsigned long long f = first_scan_core(in + uint64_t(k) * pitch, n, hv, &u);
+    first[256 * k + tid] = f;
+    h_first[256 * k + tid] = f;
+    if (tid == 0) {
+        n_out[k] = n;
+        unresolved[k] = u;
+        h_unres[k] = u;
+    }
+}
+void launch_first_counted(const uint8_t* in, uint64_t pitch, const uint64_t* ends, uint64_t cap, int count,
+                          uint32_t* hist, uint64_t* n, unsigned long long* first, unsigned* unresolved, uint32_t* h_hist,
+                          unsigned long long* h_first, unsigned* h_unres, hipStream_t s) {
+    hipLaunchKernelGGL(first_scan_counted_kernel, dim3(count), dim3(kTPB), 0, s, in, pitch, ends, cap, hist, n, first,
+                       unresolved, h_hist, h_first, h_unres);
+}
+// first_full over a batch whose first_scan left strings unresolved (hist: any device-readable copy)
+void launch_first_full_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uint64_t maxn, int count,
+                             const uint32_t* hist, unsigned long long* first, const unsigned* unresolved, hipStream_t s) {
+    const uint64_t tiles = (maxn + kHistTile - 1) / kHistTile;
+    const uint64_t per = (4096 + count - 1) / count;
+    const int gx = int(tiles < per ? (tiles ? tiles : 1) : per);
+    hipLaunchKernelGGL(first_full_batch_kernel, dim3(gx, count), dim3(kTPB), 0, s, in, pitch, n, hist, first,
+                       unresolved);
 }
 
 // n[k] = the byte length of a stream ending at bit ends[k] (capped at cap): the batched Huffman

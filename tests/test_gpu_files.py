@@ -362,20 +362,35 @@ def test_huffman_after_encode_pipeline(codec):
         assert host[k * hpitch: k * hpitch + sizes[k]].tobytes() == want, k
 
 
+def _late_frames(w, h, f, seed):
+    """Flat frames whose last 32 rows are noise: their streams' byte values other than the flat
+    records' first appear past the first-occurrence scan's prefix (64 chunks of 4 KiB), so the
+    counted pipeline takes its full-pass fallback."""
+    rng = np.random.default_rng(seed)
+    y = np.full((f, h, w), 77, dtype=np.uint8)
+    y[:, h - 32:, :] = rng.integers(0, 256, (f, 32, w), dtype=np.uint8)
+    return y
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("counted", [False, True], ids=["hist_pass", "counted_encode"])
-def test_huffman_after_encode_pipelined(codec, counted):
+@pytest.mark.parametrize("counted,late", [(False, False), (True, False), (True, True)],
+                         ids=["hist_pass", "counted_encode", "counted_late_values"])
+def test_huffman_after_encode_pipelined(codec, counted, late):
     """Batches pipelined as in bench.py's C5 step: batch i+1's encode and histogram are issued
     before batch i's trees + pack (two output buffers, histogram slots alternating); every
     image's Huffman-coded file still equals the reference's.  counted: the byte counts come from
-    the encoder itself (ie_encode_images_counted)."""
+    the encoder itself (ie_encode_images_counted).  late: values first seen past the scanned
+    prefix (the full first-occurrence pass, run from ie_huffman_hist_batch_wait)."""
     import torch
     from imageencoder_amd import stream_bound, write_header
     n, q, w, h, f, nb = 4, O.read_matrix("matrix.txt", 4), 256, 128, 3, 4
+    if late:
+        w, h, f, nb = 2048, 2048, 2, 3
     codec.set_quant(q, n)
     hdr, hb = write_header(n, q, True, w, h, huffman=True)
     pitch = (stream_bound(w, h, n, 1, hb) + 255) // 256 * 256
-    ys = [synth.frames("M" if b % 2 else "U", w, h, f, seed=50 + b) for b in range(nb)]
+    ys = [_late_frames(w, h, f, 50 + b) if late else synth.frames("M" if b % 2 else "U", w, h, f, seed=50 + b)
+          for b in range(nb)]
     outs = []
     for _ in range(2):
         o = torch.zeros(pitch * f, dtype=torch.uint8)
@@ -412,6 +427,7 @@ def test_huffman_after_encode_pipelined(codec, counted):
     (200, 56, 4, 0, "U"),        # no header; ragged tile coverage
     (1000, 600, 3, 64, "U"),     # multi-tile chains, header of whole words
     (3840, 2160, 2, 171, "M"),   # 4K: hundreds of tiles per chain
+    (2048, 2048, 2, 165, "late"),  # values first seen past the scanned prefix: the full pass
 ])
 def test_counted_encode_histogram(codec, w, h, f, start_bit, kind):
     """ie_encode_images_counted's fused byte counts equal the separate histogram pass's and a
@@ -422,7 +438,7 @@ def test_counted_encode_histogram(codec, w, h, f, start_bit, kind):
     n, q = 4, O.read_matrix("matrix.txt", 4)
     codec.set_quant(q, n)
     pitch = (stream_bound(w, h, n, 1, start_bit) + 255) // 256 * 256
-    y = torch.from_numpy(synth.frames(kind, w, h, f, seed=77)).cuda()
+    y = torch.from_numpy(_late_frames(w, h, f, 77) if kind == "late" else synth.frames(kind, w, h, f, seed=77)).cuda()
     rng = np.random.default_rng(5)
     out = torch.zeros(pitch * f, dtype=torch.uint8)
     nh = (start_bit + 7) // 8
@@ -443,6 +459,8 @@ def test_counted_encode_histogram(codec, w, h, f, start_bit, kind):
         np.testing.assert_array_equal(h_pass[k], want)
         np.testing.assert_array_equal(h_fused[k], want)
     np.testing.assert_array_equal(f_fused, f_pass)
+    if kind == "late":  # the case exercises the full pass: some value first seen past 64 chunks of 4 KiB
+        assert int(f_pass[f_pass != np.uint64(2**64 - 1)].max()) >= 64 * 4096
 
 
 # ------------------------------------------------- multi-segment decode; one-launch path (opt-in)
