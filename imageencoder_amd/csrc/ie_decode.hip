@@ -83,62 +83,6 @@ __device__ __forceinline__ void huf_l1(const uint16_t* lut, uint16_t* l1) {
     __syncthreads();
 }
 
-// Walk [pos, end): returns the exit position; *cnt symbols; out (optional) receives them.
-__device__ __forceinline__ uint64_t huf_walk(const HufArgs& a, const uint16_t* l1, uint64_t pos, uint64_t end,
-                                             uint32_t* cnt, uint8_t* out, bool exact) {
-    uint32_t c = 0;
-    while (pos < end && pos < a.nbits) {
-        const uint32_t p15 = getbits(a.words, pos, 15);
-        uint32_t e = l1[p15 >> (15 - kHufL1)];
-        if (!e) e = a.lut[p15];
-        const uint32_t len = e >> 8;
-        if (!len) {  // no code starts here: a speculative walk slides; the exact walk reports
-            if (exact) {
-                atomicOr(&a.changed[1], 1u);
-                break;
-            }
-            pos += 1;
-            continue;
-        }
-        if (out) out[c] = uint8_t(e);
-        c++;
-        pos += len;
-    }
-    *cnt = c;
-    return pos;
-}
-
-// The counting walk: each chunk from its true entry (its top-level entry through every level's
-// prefix map of the composed transfer tables), symbols counted; the entry is kept for the emit.
-// The workgroup scans its chunks' counts: base[k] = the symbols before chunk k among the
-// workgroup's, wgsum[g] = the workgroup's total (no separate scan launch).
-__global__ __launch_bounds__(kTPB) void huf_walk_kernel(HufArgs a) {
-    __shared__ uint16_t l1[1 << kHufL1];
-    __shared__ alignas(8) uint32_t scratch[8];
-    huf_l1(a.lut, l1);
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t c = 0;
-    if (k < a.nchunks) {
-        const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
-        int u = k;
-        for (int l = 0; l < a.levels; l++) u /= kHufG;
-        uint32_t x = a.E[u];
-        for (int l = a.levels - 1; l >= 0; l--) {
-            int ul = k;
-            for (int m = 0; m < l; m++) ul /= kHufG;
-            x = a.lvl[l][size_t(ul) * kHufD + x];
-        }
-        const uint64_t e = cstart + x;
-        a.entry[k] = e;
-        huf_walk(a, l1, e, cstart + a.chunk_bits, &c, nullptr, false);
-        a.count[k] = c;
-    }
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan(c, scratch, &tot);
-    if (k < a.nchunks) a.base[k] = ex;
-    if (threadIdx.x == 0) a.wgsum[blockIdx.x] = tot;
-}
-
 // The symbols before workgroup g's chunks: the totals of the workgroups before it, summed by the
 // whole workgroup (every thread receives it).
 __device__ __forceinline__ uint64_t huf_wg_prefix(const uint32_t* wgsum, int g, uint32_t* scratch) {
@@ -149,33 +93,6 @@ __device__ __forceinline__ uint64_t huf_wg_prefix(const uint32_t* wgsum, int g, 
     __syncthreads();
     const uint64_t* s64 = reinterpret_cast<const uint64_t*>(scratch);
     return s64[0] + s64[1] + s64[2] + s64[3];
-}
-
-// The emitting walk: every chunk again from its entry, its symbols into LDS at the chunk's place
-// in the workgroup's output, then the workgroup's output copied out whole (consecutive lanes,
-// consecutive bytes) -- a lane writing its own chunk's bytes straight to memory touches 64 lines
-// per store instruction.  A workgroup whose output exceeds the buffer writes from the walk.
-#ifndef IE_HUF_EMIT_LDS
-#define IE_HUF_EMIT_LDS 40960
-#endif
-__global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
-    __shared__ uint16_t l1[1 << kHufL1];
-    __shared__ alignas(8) uint32_t scratch[8];
-    __shared__ uint8_t sym[IE_HUF_EMIT_LDS > 0 ? IE_HUF_EMIT_LDS : 1];
-    huf_l1(a.lut, l1);
-    const uint64_t pre = huf_wg_prefix(a.wgsum, int(blockIdx.x), scratch);
-    const uint32_t tot = a.wgsum[blockIdx.x];
-    const bool staged = IE_HUF_EMIT_LDS > 0 && tot <= uint32_t(IE_HUF_EMIT_LDS);
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < a.nchunks) {
-        const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
-        uint32_t c;
-        if (staged) huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, sym + a.base[k], true);
-        else huf_walk(a, l1, a.entry[k], cstart + a.chunk_bits, &c, a.out + pre + a.base[k], true);
-    }
-    if (!staged) return;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < tot; i += kTPB) a.out[pre + i] = sym[i];
 }
 
 // total receives the symbol count (device, 1 word): the sum of the walk's workgroup totals.
@@ -1066,14 +983,27 @@ void launch_rec_spec_decode(const RecParseArgs& a, const DecArgs& d, int n, hipS
 // of the record stream, with 15 entries instead of D.  huf_table_kernel walks all 15 entries of
 // 16 chunks per workgroup (one lane each, the chunks' bits staged in LDS; a position where no code
 // starts slides one bit -- never on the true path of a valid stream); compose_kernel composes the
-// tables; huf_walk_kernel (mode 2) then walks each chunk once from its true entry for the symbol
-// count, and huf_emit_kernel writes the symbols.  Exact for any content: a periodic stream (e.g. a
+// tables; huf_count_kernel reads each chunk's symbol count at its true entry, and huf_emit_kernel
+// writes the symbols.  Exact for any content: a periodic stream (e.g. a
 // flat image's records, Huffman-coded) no longer leaves speculative walks locked in a wrong phase.
-__global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* tab) {
+// Walks from different entries of a chunk fall onto the same code boundaries after a few codes
+// (prefix codes resynchronise), so only the first kHufSync bits are walked from all 15 entries: the
+// walks that stand on the same first boundary at or past cs + kHufSync have merged; one walk per
+// distinct boundary (almost always one per chunk) goes on to the chunk's end, the workgroup's
+// survivors side by side.  Every entry also gets its symbol count to the exit (cnt), so the true
+// path's counts follow from the composed entries without another walk (huf_count_kernel).
+#ifndef IE_HUF_SYNC
+#define IE_HUF_SYNC 64
+#endif
+constexpr uint32_t kHufSync = IE_HUF_SYNC;
+__global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* tab, uint16_t* cnt) {
     __shared__ uint16_t l1[1 << kHufL1];
+    __shared__ uint32_t P[kTPB], X[kTPB], R[kTPB + 1];  // boundary after the sync walk; exit; survivors
+    __shared__ uint16_t K2[kTPB];                      // a survivor's codes from P to its exit
     extern __shared__ uint32_t L[];  // the block's 16 chunks' bits (+ 64 for the last code)
-    huf_l1(a.lut, l1);               // (ends with a barrier)
     const int tid = threadIdx.x, kc = tid >> 4, d = tid & 15;
+    if (tid == 0) R[kTPB] = 0u;
+    huf_l1(a.lut, l1);               // (ends with a barrier)
     const int k0 = blockIdx.x * 16, k = k0 + kc;
     const uint32_t C = uint32_t(a.chunk_bits);
     const int m = min(16, a.nchunks - k0);
@@ -1082,22 +1012,135 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
     const uint32_t s0 = uint32_t(c0 - base);
     stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
     __syncthreads();
-    if (d >= kHufD || kc >= m) return;
+    const bool act = d < kHufD && kc < m;
     const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(s0) + uint64_t(m) * C));
-    const uint32_t ce = s0 + uint32_t(kc + 1) * C;
-    uint32_t p = s0 + uint32_t(kc) * C + uint32_t(d);
-    while (p < ce) {
-        if (p >= lim) {  // past the stream: the walk ends (the last chunk's exit is never used)
-            p = ce;
-            break;
-        }
+    const uint32_t cs = s0 + uint32_t(kc) * C, ce = cs + C;
+    // one step from p: the next position (a code at p: counted in *n); past the stream: the
+    // chunk's end e (the last chunk's exit is never used)
+    auto step = [&](uint32_t p, uint32_t e, uint32_t* n) -> uint32_t {
+        if (p >= lim) return e;
         const uint32_t p15 = lbits(L, p, 15);
-        uint32_t e = l1[p15 >> (15 - kHufL1)];
-        if (!e) e = a.lut[p15];
-        const uint32_t len = e >> 8;
-        p += len ? len : 1u;
+        uint32_t v = l1[p15 >> (15 - kHufL1)];
+        if (!v) v = a.lut[p15];
+        const uint32_t len = v >> 8;
+        *n += len ? 1u : 0u;
+        return p + (len ? len : 1u);
+    };
+    uint32_t p = cs + uint32_t(d), n1 = 0;
+    if (act) {
+        const uint32_t sync = min(cs + kHufSync, ce);
+        while (p < sync) p = step(p, ce, &n1);
+        p = min(p, ce);
     }
-    tab[size_t(k) * kHufD + d] = uint16_t(p - ce);
+    P[tid] = act ? p : 0xFFFFFFFFu;
+    __syncthreads();
+    // the first entry of the chunk standing on the same boundary leads; leaders still inside the
+    // chunk are the survivors
+    int lead = d;
+    if (act)
+        for (int j = 0; j < d; j++)
+            if (P[(kc << 4) + j] == p) {
+                lead = j;
+                break;
+            }
+    if (act && lead == d) {
+        if (p < ce) {
+            R[atomicAdd(&R[kTPB], 1u)] = uint32_t(tid);
+        } else {
+            X[tid] = p;
+            K2[tid] = 0;
+        }
+    }
+    __syncthreads();
+    const uint32_t nr = R[kTPB];
+    for (uint32_t r = tid; r < nr; r += kTPB) {
+        const uint32_t t = R[r], e = s0 + ((t >> 4) + 1u) * C;
+        uint32_t q = P[t], n2 = 0;
+        while (q < e) q = step(q, e, &n2);
+        X[t] = q;
+        K2[t] = uint16_t(n2);
+    }
+    __syncthreads();
+    if (!act) return;
+    const int lt = (kc << 4) + lead;
+    tab[size_t(k) * kHufD + d] = uint16_t(X[lt] - ce);
+    cnt[size_t(k) * kHufD + d] = uint16_t(n1 + K2[lt]);
+}
+
+// The true entry of every chunk through the composed tables, its symbol count from the table pass,
+// and the workgroup scan of the counts (base[k], wgsum[g]) -- no walk.
+__global__ __launch_bounds__(kTPB) void huf_count_kernel(HufArgs a, const uint16_t* cnt) {
+    __shared__ alignas(8) uint32_t scratch[8];
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t c = 0;
+    if (k < a.nchunks) {
+        const uint64_t cstart = a.start_bit + uint64_t(k) * a.chunk_bits;
+        int u = k;
+        for (int l = 0; l < a.levels; l++) u /= kHufG;
+        uint32_t x = a.E[u];
+        for (int l = a.levels - 1; l >= 0; l--) {
+            int ul = k;
+            for (int m = 0; m < l; m++) ul /= kHufG;
+            x = a.lvl[l][size_t(ul) * kHufD + x];
+        }
+        a.entry[k] = cstart + x;
+        c = cnt[size_t(k) * kHufD + x];
+        a.count[k] = c;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(c, scratch, &tot);
+    if (k < a.nchunks) a.base[k] = ex;
+    if (threadIdx.x == 0) a.wgsum[blockIdx.x] = tot;
+}
+
+// The emitting walk: every chunk again from its entry, over the workgroup's chunks' bits staged
+// in LDS (a step reads LDS, not the stream in memory: the walk is one dependent chain per lane,
+// and the ~800 waves of a 4K payload are too few to hide a memory round trip per code), its
+// symbols into LDS at the chunk's place in the workgroup's output, then the workgroup's output
+// copied out whole (consecutive lanes, consecutive bytes) -- a lane writing its own chunk's bytes
+// straight to memory touches 64 lines per store instruction.  A workgroup whose output exceeds the
+// buffer writes from the walk.  A position no code prefixes flags the stream (changed[1]).
+#ifndef IE_HUF_EMIT_LDS
+#define IE_HUF_EMIT_LDS 40960
+#endif
+__global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
+    __shared__ uint16_t l1[1 << kHufL1];
+    __shared__ alignas(8) uint32_t scratch[8];
+    __shared__ uint8_t sym[IE_HUF_EMIT_LDS > 0 ? IE_HUF_EMIT_LDS : 1];
+    extern __shared__ uint32_t L[];  // the workgroup's chunks' bits (+ 64 past the last)
+    const int tid = threadIdx.x;
+    const uint32_t C = uint32_t(a.chunk_bits);
+    const int k0 = blockIdx.x * kTPB, m = min(kTPB, a.nchunks - k0);
+    const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
+    const uint64_t base = c0 & ~31ull;
+    const uint32_t s0 = uint32_t(c0 - base);
+    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
+    huf_l1(a.lut, l1);  // (ends with a barrier: L staged too)
+    const uint64_t pre = huf_wg_prefix(a.wgsum, int(blockIdx.x), scratch);
+    const uint32_t tot = a.wgsum[blockIdx.x];
+    const bool staged = IE_HUF_EMIT_LDS > 0 && tot <= uint32_t(IE_HUF_EMIT_LDS);
+    const int k = k0 + tid;
+    if (tid < m) {
+        const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(s0) + uint64_t(m) * C));
+        const uint32_t e = s0 + uint32_t(tid + 1) * C;
+        uint32_t p = uint32_t(a.entry[k] - base), c = 0;
+        uint8_t* o = staged ? sym + a.base[k] : a.out + pre + a.base[k];
+        while (p < e && p < lim) {
+            const uint32_t p15 = lbits(L, p, 15);
+            uint32_t v = l1[p15 >> (15 - kHufL1)];
+            if (!v) v = a.lut[p15];
+            const uint32_t len = v >> 8;
+            if (!len) {
+                atomicOr(&a.changed[1], 1u);
+                break;
+            }
+            o[c++] = uint8_t(v);
+            p += len;
+        }
+    }
+    if (!staged) return;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += kTPB) a.out[pre + i] = sym[i];
 }
 
 int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
@@ -1122,16 +1165,18 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
     a.out = out;
     const dim3 g((nchunks + kTPB - 1) / kTPB), blk(kTPB);
     if (write) {
-        hipLaunchKernelGGL(huf_emit_kernel, g, blk, 0, s, a);
+        hipLaunchKernelGGL(huf_emit_kernel, g, blk, size_t(((uint64_t(kTPB) * chunk_bits + 95) >> 5) + 3) * 4, s, a);
         return 0;
     }
     const size_t lds = size_t(((16 * chunk_bits + 95) >> 5) + 3) * 4;
-    hipLaunchKernelGGL(huf_table_kernel, dim3((nchunks + 15) / 16), blk, lds, s, a, tab);
+    // the symbol counts after the composition's rows (compose_kernel rewrites the exit tables)
+    uint16_t* cnt = tab + compose_rows<kHufD, kHufG>(nchunks) * kHufD;
+    hipLaunchKernelGGL(huf_table_kernel, dim3((nchunks + 15) / 16), blk, lds, s, a, tab, cnt);
     const int levels = launch_compose<kHufD, kHufG>(tab, nchunks, E, ticket, a.lvl, s);
     if (levels < 0) return -1;
     a.levels = levels;
     a.E = E;
-    hipLaunchKernelGGL(huf_walk_kernel, g, blk, 0, s, a);
+    hipLaunchKernelGGL(huf_count_kernel, g, blk, 0, s, a, cnt);
     hipLaunchKernelGGL(huf_total_kernel, dim3(1), blk, 0, s, a.wgsum, int(g.x), total);
     return levels;
 }
@@ -1139,7 +1184,7 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
 size_t huffman_table_rows(uint64_t nbits, uint64_t start_bit, uint64_t chunk_bits) {
     const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
     const int nchunks = int((span + chunk_bits - 1) / chunk_bits);
-    return nchunks ? compose_rows<kHufD, kHufG>(nchunks) * kHufD : 0;
+    return nchunks ? (compose_rows<kHufD, kHufG>(nchunks) + size_t(nchunks)) * kHufD : 0;  // (+ the counts)
 }
 
 }  // namespace ie

@@ -20,6 +20,10 @@
 
 namespace ie {
 
+#ifndef IE_PACK_WAVES  // pack_kernel's minimum waves per SIMD (launch bound; 1: the compiler's choice)
+#define IE_PACK_WAVES 1
+#endif
+
 constexpr int kHistTile = kTPB * 16;  // bytes per workgroup pass
 constexpr int kHistLoads = 4;          // hist_body: 16-byte loads per thread in flight
 
@@ -279,7 +283,7 @@ void launch_hist_batch(const uint8_t* in, uint64_t pitch, const uint64_t* n, uin
 // so short-code tables leave room for more resident tiles.
 __host__ __device__ constexpr int pack_image_words(int bpt, int maxlen) { return kTPB * bpt * maxlen / 32 + 4; }
 template <int BPT, int MAXLEN>
-__global__ __launch_bounds__(kTPB) void pack_kernel(PackArgs a) {
+__global__ __launch_bounds__(kTPB, IE_PACK_WAVES) void pack_kernel(PackArgs a) {
     extern __shared__ uint32_t smem[];  // [pack_image_words(BPT, a.maxlen)] image, [32] misc
     __shared__ uint32_t s_code[256];
     __shared__ uint8_t s_len[256];
