@@ -2408,15 +2408,24 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
     if (start_bit > uint64_t(len) * 8) return fail(c, IE_EINVAL, "start_bit beyond the stream");
     HIPCHK(c, hipSetDevice(c->device));
     int r;
-    const size_t padded = (len + 3) / 4 * 4 + 16;  // two zero words past the end for the bit reader
-    if ((r = ensure(c, c->d_dec, c->cap_dec, padded))) return r;
-    HIPCHK(c, hipMemsetAsync(c->d_dec + (len / 4) * 4, 0, padded - (len / 4) * 4, c->stream));
-    if (len)
-        HIPCHK(c, hipMemcpyAsync(c->d_dec, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                                 c->stream));
-    if ((r = ensure(c, c->d_hlut, c->cap_hlut, size_t(32768)))) return r;
-    HIPCHK(c, hipMemcpyAsync(c->d_hlut, lut, 32768 * sizeof(uint16_t),
-                             is_device_ptr(lut) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    // the kernels read the stream only through their LDS staging, which stops at its last byte: a
+    // 4-byte-aligned device stream is read in place, and a device table too (no copies)
+    const uint8_t* src = in;
+    if (!is_device_ptr(in) || reinterpret_cast<uintptr_t>(in) % 4) {
+        const size_t padded = (len + 3) / 4 * 4 + 16;
+        if ((r = ensure(c, c->d_dec, c->cap_dec, padded))) return r;
+        if (len)
+            HIPCHK(c, hipMemcpyAsync(c->d_dec, in, len, is_device_ptr(in) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                     c->stream));
+        src = c->d_dec;
+    }
+    const uint16_t* dlut = lut;
+    if (!is_device_ptr(lut) || reinterpret_cast<uintptr_t>(lut) % 2) {
+        if ((r = ensure(c, c->d_hlut, c->cap_hlut, size_t(32768)))) return r;
+        HIPCHK(c, hipMemcpyAsync(c->d_hlut, lut, 32768 * sizeof(uint16_t),
+                                 is_device_ptr(lut) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+        dlut = c->d_hlut;
+    }
     const uint64_t nbits = uint64_t(len) * 8;
     // walk chunk of the Huffman decode; IE_HUF_CHUNK overrides (tuning aid).  1024 bits measured
     // best on a 4K payload (tools/gpu_huf_chunk.sh: 0.30-0.32 ms against 0.34 at 512, 0.37 at 768
@@ -2436,12 +2445,26 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
     uint32_t* E = reinterpret_cast<uint32_t*>(wk + 2 * cap);
     unsigned* ticket = reinterpret_cast<unsigned*>(c->d_misc + 5);
     HIPCHK(c, hipMemsetAsync(c->d_misc, 0, 6 * sizeof(uint64_t), c->stream));
-    const uint32_t* W = reinterpret_cast<const uint32_t*>(c->d_dec);
-    const int rounds = ie::huffman_decode_device(W, nbits, start_bit, c->d_hlut, chunk_bits, wk, c->d_rtab, E, ticket,
+    const uint32_t* W = reinterpret_cast<const uint32_t*>(src);
+    const int rounds = ie::huffman_decode_device(W, nbits, start_bit, dlut, chunk_bits, wk, c->d_rtab, E, ticket,
                                                  c->d_count, wk + cap, flags, c->d_misc + 2, nullptr, false,
                                                  c->stream);
     if (rounds < 0) return fail(c, IE_EHIP, "Huffman decode walk failed");
     HIPCHK(c, hipGetLastError());
+    if (is_device_ptr(out)) {
+        // device output: the emit follows at once, bounded by out_cap (a symbol past it is not
+        // written and flags the launch), and the total and flags come back in ONE read
+        ie::huffman_decode_device(W, nbits, start_bit, dlut, chunk_bits, wk, c->d_rtab, E, ticket, c->d_count,
+                                  wk + cap, flags, c->d_misc + 2, out, true, c->stream, uint64_t(out_cap));
+        HIPCHK(c, hipGetLastError());
+        uint64_t rb[2] = {0, 0};  // d_misc[1]: the two flag words, d_misc[2]: the total
+        HIPCHK(c, hipMemcpyAsync(rb, c->d_misc + 1, sizeof(rb), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        *nout = size_t(rb[1]);
+        if (uint32_t(rb[0] >> 32)) return fail(c, IE_EFORMAT, "Huffman stream holds a bit string no code prefixes");
+        if (rb[1] > out_cap) return fail(c, IE_ECAP, "output capacity below the decoded symbol count");
+        return IE_OK;
+    }
     uint64_t total = 0;
     HIPCHK(c, hipMemcpyAsync(&total, c->d_misc + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2453,7 +2476,7 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
         if ((r = ensure(c, c->d_hout, c->cap_hout, size_t(total) + 1))) return r;
         dout = c->d_hout;
     }
-    ie::huffman_decode_device(W, nbits, start_bit, c->d_hlut, chunk_bits, wk, c->d_rtab, E, ticket, c->d_count,
+    ie::huffman_decode_device(W, nbits, start_bit, dlut, chunk_bits, wk, c->d_rtab, E, ticket, c->d_count,
                               wk + cap, flags, c->d_misc + 2, dout, true, c->stream);
     HIPCHK(c, hipGetLastError());
     unsigned f[2] = {0, 0};

@@ -67,18 +67,29 @@ struct HufArgs {
     uint64_t* entry;
     uint32_t* count;
     uint32_t* wgsum;    // [walk workgroups] their chunks' symbol totals
-    unsigned* changed;  // [1] invalid code on the emitting walk
+    unsigned* changed;  // [1] invalid code on the emitting walk; [0] output past out_cap (not written)
     uint64_t* base;     // symbols before each chunk within its walk workgroup
     uint8_t* out;
     uint16_t* lvl[kRecMaxLevels];  // mode 2: the composition's levels
     int levels;
     const uint32_t* E;
+    uint64_t out_cap;   // bytes of out (the emit launched before the total is known checks it)
 };
 
 __device__ __forceinline__ void huf_l1(const uint16_t* lut, uint16_t* l1) {
-    for (int q = threadIdx.x; q < (1 << kHufL1); q += blockDim.x) {
-        const uint16_t e = lut[uint32_t(q) << (15 - kHufL1)];
-        l1[q] = ((e >> 8) != 0 && (e >> 8) <= kHufL1) ? e : uint16_t(0);  // 0: look in lut
+    constexpr int B = 8;  // loads in flight per thread
+    for (int q0 = 0; q0 < (1 << kHufL1); q0 += B * int(blockDim.x)) {
+        uint16_t e[B];
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const int q = q0 + u * int(blockDim.x) + int(threadIdx.x);
+            e[u] = q < (1 << kHufL1) ? lut[uint32_t(q) << (15 - kHufL1)] : uint16_t(0);
+        }
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const int q = q0 + u * int(blockDim.x) + int(threadIdx.x);
+            if (q < (1 << kHufL1)) l1[q] = ((e[u] >> 8) != 0 && (e[u] >> 8) <= kHufL1) ? e[u] : uint16_t(0);  // 0: look in lut
+        }
     }
     __syncthreads();
 }
@@ -188,8 +199,58 @@ __device__ __forceinline__ uint32_t tail_word(uint32_t raw, uint64_t w, uint64_t
 __device__ __forceinline__ void stage_words(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nbits,
                                             int tid, int nthreads) {
     const uint64_t nwords = (nbits + 31) >> 5;
-    for (int i = tid; i < nw; i += nthreads)
-        L[i] = (w0 + i < nwords) ? tail_word(__builtin_nontemporal_load(W + w0 + i), w0 + i, nbits) : 0u;
+    constexpr int B = 8;  // loads in flight per thread (one round trip per B * nthreads words)
+    for (int i0 = 0; i0 < nw; i0 += B * nthreads) {
+        uint32_t v[B];
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const int i = i0 + u * nthreads + tid;
+            v[u] = (i < nw && w0 + i < nwords) ? __builtin_nontemporal_load(W + w0 + i) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const int i = i0 + u * nthreads + tid;
+            if (i < nw) L[i] = (w0 + i < nwords) ? tail_word(v[u], w0 + i, nbits) : 0u;
+        }
+    }
+}
+
+// stage_words with one pad word after every 32 (word i at i + i / 32): lanes walking chunks of
+// 1 024 bits side by side read words 32 apart -- one bank -- without it (lbits_pad reads it)
+__device__ __forceinline__ void stage_words_pad(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nbits,
+                                                int tid, int nthreads) {
+    const uint64_t nwords = (nbits + 31) >> 5;
+    constexpr int B = 8;
+    for (int i0 = 0; i0 < nw; i0 += B * nthreads) {
+        uint32_t v[B];
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const int i = i0 + u * nthreads + tid;
+            const uint64_t w = w0 + i;
+            if (i < nw && (w + 1) * 32 <= nbits) {
+                v[u] = __builtin_nontemporal_load(W + w);
+            } else if (i < nw && w < nwords) {  // the stream's last, partial word: its bytes only (the
+                                                // caller's buffer may end there)
+                const uint8_t* b = reinterpret_cast<const uint8_t*>(W + w);
+                uint32_t x = 0;
+                for (uint32_t e = 0; e < 4u && 32 * w + 8 * e < nbits; e++) x |= uint32_t(b[e]) << (8 * e);
+                v[u] = x;
+            } else {
+                v[u] = 0u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const int i = i0 + u * nthreads + tid;
+            if (i < nw) L[i + (i >> 5)] = (w0 + i < nwords) ? tail_word(v[u], w0 + i, nbits) : 0u;
+        }
+    }
+}
+__host__ __device__ constexpr int pad_words(int nw) { return nw + (nw >> 5) + 1; }
+__device__ __forceinline__ uint32_t lbits_pad(const uint32_t* L, uint32_t p, int l) {
+    const uint32_t w = p >> 5, w1 = w + 1u, s = p & 31u;
+    const uint64_t v = (uint64_t(L[w + (w >> 5)]) << 32) | L[w1 + (w1 >> 5)];
+    return l ? uint32_t((v << s) >> (64 - l)) : 0u;
 }
 
 // zig-zag rank of every coefficient position (the inverse of kZZ4 / kZZ8)
@@ -1010,7 +1071,7 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
     const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
     const uint32_t s0 = uint32_t(c0 - base);
-    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
+    stage_words_pad(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
     __syncthreads();
     const bool act = d < kHufD && kc < m;
     const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(s0) + uint64_t(m) * C));
@@ -1019,7 +1080,7 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
     // chunk's end e (the last chunk's exit is never used)
     auto step = [&](uint32_t p, uint32_t e, uint32_t* n) -> uint32_t {
         if (p >= lim) return e;
-        const uint32_t p15 = lbits(L, p, 15);
+        const uint32_t p15 = lbits_pad(L, p, 15);
         uint32_t v = l1[p15 >> (15 - kHufL1)];
         if (!v) v = a.lut[p15];
         const uint32_t len = v >> 8;
@@ -1114,7 +1175,7 @@ __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
     const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
     const uint32_t s0 = uint32_t(c0 - base);
-    stage_words(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
+    stage_words_pad(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
     huf_l1(a.lut, l1);  // (ends with a barrier: L staged too)
     const uint64_t pre = huf_wg_prefix(a.wgsum, int(blockIdx.x), scratch);
     const uint32_t tot = a.wgsum[blockIdx.x];
@@ -1124,14 +1185,20 @@ __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
         const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(s0) + uint64_t(m) * C));
         const uint32_t e = s0 + uint32_t(tid + 1) * C;
         uint32_t p = uint32_t(a.entry[k] - base), c = 0;
-        uint8_t* o = staged ? sym + a.base[k] : a.out + pre + a.base[k];
+        const uint64_t at = pre + a.base[k];
+        uint8_t* o = staged ? sym + a.base[k] : a.out + at;
+        const uint64_t room = staged ? ~0ull : (a.out_cap > at ? a.out_cap - at : 0ull);
         while (p < e && p < lim) {
-            const uint32_t p15 = lbits(L, p, 15);
+            const uint32_t p15 = lbits_pad(L, p, 15);
             uint32_t v = l1[p15 >> (15 - kHufL1)];
             if (!v) v = a.lut[p15];
             const uint32_t len = v >> 8;
             if (!len) {
                 atomicOr(&a.changed[1], 1u);
+                break;
+            }
+            if (c >= room) {
+                atomicOr(&a.changed[0], 1u);
                 break;
             }
             o[c++] = uint8_t(v);
@@ -1140,13 +1207,14 @@ __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
     }
     if (!staged) return;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < tot; i += kTPB) a.out[pre + i] = sym[i];
+    if (pre + tot > a.out_cap && threadIdx.x == 0) atomicOr(&a.changed[0], 1u);
+    for (uint32_t i = threadIdx.x; i < tot && pre + i < a.out_cap; i += kTPB) a.out[pre + i] = sym[i];
 }
 
 int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
                           uint64_t chunk_bits, uint64_t* entry, uint16_t* tab, uint32_t* E, unsigned* ticket,
                           uint32_t* count, uint64_t* base, unsigned* changed, uint64_t* total, uint8_t* out,
-                          bool write, hipStream_t s) {
+                          bool write, hipStream_t s, uint64_t out_cap) {
     const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
     const int nchunks = int((span + chunk_bits - 1) / chunk_bits);
     if (nchunks == 0) return 0;
@@ -1163,12 +1231,13 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
     a.changed = changed;
     a.base = base;
     a.out = out;
+    a.out_cap = out_cap;
     const dim3 g((nchunks + kTPB - 1) / kTPB), blk(kTPB);
     if (write) {
-        hipLaunchKernelGGL(huf_emit_kernel, g, blk, size_t(((uint64_t(kTPB) * chunk_bits + 95) >> 5) + 3) * 4, s, a);
+        hipLaunchKernelGGL(huf_emit_kernel, g, blk, size_t(pad_words(int(((uint64_t(kTPB) * chunk_bits + 95) >> 5) + 3))) * 4, s, a);
         return 0;
     }
-    const size_t lds = size_t(((16 * chunk_bits + 95) >> 5) + 3) * 4;
+    const size_t lds = size_t(pad_words(int(((16 * chunk_bits + 95) >> 5) + 3))) * 4;
     // the symbol counts after the composition's rows (compose_kernel rewrites the exit tables)
     uint16_t* cnt = tab + compose_rows<kHufD, kHufG>(nchunks) * kHufD;
     hipLaunchKernelGGL(huf_table_kernel, dim3((nchunks + 15) / 16), blk, lds, s, a, tab, cnt);

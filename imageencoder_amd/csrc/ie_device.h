@@ -271,7 +271,7 @@ void launch_rec_spec_decode(const RecParseArgs& a, const DecArgs& d, int n, hipS
 int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
                           uint64_t chunk_bits, uint64_t* entry, uint16_t* tab, uint32_t* E, unsigned* ticket,
                           uint32_t* count, uint64_t* base, unsigned* changed, uint64_t* total, uint8_t* out,
-                          bool write, hipStream_t s);
+                          bool write, hipStream_t s, uint64_t out_cap = ~0ull);
 size_t huffman_table_rows(uint64_t nbits, uint64_t start_bit, uint64_t chunk_bits);
 
 // P-frame of a gop > 1 video (ie_pframe.hip): one launch sequence per frame, chained on the device.

@@ -634,3 +634,36 @@ def test_decode_speculative_warm(codec, n, warm):
     e_e = c.decode_frames(dev, w, h, pix_e, length=length)
     assert e_s == e_e == end
     assert torch.equal(pix_s, pix_e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("short", [0, 1, 777])
+def test_huffman_decode_device_output(codec, short):
+    """ie_huffman_decode with device stream, table and output (one read-back: the emit runs before
+    the symbol count is known and is bounded by the output's size): the symbols (the walk runs to
+    the buffer's end, the last byte's padding bits included, as the reference's does); an output
+    `short` bytes below the count raises IE_ECAP and leaves the bytes past it untouched."""
+    import torch
+    from imageencoder_amd import IE_ECAP, IEError
+    rng = np.random.default_rng(9)
+    data = np.minimum(rng.geometric(0.25, 300_000), 24).astype(np.uint8)  # skewed, codes <= 15 bits
+    enc = codec.huffman_encode(data)
+    lut, sb = codec.huffman_table(enc)
+    d_enc = torch.from_numpy(np.frombuffer(enc, np.uint8).copy()).cuda()
+    d_lut = torch.from_numpy(lut.view(np.int16).copy()).cuda()
+    guard = 4096
+    out = torch.full((data.size + guard,), 0xA5, dtype=torch.uint8, device="cuda")
+    n = codec.huffman_decode_device(d_enc, len(enc), d_lut, sb, out)
+    host = out.cpu().numpy()
+    assert data.size <= n < data.size + 8
+    np.testing.assert_array_equal(host[: data.size], data)
+    assert (host[n:] == 0xA5).all()
+    if short:
+        full = host[:n].copy()
+        out.fill_(0xA5)
+        with pytest.raises(IEError) as e:
+            codec.huffman_decode_device(d_enc, len(enc), d_lut, sb, out[: n - short])
+        assert e.value.code == IE_ECAP
+        host = out.cpu().numpy()
+        assert (host[n - short:] == 0xA5).all()
+        np.testing.assert_array_equal(host[: n - short], full[: n - short])
