@@ -1042,7 +1042,7 @@ void launch_rec_spec_decode(const RecParseArgs& a, const DecArgs& d, int n, hipS
 // A code is at most 15 bits long, so the first code that starts at or after a chunk's first bit
 // sits at an offset d < 15: a chunk of the Huffman stream is a function of d exactly like a chunk
 // of the record stream, with 15 entries instead of D.  huf_table_kernel walks all 15 entries of
-// 16 chunks per workgroup (one lane each, the chunks' bits staged in LDS; a position where no code
+// kHufTC chunks per workgroup (the chunks' bits staged in LDS; a position where no code
 // starts slides one bit -- never on the true path of a valid stream); compose_kernel composes the
 // tables; huf_count_kernel reads each chunk's symbol count at its true entry, and huf_emit_kernel
 // writes the symbols.  Exact for any content: a periodic stream (e.g. a
@@ -1057,25 +1057,28 @@ void launch_rec_spec_decode(const RecParseArgs& a, const DecArgs& d, int n, hipS
 #define IE_HUF_SYNC 64
 #endif
 constexpr uint32_t kHufSync = IE_HUF_SYNC;
+#ifndef IE_HUF_TC
+#define IE_HUF_TC 64
+#endif
+constexpr int kHufTC = IE_HUF_TC;  // chunks per table workgroup: its survivors fill a wave
 __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* tab, uint16_t* cnt) {
+    constexpr int S = kHufTC * 16, U = S / kTPB;  // walk slots (chunk, entry); slots per thread
+    static_assert(S % kTPB == 0, "whole slots per thread");
     __shared__ uint16_t l1[1 << kHufL1];
-    __shared__ uint32_t P[kTPB], X[kTPB], R[kTPB + 1];  // boundary after the sync walk; exit; survivors
-    __shared__ uint16_t K2[kTPB];                      // a survivor's codes from P to its exit
-    extern __shared__ uint32_t L[];  // the block's 16 chunks' bits (+ 64 for the last code)
-    const int tid = threadIdx.x, kc = tid >> 4, d = tid & 15;
-    if (tid == 0) R[kTPB] = 0u;
-    huf_l1(a.lut, l1);               // (ends with a barrier)
-    const int k0 = blockIdx.x * 16, k = k0 + kc;
+    __shared__ uint32_t P[S], X[S], R[S + 1];  // boundary after the sync walk; exit; survivors
+    __shared__ uint16_t K2[S];                 // a survivor's codes from P to its exit
+    extern __shared__ uint32_t L[];            // the workgroup's chunks' bits (+ 64 past the last)
+    const int tid = threadIdx.x;
+    if (tid == 0) R[S] = 0u;
+    const int k0 = blockIdx.x * kHufTC;
     const uint32_t C = uint32_t(a.chunk_bits);
-    const int m = min(16, a.nchunks - k0);
+    const int m = min(kHufTC, a.nchunks - k0);
     const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
     const uint32_t s0 = uint32_t(c0 - base);
     stage_words_pad(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
-    __syncthreads();
-    const bool act = d < kHufD && kc < m;
+    huf_l1(a.lut, l1);  // (ends with a barrier: L staged too)
     const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(s0) + uint64_t(m) * C));
-    const uint32_t cs = s0 + uint32_t(kc) * C, ce = cs + C;
     // one step from p: the next position (a code at p: counted in *n); past the stream: the
     // chunk's end e (the last chunk's exit is never used)
     auto step = [&](uint32_t p, uint32_t e, uint32_t* n) -> uint32_t {
@@ -1087,33 +1090,63 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
         *n += len ? 1u : 0u;
         return p + (len ? len : 1u);
     };
-    uint32_t p = cs + uint32_t(d), n1 = 0;
-    if (act) {
-        const uint32_t sync = min(cs + kHufSync, ce);
-        while (p < sync) p = step(p, ce, &n1);
-        p = min(p, ce);
+    // slot u of this thread: s = u kTPB + tid, chunk s / 16, entry s % 16 (15: none)
+    auto kc_of = [&](int u) { return (u * kTPB + tid) >> 4; };
+    const int d = tid & 15;
+    uint32_t p[U], n1[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        p[u] = s0 + uint32_t(kc_of(u)) * C + uint32_t(d);
+        n1[u] = 0;
     }
-    P[tid] = act ? p : 0xFFFFFFFFu;
+    // the sync walks, the thread's U slots interleaved (independent chains: their LDS reads overlap)
+    for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int kc = kc_of(u);
+            const uint32_t cs = s0 + uint32_t(kc) * C, ce = cs + C;
+            if (d < kHufD && kc < m && p[u] < min(cs + kHufSync, ce)) {
+                p[u] = step(p[u], ce, &n1[u]);
+                any = true;
+            }
+        }
+        if (!any) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int kc = kc_of(u);
+        const bool act = d < kHufD && kc < m;
+        p[u] = min(p[u], s0 + uint32_t(kc + 1) * C);
+        P[u * kTPB + tid] = act ? p[u] : 0xFFFFFFFFu;
+    }
     __syncthreads();
     // the first entry of the chunk standing on the same boundary leads; leaders still inside the
     // chunk are the survivors
-    int lead = d;
-    if (act)
-        for (int j = 0; j < d; j++)
-            if (P[(kc << 4) + j] == p) {
-                lead = j;
-                break;
+    int lead[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int kc = kc_of(u), sl = u * kTPB + tid;
+        const uint32_t ce = s0 + uint32_t(kc + 1) * C;
+        lead[u] = d;
+        if (d < kHufD && kc < m) {
+            for (int j = 0; j < d; j++)
+                if (P[(kc << 4) + j] == p[u]) {
+                    lead[u] = j;
+                    break;
+                }
+            if (lead[u] == d) {
+                if (p[u] < ce) {
+                    R[atomicAdd(&R[S], 1u)] = uint32_t(sl);
+                } else {
+                    X[sl] = p[u];
+                    K2[sl] = 0;
+                }
             }
-    if (act && lead == d) {
-        if (p < ce) {
-            R[atomicAdd(&R[kTPB], 1u)] = uint32_t(tid);
-        } else {
-            X[tid] = p;
-            K2[tid] = 0;
         }
     }
     __syncthreads();
-    const uint32_t nr = R[kTPB];
+    const uint32_t nr = R[S];
     for (uint32_t r = tid; r < nr; r += kTPB) {
         const uint32_t t = R[r], e = s0 + ((t >> 4) + 1u) * C;
         uint32_t q = P[t], n2 = 0;
@@ -1122,10 +1155,15 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
         K2[t] = uint16_t(n2);
     }
     __syncthreads();
-    if (!act) return;
-    const int lt = (kc << 4) + lead;
-    tab[size_t(k) * kHufD + d] = uint16_t(X[lt] - ce);
-    cnt[size_t(k) * kHufD + d] = uint16_t(n1 + K2[lt]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int kc = kc_of(u);
+        if (d >= kHufD || kc >= m) continue;
+        const uint32_t ce = s0 + uint32_t(kc + 1) * C;
+        const int lt = (kc << 4) + lead[u], k = k0 + kc;
+        tab[size_t(k) * kHufD + d] = uint16_t(X[lt] - ce);
+        cnt[size_t(k) * kHufD + d] = uint16_t(n1[u] + K2[lt]);
+    }
 }
 
 // The true entry of every chunk through the composed tables, its symbol count from the table pass,
@@ -1237,10 +1275,10 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
         hipLaunchKernelGGL(huf_emit_kernel, g, blk, size_t(pad_words(int(((uint64_t(kTPB) * chunk_bits + 95) >> 5) + 3))) * 4, s, a);
         return 0;
     }
-    const size_t lds = size_t(pad_words(int(((16 * chunk_bits + 95) >> 5) + 3))) * 4;
+    const size_t lds = size_t(pad_words(int(((uint64_t(kHufTC) * chunk_bits + 95) >> 5) + 3))) * 4;
     // the symbol counts after the composition's rows (compose_kernel rewrites the exit tables)
     uint16_t* cnt = tab + compose_rows<kHufD, kHufG>(nchunks) * kHufD;
-    hipLaunchKernelGGL(huf_table_kernel, dim3((nchunks + 15) / 16), blk, lds, s, a, tab, cnt);
+    hipLaunchKernelGGL(huf_table_kernel, dim3((nchunks + kHufTC - 1) / kHufTC), blk, lds, s, a, tab, cnt);
     const int levels = launch_compose<kHufD, kHufG>(tab, nchunks, E, ticket, a.lvl, s);
     if (levels < 0) return -1;
     a.levels = levels;
