@@ -375,7 +375,7 @@ def main():
             t_cnt = g3 / args.steps
             # the roofline prices the launch the step runs (the counting encoder); the plain encoder
             # (same kernel without the byte counts) is reported beside it
-            extra["plain_encode"] = {"kernel": "encode4w_kernel<false>", "launch_us": round(enc_s * 1e6, 2),
+            extra["plain_encode"] = {"kernel": "encode4p_kernel<false, 4>", "launch_us": round(enc_s * 1e6, 2),
                                      "frac": round((B * w * h + out_bytes_per_launch) / enc_s / 1e9 / HBM_PEAK_GBS, 4)}
             enc_s = t_cnt
             extra["huffman_roofline"] = {

@@ -30,9 +30,11 @@ if len(rt):  # chip-wide 100 MHz clock: starts and ends across the launch
     en = (rt[:, 1] - rt[:, 0].min()) / 100.0
     print(f"launch span {en.max():.2f} us: wave starts p50 {np.median(st):.2f} p90 {np.percentile(st, 90):.2f} "
           f"max {st.max():.2f}; ends p50 {np.median(en):.2f} p90 {np.percentile(en, 90):.2f}")
-fx = w16.reshape(-1, 16)[:, [2, 11, 12, 13, 3]]
-fx = fx[(fx > 0).all(axis=1)]
-if len(fx):
-    dd = np.diff(fx, axis=1) / ghz / 1e3
-    print(f"fix-up split ({len(fx)} waves): tasks+barrier {dd[:, 0].mean():.3f}  eval {dd[:, 1].mean():.3f}  "
-          f"barrier {dd[:, 2].mean():.3f}  patch {dd[:, 3].mean():.3f} us")
+# encode4p_kernel's prologue on the 100 MHz clock (words 13 entry, 12 own loads landed, 11 past
+# the first barrier, 14 the tile's start; tools/conc.py reads the same words)
+pr = w16.reshape(-1, 16)[:, [13, 12, 11, 14]]
+pr = pr[(pr > 0).all(axis=1)]
+if len(pr):
+    dd = np.diff(pr, axis=1) / 100.0
+    print(f"prologue ({len(pr)} waves): entry -> loads landed {dd[:, 0].mean():.2f}, -> past the barrier "
+          f"{dd[:, 1].mean():.2f}, -> tile start {dd[:, 2].mean():.2f} us")
