@@ -216,6 +216,11 @@ int ie_huffman_hist_batch_ends(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, 
  * complete and copies out count*256 counts and first positions.  While the host builds the trees
  * of batch i (between _wait and ie_huffman_pack_batch), the device runs batch i+1's encode and
  * histogram.  Same reference interface as ie_huffman_hist_batch (Huffman.cpp:237-243). */
+/* After ie_encode_images_counted over the same batch, _async is ONE launch that takes the
+ * encoder's counts (and clears them for the next counted encode) and writes counts and first
+ * positions straight into the pinned slot; a string with a value first seen past its first
+ * 256 KiB is finished by _wait, so `in` must stay unchanged until _wait returns (the pack that
+ * follows reads it anyway). */
 int ie_huffman_hist_batch_ends_async(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const uint64_t* end_bits,
                                      int count, int slot);
 int ie_huffman_hist_batch_wait(ie_ctx* ctx, int slot, uint32_t* hist, uint64_t* first_pos);
@@ -251,7 +256,10 @@ int ie_bitcopy(ie_ctx* ctx, const uint8_t* bytes, size_t n, uint8_t* out, size_t
  * (host or device): 32768 uint16 entries, lut[p] = sym | len << 8 for the code that prefixes the
  * 15-bit string p (len 0: none; codes are <= 15 bits, Huffman.cpp:41-42), built by the caller from
  * the dictionary.  out (host or device, out_cap bytes) receives the symbols; *nout their count
- * (also when IE_ECAP is returned).  IE_EFORMAT: a bit string that no code prefixes. */
+ * (also when IE_ECAP is returned).  IE_EFORMAT: a bit string that no code prefixes.  A device
+ * stream (4-byte aligned) and a device lut are read in place, not copied; with a device out the
+ * symbols are written as they are decoded, never past out_cap (on IE_ECAP the first out_cap
+ * symbols are there), and the call synchronises once. */
 /* The dictionary half of Huffman<uint8_t>::decode (buildTree, Huffman.cpp:120-173): parse the
  * dictionary of a Huffman-coded stream from bit start_bit of `in` (host memory, len bytes) into
  * ie_huffman_decode's prefix table lut (32768 entries); *code_start = the bit after its stop bit.
