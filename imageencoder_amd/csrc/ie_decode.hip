@@ -195,27 +195,8 @@ __device__ __forceinline__ uint32_t tail_word(uint32_t raw, uint64_t w, uint64_t
     return vb >= 32 ? b : (b & ~(0xFFFFFFFFu >> uint32_t(vb)));
 }
 
-// words [w0, w0 + nw) of the stream, byte-swapped to MSB-first, zeros past the stream's nbits
-__device__ __forceinline__ void stage_words(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nbits,
-                                            int tid, int nthreads) {
-    const uint64_t nwords = (nbits + 31) >> 5;
-    constexpr int B = 8;  // loads in flight per thread (one round trip per B * nthreads words)
-    for (int i0 = 0; i0 < nw; i0 += B * nthreads) {
-        uint32_t v[B];
-#pragma unroll
-        for (int u = 0; u < B; u++) {
-            const int i = i0 + u * nthreads + tid;
-            v[u] = (i < nw && w0 + i < nwords) ? __builtin_nontemporal_load(W + w0 + i) : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < B; u++) {
-            const int i = i0 + u * nthreads + tid;
-            if (i < nw) L[i] = (w0 + i < nwords) ? tail_word(v[u], w0 + i, nbits) : 0u;
-        }
-    }
-}
-
-// stage_words with one pad word after every 32 (word i at i + i / 32): lanes walking chunks of
+// Words [w0, w0 + nw) of the stream, byte-swapped to MSB-first, zeros past the stream's nbits,
+// with one pad word after every 32 (word i at i + i / 32): lanes walking chunks of
 // 1 024 bits side by side read words 32 apart -- one bank -- without it (lbits_pad reads it)
 __device__ __forceinline__ void stage_words_pad(uint32_t* L, const uint32_t* W, uint64_t w0, int nw, uint64_t nbits,
                                                 int tid, int nthreads) {

@@ -1975,7 +1975,6 @@ __device__ __forceinline__ void boundary_finish(uint32_t* out, uint64_t word, ui
     if (uint32_t(old >> 56) == tag && uint32_t((old >> 48) & 0xFFu) == 3u - role) out[word] = bswap32(part | uint32_t(old));
 }
 
-constexpr int kPMisc = 64;  // two copies of encode4w_kernel's 32 misc words
 constexpr int kPWfrag = 256;  // the matrix-pipe A fragments [64 lanes][4 words]
 // encode4p_kernel's misc words per copy by waves per tile: [0, WPT) wave bit counts, H the waves'
 // head words, E the tile's exclusive prefix (2), PT the tail before the chain start, PD the pending
@@ -1990,7 +1989,6 @@ template <int WPT> struct PMisc {
 template <int WPT> constexpr int p_lds_bytes() {
     return (WPT * 4 * 64 * (16 / WPT) + WPT * kWTask + 2 * PMisc<WPT>::S + kPWfrag) * 4 + kWRows * 8;
 }
-constexpr int kPLdsBytes = (4 * kWReg + 4 * kWTask + kPMisc + kPWfrag) * 4 + kWRows * 8;
 
 typedef int v4i32 __attribute__((ext_vector_type(4)));
 typedef int v16i32 __attribute__((ext_vector_type(16)));
@@ -2986,11 +2984,10 @@ __global__ __launch_bounds__(256, IE_Q_PER_CU) void encode4q_kernel(EncArgs a_, 
         }
         lds_barrier();  // ---- the tile's position
         QSTAMP(6);
-        uint32_t W = 0, A = 0;
+        uint32_t W = 0;
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             const uint32_t v = __builtin_amdgcn_readfirstlane(bm[w]);
-            A += v;
             W += (w < wv) ? v : 0u;
         }
         const uint32_t bTw = __builtin_amdgcn_readfirstlane(bm[wv]);
