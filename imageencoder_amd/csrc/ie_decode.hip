@@ -1042,12 +1042,15 @@ constexpr uint32_t kHufSync = IE_HUF_SYNC;
 #define IE_HUF_TC 64
 #endif
 constexpr int kHufTC = IE_HUF_TC;  // chunks per table workgroup: its survivors fill a wave
-__global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* tab, uint16_t* cnt) {
+__global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* tab, uint16_t* cnt, uint16_t* mo,
+                                                          uint16_t* mc) {
     constexpr int S = kHufTC * 16, U = S / kTPB;  // walk slots (chunk, entry); slots per thread
     static_assert(S % kTPB == 0, "whole slots per thread");
     __shared__ uint16_t l1[1 << kHufL1];
     __shared__ uint32_t P[S], X[S], R[S + 1];  // boundary after the sync walk; exit; survivors
     __shared__ uint16_t K2[S];                 // a survivor's codes from P to its exit
+    __shared__ uint32_t M[S];                  // its first boundary at or past the chunk's middle
+    __shared__ uint16_t KM[S];                 // its codes from P to that boundary
     extern __shared__ uint32_t L[];            // the workgroup's chunks' bits (+ 64 past the last)
     const int tid = threadIdx.x;
     if (tid == 0) R[S] = 0u;
@@ -1122,6 +1125,8 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
                 } else {
                     X[sl] = p[u];
                     K2[sl] = 0;
+                    M[sl] = p[u];
+                    KM[sl] = 0;
                 }
             }
         }
@@ -1129,8 +1134,11 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
     __syncthreads();
     const uint32_t nr = R[S];
     for (uint32_t r = tid; r < nr; r += kTPB) {
-        const uint32_t t = R[r], e = s0 + ((t >> 4) + 1u) * C;
+        const uint32_t t = R[r], e = s0 + ((t >> 4) + 1u) * C, mid = e - C / 2u;
         uint32_t q = P[t], n2 = 0;
+        while (q < mid) q = step(q, e, &n2);  // (the sync walk ends well before the middle)
+        M[t] = q;
+        KM[t] = uint16_t(n2);
         while (q < e) q = step(q, e, &n2);
         X[t] = q;
         K2[t] = uint16_t(n2);
@@ -1144,6 +1152,8 @@ __global__ __launch_bounds__(kTPB) void huf_table_kernel(HufArgs a, uint16_t* ta
         const int lt = (kc << 4) + lead[u], k = k0 + kc;
         tab[size_t(k) * kHufD + d] = uint16_t(X[lt] - ce);
         cnt[size_t(k) * kHufD + d] = uint16_t(n1[u] + K2[lt]);
+        mo[size_t(k) * kHufD + d] = uint16_t(M[lt] - (ce - C));  // (from the chunk's first bit)
+        mc[size_t(k) * kHufD + d] = uint16_t(n1[u] + KM[lt]);
     }
 }
 
@@ -1183,31 +1193,44 @@ __global__ __launch_bounds__(kTPB) void huf_count_kernel(HufArgs a, const uint16
 #ifndef IE_HUF_EMIT_LDS
 #define IE_HUF_EMIT_LDS 40960
 #endif
-__global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
+constexpr int kHufEmitT = 2 * kTPB;  // emit threads: two per chunk (its halves, split at the
+                                     // middle boundary the table pass recorded)
+__global__ __launch_bounds__(kHufEmitT) void huf_emit_kernel(HufArgs a, const uint16_t* mo, const uint16_t* mc) {
     __shared__ uint16_t l1[1 << kHufL1];
-    __shared__ alignas(8) uint32_t scratch[8];
+    __shared__ alignas(8) uint64_t scratch[kHufEmitT / 64];
     __shared__ uint8_t sym[IE_HUF_EMIT_LDS > 0 ? IE_HUF_EMIT_LDS : 1];
     extern __shared__ uint32_t L[];  // the workgroup's chunks' bits (+ 64 past the last)
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, j = tid % kTPB, half = tid / kTPB;
     const uint32_t C = uint32_t(a.chunk_bits);
     const int k0 = blockIdx.x * kTPB, m = min(kTPB, a.nchunks - k0);
     const uint64_t c0 = a.start_bit + uint64_t(k0) * C;
     const uint64_t base = c0 & ~31ull;
     const uint32_t s0 = uint32_t(c0 - base);
-    stage_words_pad(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kTPB);
+    stage_words_pad(L, a.words, base >> 5, int((s0 + uint32_t(m) * C + 64) >> 5) + 2, a.nbits, tid, kHufEmitT);
     huf_l1(a.lut, l1);  // (ends with a barrier: L staged too)
-    const uint64_t pre = huf_wg_prefix(a.wgsum, int(blockIdx.x), scratch);
+    // the symbols before this workgroup's chunks: the totals of the workgroups before it
+    uint64_t part = 0;
+    for (int i = tid; i < int(blockIdx.x); i += kHufEmitT) part += a.wgsum[i];
+    const uint64_t ws = wave_sum64(part);
+    if ((tid & 63) == 0) scratch[tid >> 6] = ws;
+    __syncthreads();
+    uint64_t pre = 0;
+#pragma unroll
+    for (int w = 0; w < kHufEmitT / 64; w++) pre += scratch[w];
     const uint32_t tot = a.wgsum[blockIdx.x];
     const bool staged = IE_HUF_EMIT_LDS > 0 && tot <= uint32_t(IE_HUF_EMIT_LDS);
-    const int k = k0 + tid;
-    if (tid < m) {
+    const int k = k0 + j;
+    if (j < m) {
         const uint32_t lim = uint32_t(min<uint64_t>(a.nbits - base, uint64_t(s0) + uint64_t(m) * C));
-        const uint32_t e = s0 + uint32_t(tid + 1) * C;
-        uint32_t p = uint32_t(a.entry[k] - base), c = 0;
-        const uint64_t at = pre + a.base[k];
-        uint8_t* o = staged ? sym + a.base[k] : a.out + at;
-        const uint64_t room = staged ? ~0ull : (a.out_cap > at ? a.out_cap - at : 0ull);
-        while (p < e && p < lim) {
+        const uint32_t cs = s0 + uint32_t(j) * C, e = cs + C;
+        const uint32_t x = uint32_t(a.entry[k] - (a.start_bit + uint64_t(k) * C));  // the true entry offset
+        const uint32_t mid = cs + mo[size_t(k) * kHufD + x];
+        uint32_t p = half ? mid : cs + x, c = 0;
+        const uint32_t end = half ? e : mid;
+        const uint64_t at = a.base[k] + (half ? mc[size_t(k) * kHufD + x] : 0u);
+        uint8_t* o = staged ? sym + at : a.out + pre + at;
+        const uint64_t room = staged ? ~0ull : (a.out_cap > pre + at ? a.out_cap - pre - at : 0ull);
+        while (p < end && p < lim) {
             const uint32_t p15 = lbits_pad(L, p, 15);
             uint32_t v = l1[p15 >> (15 - kHufL1)];
             if (!v) v = a.lut[p15];
@@ -1226,8 +1249,8 @@ __global__ __launch_bounds__(kTPB) void huf_emit_kernel(HufArgs a) {
     }
     if (!staged) return;
     __syncthreads();
-    if (pre + tot > a.out_cap && threadIdx.x == 0) atomicOr(&a.changed[0], 1u);
-    for (uint32_t i = threadIdx.x; i < tot && pre + i < a.out_cap; i += kTPB) a.out[pre + i] = sym[i];
+    if (pre + tot > a.out_cap && tid == 0) atomicOr(&a.changed[0], 1u);
+    for (uint32_t i = tid; i < tot && pre + i < a.out_cap; i += kHufEmitT) a.out[pre + i] = sym[i];
 }
 
 int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit, const uint16_t* lut,
@@ -1253,13 +1276,18 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
     a.out_cap = out_cap;
     const dim3 g((nchunks + kTPB - 1) / kTPB), blk(kTPB);
     if (write) {
-        hipLaunchKernelGGL(huf_emit_kernel, g, blk, size_t(pad_words(int(((uint64_t(kTPB) * chunk_bits + 95) >> 5) + 3))) * 4, s, a);
+        const uint16_t* cnt = tab + compose_rows<kHufD, kHufG>(nchunks) * kHufD;
+        const uint16_t* mo = cnt + size_t(nchunks) * kHufD;
+        hipLaunchKernelGGL(huf_emit_kernel, g, dim3(kHufEmitT), size_t(pad_words(int(((uint64_t(kTPB) * chunk_bits + 95) >> 5) + 3))) * 4, s,
+                           a, mo, mo + size_t(nchunks) * kHufD);
         return 0;
     }
     const size_t lds = size_t(pad_words(int(((uint64_t(kHufTC) * chunk_bits + 95) >> 5) + 3))) * 4;
     // the symbol counts after the composition's rows (compose_kernel rewrites the exit tables)
     uint16_t* cnt = tab + compose_rows<kHufD, kHufG>(nchunks) * kHufD;
-    hipLaunchKernelGGL(huf_table_kernel, dim3((nchunks + kHufTC - 1) / kHufTC), blk, lds, s, a, tab, cnt);
+    uint16_t* mo = cnt + size_t(nchunks) * kHufD;  // then the middle boundaries and their counts
+    hipLaunchKernelGGL(huf_table_kernel, dim3((nchunks + kHufTC - 1) / kHufTC), blk, lds, s, a, tab, cnt, mo,
+                       mo + size_t(nchunks) * kHufD);
     const int levels = launch_compose<kHufD, kHufG>(tab, nchunks, E, ticket, a.lvl, s);
     if (levels < 0) return -1;
     a.levels = levels;
@@ -1272,7 +1300,7 @@ int huffman_decode_device(const uint32_t* W, uint64_t nbits, uint64_t start_bit,
 size_t huffman_table_rows(uint64_t nbits, uint64_t start_bit, uint64_t chunk_bits) {
     const uint64_t span = nbits > start_bit ? nbits - start_bit : 0;
     const int nchunks = int((span + chunk_bits - 1) / chunk_bits);
-    return nchunks ? (compose_rows<kHufD, kHufG>(nchunks) + size_t(nchunks)) * kHufD : 0;  // (+ the counts)
+    return nchunks ? (compose_rows<kHufD, kHufG>(nchunks) + 3 * size_t(nchunks)) * kHufD : 0;  // (+ counts, middles)
 }
 
 }  // namespace ie
