@@ -387,7 +387,7 @@ def main():
                         "counts are taken by the encoder as it stores (its launch is the line's roofline)"}
             # the inverse of the Huffman pass: image 0's Huffman stream decoded back
             # to payload bytes, device-resident (ie_huffman_decode: table walk + composition + count +
-            # emit kernels), wall time per call incl. its host syncs
+            # emit kernels), wall time per call incl. its host sync
             hs0 = codec.huffman_encode_after_encode(outs[0], pitch, B, houts, hpitch)
             henc = houts[: hs0[0]].cpu().numpy().tobytes()
             tab = codec.huffman_table(henc)
@@ -409,7 +409,8 @@ def main():
                                            "achieved_GBps": round(hb_dec / thd / 1e9, 1),
                                            "frac": round(hb_dec / thd / 1e9 / HBM_PEAK_GBS, 4),
                                            "note": "Huffman stream read + symbols written per call, wall time incl. "
-                                                   "the host syncs (symbol count, then the decode)"}
+                                                   "its one host sync (device output: the emit is bounded by the "
+                                                   "output size, then the total and flags are read back together)"}
         if args.single_frame:  # one 4K frame per launch: the latency of the single-image configuration
             one = outs[0][:pitch]
 
