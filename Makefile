@@ -65,7 +65,7 @@ $(OBJDIR)/asm/%.s: $(CSRC)/%.hip $(CSRC)/ie_device.h $(CSRC)/ie_common.hpp $(CSR
 	@mkdir -p $(OBJDIR)/asm
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o $@
 asmcheck: $(ASMS)
-	python3 tools/asmcheck.py $(ASMS)
+	python3 tools/asmcheck.py $(ASMS) $(wildcard $(CSRC)/*.hip $(CSRC)/*.h $(CSRC)/*.hpp)
 
 clean:
 	rm -rf $(OBJDIR) $(LIBDIR)

@@ -41,7 +41,6 @@ struct ie_ctx {
 
     uint64_t* d_frame_start = nullptr;  // [cap_frames]
     uint64_t* d_chain_end = nullptr;    // [cap_frames]
-    unsigned* d_claim = nullptr;        // [cap_frames + 1] the persistent encoder's tile claim counters
     size_t cap_frames = 0;
     unsigned* d_err = nullptr;          // [0] look-back timeouts (cumulative)
     uint32_t* d_wave_fix = nullptr;     // [cap_tiles * waves per tile] fix-up requests of the last launch
@@ -96,11 +95,14 @@ struct ie_ctx {
     int pack_slot = 0;
     int fused_count = 0;  // > 0: the last encode (ie_encode_images_counted) left this many histograms in d_chist
     // the counted pipeline: the encoder's histograms (cleared by the first-occurrence pass that reads
-    // them: chist_zero), and per pinned slot the device n / first / unresolved the rare first_full
+    // them: chist_zero_rows), and per pinned slot the device n / first / unresolved the rare first_full
     // pass of ie_huffman_hist_batch_wait needs, with the batch it reads
     uint32_t* d_chist = nullptr;
     size_t cap_chist = 0;  // (words)
-    bool chist_zero = false;
+    // leading 256-word rows of d_chist known to be zero (the counted encode skips its memset when
+    // its rows lie within them), and the rows that will be zero once the fused pass has read -- and
+    // cleared -- the last counted encode's rows
+    size_t chist_zero_rows = 0, chist_clean_after = 0;
     bool hist_skip_zero = false;  // one shot: encode() skips its histogram memset (set by the counted encode)
     uint8_t* d_cslot[2] = {};
     size_t cap_cslot[2] = {};
@@ -495,9 +497,6 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
         const size_t cap = std::max<size_t>(nframes, 64);
         HIPCHK(c, hipMalloc(&c->d_frame_start, cap * sizeof(uint64_t)));
         HIPCHK(c, hipMalloc(&c->d_chain_end, cap * sizeof(uint64_t)));
-        if (c->d_claim) HIPCHK(c, hipFree(c->d_claim));
-        HIPCHK(c, hipMalloc(&c->d_claim, (cap + 1) * ie::kClaimStride * sizeof(unsigned)));
-        HIPCHK(c, hipMemsetAsync(c->d_claim, 0, (cap + 1) * ie::kClaimStride * sizeof(unsigned), c->stream));
         c->cap_frames = cap;
     }
     return IE_OK;
@@ -661,7 +660,6 @@ int launch_chain(ie_ctx* c, const Launch& L) {
     a.ticket_base = c->ticket_base;
     a.tag = c->tag;
     a.frame_start = c->d_frame_start;
-    a.claim = c->d_claim;
     a.chain_end = L.chain_end ? L.chain_end : c->d_chain_end;
     a.err = c->d_err;
     a.wave_fix = c->d_wave_fix;
@@ -1588,7 +1586,6 @@ int ie_destroy(ie_ctx* c) {
     (void)hipFree(c->d_state);
     (void)hipFree(c->d_ticket);
     (void)hipFree(c->d_frame_start);
-    (void)hipFree(c->d_claim);
     (void)hipFree(c->d_chain_end);
     (void)hipFree(c->d_err);
     (void)hipFree(c->d_wave_fix);
@@ -1892,10 +1889,13 @@ int ie_encode_images_counted(ie_ctx* c, const uint8_t* y, int w, int h, size_t s
     if (c->cap_chist < K * 256 || !c->d_chist) {
         if ((r = ensure(c, c->d_chist, c->cap_chist, K * 256))) return r;
         HIPCHK(c, hipMemsetAsync(c->d_chist, 0, c->cap_chist * sizeof(uint32_t), c->stream));
-        c->chist_zero = true;
+        c->chist_zero_rows = c->cap_chist / 256;
     }
-    c->hist_skip_zero = c->chist_zero;
-    c->chist_zero = false;
+    // rows [0, K) are counted into: skip their memset only when all of them are known zero (rows
+    // of an earlier, larger batch that no fused pass cleared may hold stale counts)
+    c->hist_skip_zero = K <= c->chist_zero_rows;
+    c->chist_clean_after = c->hist_skip_zero ? c->chist_zero_rows : K;
+    c->chist_zero_rows = 0;  // dirty until the fused pass reads this batch
     r = encode(c, y, w, h, stride, frame_pitch, nframes, use_rle, mode, out, out_pitch * K, out_pitch, start_bit, 1,
                nullptr, nullptr, nullptr, c->d_chist);
     c->hist_skip_zero = false;
@@ -2139,7 +2139,7 @@ int ie_huffman_hist_batch_ends_async(ie_ctx* c, const uint8_t* in, size_t in_pit
                                  reinterpret_cast<unsigned long long*>(hp + hb), reinterpret_cast<unsigned*>(hp + hb + fb),
                                  c->stream);
         HIPCHK(c, hipGetLastError());
-        c->chist_zero = true;
+        c->chist_zero_rows = c->chist_clean_after;  // (the pass cleared rows [0, count))
         if ((r = stage_mark(c, 1))) return r;
         HIPCHK(c, hipEventRecord(c->ev_hist[slot], c->stream));
         c->hist_count[slot] = count;
@@ -2188,12 +2188,17 @@ int ie_huffman_hist_batch_wait(ie_ctx* c, int slot, uint32_t* hist, uint64_t* fi
             }
             uint8_t* hp = nullptr;
             HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&hp), c->h_hist[slot], 0));
+            // on the side stream, ordered after the batch's histogram only: work the caller queued on
+            // c->stream since _async (e.g. the next batch's encode) is neither waited for nor
+            // delayed, and only this launch and its read-back are synchronised
+            if (!c->tab_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->tab_stream, hipStreamNonBlocking));
+            HIPCHK(c, hipStreamWaitEvent(c->tab_stream, c->ev_hist[slot], 0));
             ie::launch_first_full_batch(c->hist_in[slot], c->hist_pitch[slot], nn, maxn, K, reinterpret_cast<const uint32_t*>(hp),
                                         reinterpret_cast<unsigned long long*>(c->d_cslot[slot]),
-                                        reinterpret_cast<const unsigned*>(c->d_cslot[slot] + fb + nb), c->stream);
+                                        reinterpret_cast<const unsigned*>(c->d_cslot[slot] + fb + nb), c->tab_stream);
             HIPCHK(c, hipGetLastError());
-            HIPCHK(c, hipMemcpyAsync(first_pos, c->d_cslot[slot], fb, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipMemcpyAsync(first_pos, c->d_cslot[slot], fb, hipMemcpyDeviceToHost, c->tab_stream));
+            HIPCHK(c, hipStreamSynchronize(c->tab_stream));
         }
     }
     return IE_OK;
@@ -2431,7 +2436,9 @@ int ie_huffman_decode(ie_ctx* c, const uint8_t* in, size_t len, uint64_t start_b
     // best on a 4K payload (tools/gpu_huf_chunk.sh: 0.30-0.32 ms against 0.34 at 512, 0.37 at 768
     // and 2048, 0.55 at 4096)
     static const uint64_t huf_chunk = getenv("IE_HUF_CHUNK") ? strtoull(getenv("IE_HUF_CHUNK"), nullptr, 10) : 1024;
-    const uint64_t chunk_bits = std::max<uint64_t>(256, huf_chunk);
+    // (at most 2048: the per-chunk symbol counts and middle offsets are u16, and huf_emit_kernel's
+    // LDS grows ~33 bytes per chunk bit -- 4096-bit chunks would not fit gfx950's 160 KB)
+    const uint64_t chunk_bits = std::min<uint64_t>(2048, std::max<uint64_t>(256, huf_chunk));
     const size_t nchunks = size_t((nbits - start_bit + chunk_bits - 1) / chunk_bits);
     if (!nchunks) return IE_OK;
     // d_walk: [cap] entries, [cap] symbol bases, then 128 words of top-level entries (256 x u32)

@@ -16,6 +16,15 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// The lane id computed afresh (two VALU): an opaque value the compiler cannot CSE with earlier
+// copies, so a kernel that re-derives it per phase holds no lane-derived VGPR across its phases
+// (values live across a whole tile otherwise end up spilled at higher occupancy).
+__device__ __forceinline__ int fresh_lane() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations but not for its
 // global loads, so a prefetch of the next tile's pixels stays in flight across it (a
 // __syncthreads() would drain it).  Global memory is never handed between the threads of a

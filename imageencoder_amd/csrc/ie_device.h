@@ -111,12 +111,7 @@ struct EncArgs {
     // optional (segmented launches): per-frame byte histograms [nframes][256] of the stream bytes
     // [0, ceil(end/8)) -- header included -- ADDED to by the launch (the Huffman pass's counts)
     uint32_t* hist;
-    // persistent encoder (encode4p_kernel): per-chain claim counters [nchains] then the exit counter,
-    // kClaimStride words apart (a 128-byte line each: atomics on one line serialise), all zero
-    // before the launch and left zero by its last workgroup
-    unsigned* claim;
 };
-constexpr int kClaimStride = 32;
 
 constexpr int kStamps = 64;  // encode_kernel: [0, 16) by thread 0; encode4w_kernel: [4 waves][16] by each wave's lane 0
 // chain-state words per tile (the host allocates; ie_common.hpp kGran must not exceed it)

@@ -50,9 +50,6 @@ template <> struct ZigZagInv<8> {
                                     21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 };
 
-#ifndef IE_P_GEO  // encode4p_kernel: a tile's geometry fields in one scalar round trip (load_geo)
-#define IE_P_GEO 1
-#endif
 #ifndef IE_PROFILE
 #define IE_PROFILE 0
 #endif
@@ -1934,61 +1931,36 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
 
 // =============================================================================================
 // encode4p_kernel -- encode4w_kernel's tile (wave-local slots, the same emission, look-back and
-// store), made PERSISTENT and with the integer half of the transform on the matrix pipe.
-//   * Persistent: the grid is the number of tiles the chip holds at once (the occupancy API's
-//     answer, launch_encode4w); workgroup g walks tiles g, g + G, g + 2G, ... (ticket mode, the
-//     host's fallback, runs encode4w_kernel).  No workgroup is re-dispatched per tile, the FP64 rows and the matrix operand are staged once, and each wave
-//     issues its NEXT tile's pixel DMA into its own LDS region as soon as its last slot image has
-//     been read out -- the DMA flies while the wave finishes the tile (tail word, tail granule) and
-//     while the workgroup's other waves finish theirs.  Static order needs every workgroup resident:
-//     the grid never exceeds the occupancy answer, and a look-back timeout (should that ever not
-//     hold) makes the host redo the launch in ticket mode, as for encode4w_kernel.
+// store) with the integer half of the transform on the matrix pipe.  One workgroup per tile, the
+// tiles in dispatch order (ticket mode, the host's fallback after a look-back timeout, runs
+// encode4w_kernel).
 //   * Matrix pipe: per slot (64 blocks of one wave), ONE v_mfma_i32_32x32x32_i8 forms the sixteen
 //     integer basis sums J of every block (ie_dct.h quot4j: pixels as signed bytes x ^ 0x80, the
 //     {-1,0,1} A fragment from EncTables::mfma_w), which replaces the 16 pixel unpacks and the
 //     integer butterflies on the VALU; the FP32 stage (36 mul/fma) and the rounding follow, with
 //     the tie limits of quot4j's own tracked run (lim4j).  The FP64 fix-up, sizing, emission and
 //     store are encode4w_kernel's.
-//   * misc (the waves' bit counts, head words, position) alternates between two copies by tile
-//     parity, so a wave that runs ahead into its next tile never overwrites what a slower wave of
-//     the same workgroup still reads; the tile's two barriers order everything else.
+//   * Count by polling: each wave stores its bit count and a flag; wave 0 alone waits for the
+//     four flags, publishes the tile aggregate and issues its look-back probe, while waves 1-3 go
+//     straight on to their emission.  One workgroup barrier per tile (the position).
+//   * Whole-wave images: when a wave's image fits its 4 KB region, all four slots are emitted
+//     before the position barrier, beside wave 0's look-back; slot pairs in turn otherwise.
+// Measured and not kept: a persistent grid walking the tiles -- by per-chain claim
+// atomics (126.7 against 93.5 us) or in static order g, g + G, ... (110.3 against 88.4 us: a tile
+// whose chain predecessor sits in a slower workgroup waits for it, where the dispatcher starts
+// tiles in chain order as slots free) --, a software-pipelined persistent variant with two buffers
+// per wave (126.7 against 93.6 us: four tiles per CU instead of six), an L2 prefetch of the tile
+// about d dispatches later (neutral at d = 256-1024 on HBM-resident frames).
 // =============================================================================================
-// Tile boundary word (encode4p_kernel, encode4q_kernel): the word holding a tile's first bits and
-// its predecessor's last is written by whichever of the two reaches it second, found by ONE 64-bit
-// exchange on the successor's granule 3 (atomics on one address are ordered: exactly one of the
-// two sees the other's half) -- no tile waits for its predecessor's tail.
-static_assert(kGran >= 4, "the boundary exchange uses granule 3");
-// One side of a tile-boundary word: role 1 = the tile ending in it, 2 = the tile starting in it;
-// part = that tile's bits of the word (before the byte swap).  Returns the old granule.
-__device__ __forceinline__ uint64_t boundary_swap(uint64_t* st, int succ, uint32_t tag, uint32_t role, uint32_t part) {
-    const uint64_t v = (uint64_t(tag) << 56) | (uint64_t(role) << 48) | part;
-    return __hip_atomic_exchange(&st[kGran * succ + 3], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Whether this side is the second (then *w = the whole word, byte-swapped for the store).
-__device__ __forceinline__ bool boundary_second(uint64_t old, uint32_t tag, uint32_t role, uint32_t part, uint32_t* w) {
-    *w = bswap32(part | uint32_t(old));
-    return uint32_t(old >> 56) == tag && uint32_t((old >> 48) & 0xFFu) == 3u - role;
-}
-// The second side writes the word.
-__device__ __forceinline__ void boundary_finish(uint32_t* out, uint64_t word, uint64_t old, uint32_t tag, uint32_t role,
-                                                uint32_t part) {
-    if (uint32_t(old >> 56) == tag && uint32_t((old >> 48) & 0xFFu) == 3u - role) out[word] = bswap32(part | uint32_t(old));
-}
-
 constexpr int kPWfrag = 256;  // the matrix-pipe A fragments [64 lanes][4 words]
-// encode4p_kernel's misc words per copy by waves per tile: [0, WPT) wave bit counts, H the waves'
-// head words, E the tile's exclusive prefix (2), PT the tail before the chain start, PD the pending
-// first word, C12 / CL the claim words, F the count flags, D the deep look-back sums (2 per wave),
-// FD their found flags; S the copy's size (4 waves: encode4w_kernel's layout)
-template <int WPT> struct PMisc {
-    static constexpr int H = WPT, E = 2 * WPT, PT = 2 * WPT + 2, PD = 2 * WPT + 3, C12 = 2 * WPT + 4,
-                         CL = 2 * WPT + 5, F = 4 * WPT, D = 4 * WPT + WPT + 2 - (WPT == 4 ? 4 : 0),
-                         FD = D + 2 * WPT, S = WPT == 4 ? 32 : 96;
-    static_assert(FD + WPT <= S && F % 4 == 0 && CL < F, "misc layout");
+// encode4p_kernel's misc words: [0, 4) wave bit counts, H the waves' head words, E the tile's
+// exclusive prefix (2), PT the tail before the chain start, PD the pending first word, F the
+// count flags, D the deep look-back sums (2 per wave), FD their found flags
+struct PMisc {
+    static constexpr int H = 4, E = 8, PT = 10, PD = 11, F = 16, D = 20, FD = 28, S = 32;
+    static_assert(FD + 4 <= S && F % 4 == 0, "misc layout");
 };
-template <int WPT> constexpr int p_lds_bytes() {
-    return (WPT * 4 * 64 * (16 / WPT) + WPT * kWTask + 2 * PMisc<WPT>::S + kPWfrag) * 4 + kWRows * 8;
-}
+constexpr int p_lds_bytes() { return (4 * 4 * 256 + 4 * kWTask + PMisc::S + kPWfrag) * 4 + kWRows * 8; }
 
 typedef int v4i32 __attribute__((ext_vector_type(4)));
 typedef int v16i32 __attribute__((ext_vector_type(16)));
@@ -2029,1074 +2001,106 @@ __device__ __forceinline__ float round_block_lean4j(const float (&t)[16], uint32
     return emax;
 }
 
-// Tile claims of the persistent encoder.  Tiles of a chain are handed out in chain order by that
-// chain's counter (segmented launches: one chain per frame, tile = k * nframes + frame, the
-// interleave of tile_geo; otherwise one chain, tile = k); a workgroup stays on its chain until it
-// is exhausted, then moves to the next chain with tiles left.  A tile's look-back waits only on
-// earlier tiles of its chain, claimed before it by workgroups that are running (a workgroup claims
-// its next tile while it works on the current one, and no chain of such waits can close: DESIGN
-// §3), so the order needs no residency guarantee.  One wave calls it (wave-uniform result).
-__device__ __forceinline__ int claim_resolve(unsigned* cnt, int nch, int tpc, bool seg, int* c, unsigned k) {
-    const int lane = lane_id();
-    for (;;) {
-        const int kk = __builtin_amdgcn_readfirstlane(int(k));
-        if (kk < tpc) return seg ? kk * nch + *c : kk;
-        if (nch == 1) return -1;
-        int found = -1;  // the first chain after *c with tiles left, 64 chains per look
-        for (int j0 = 1; j0 < nch && found < 0; j0 += 64) {
-            const int j = j0 + lane;
-            const int cc = (*c + j) % nch;
-            const bool left = j < nch && __hip_atomic_load(&cnt[kClaimStride * cc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unsigned(tpc);
-            const uint64_t m = __ballot(left);
-            if (m) found = __builtin_amdgcn_readlane(cc, __ffsll((unsigned long long)m) - 1);
-        }
-        if (found < 0) return -1;
-        *c = found;
-        unsigned kn = 0;
-        if (lane == 0) kn = atomicAdd(&cnt[kClaimStride * found], 1u);
-        k = kn;
-    }
-}
-
-// Rounding of quotients formed as t + 1/2 (quot4j<true>): rint(t) = floor(t + 1/2) away from ties
-// (one v_cvt_flr_i32_f32), and t is within the bound of a tie exactly when f = fract(t + 1/2) is
-// within it of 0 or 1 -- the thirteen ordinary coefficients by one min and one max over their f,
-// the structural three one by one (sflags bits 0-2).  Returns whether an ordinary coefficient may
-// be at a tie.  At an exact tie floor(t + 1/2) need not be the reference's value: every tie is
-// flagged and re-evaluated.  DC (dcx: exact, q[0] a power of two): std::round's half away from
-// zero from t + 1/2 directly.
-struct HalfLims {
-    float lo0, hi0, lo1, hi1, lo2, hi2, lo, hi;
-};
-__device__ __forceinline__ bool round_half4(const float (&tp)[16], uint32_t (&zp)[8], uint32_t* sflags, bool dcx,
-                                            const HalfLims& L) {
-    constexpr int S0 = Structural<4>::k[0], S1 = Structural<4>::k[1], S2 = Structural<4>::k[2];
-    float fmin = 1.0f, fmax = 0.0f;
-    uint32_t sf = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        int r[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int k = ZigZag<4>::idx[2 * j + h];
-            const float x = tp[k];
-            const float f = __builtin_amdgcn_fractf(x);
-            asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r[h]) : "v"(x));  // (floorf + a conversion would be two)
-            if (k == 0) {
-                // t >= 0: floor(t + 1/2); t < 0: -floor(1/2 - t) = -floor(1 - (t + 1/2))
-                const int neg = -int(floorf(1.0f - x));
-                r[h] = dcx ? (x >= 0.5f ? r[h] : neg) : r[h];
-                fmin = dcx ? fmin : fminf(fmin, f);
-                fmax = dcx ? fmax : fmaxf(fmax, f);
-            } else if (k == S0) {
-                sf |= (f <= L.lo0 || f >= L.hi0) ? 1u : 0u;
-            } else if (k == S1) {
-                sf |= (f <= L.lo1 || f >= L.hi1) ? 2u : 0u;
-            } else if (k == S2) {
-                sf |= (f <= L.lo2 || f >= L.hi2) ? 4u : 0u;
-            } else {
-                fmin = fminf(fmin, f);
-                fmax = fmaxf(fmax, f);
-            }
-        }
-        zp[j] = __builtin_amdgcn_perm(uint32_t(r[1]), uint32_t(r[0]), 0x05040100u);
-        asm volatile("" : "+v"(zp[j]));
-    }
-    *sflags = sf;
-    return fmin <= L.lo || fmax >= L.hi;
-}
-
-#ifndef IE_P_SIZE4
-#define IE_P_SIZE4 1
-#endif
-#ifndef IE_P_DPPFIX
-#define IE_P_DPPFIX 1
-#endif
-#ifndef IE_P_RHALF
-#define IE_P_RHALF 0  // 1: (A/B builds) floor / fract of t + 1/2 (round_half4): +1.5 % VALU, slower
-#endif
-
 #ifndef IE_P_WAVES
 #define IE_P_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD)
 #endif
 #ifndef IE_P_WAVES_HIST
 #define IE_P_WAVES_HIST 6  // the counting instantiation (5: 89 VGPRs; measured 124.7 against 119.4 us)
 #endif
-#ifndef IE_P_MFMA
-#define IE_P_MFMA 1  // 0: (A/B builds) the transform on the VALU as in encode4w_kernel
-#endif
 #ifndef IE_P_ABL
 #define IE_P_ABL 0  // (profiling builds) phases left out: 1 FP64 fix-up, 2 emission, 4 look-back, 8 store, 16 transform
 #endif
-#ifndef IE_P_LATEPROBE
-#define IE_P_LATEPROBE 0
-#endif
-#ifndef IE_P_XCHG
-#define IE_P_XCHG 0  // 1: (A/B builds) the boundary words by exchange (measured neutral on C2: 90.8 vs 90.0 us)
-#endif
-#ifndef IE_P_CNTBAR
-#define IE_P_CNTBAR 0  // 1: (A/B builds) a workgroup barrier for the tile's count, not wave 0's polling
-#endif
-#ifndef IE_P_PERSIST
-#define IE_P_PERSIST 0  // 1: (A/B builds) the persistent grid with per-chain tile claims
-#endif
 
-// WPT: waves per tile -- 4 (four slots of 64 blocks per lane), or 8 for launches too small to fill
-// the chip (two slots per lane: twice the waves per tile, half the work per wave; the tile, its
-// chain element and its stream layout are the same)
-template <bool HIST, int WPT>
-__global__ __launch_bounds__(64 * WPT, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void encode4p_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
-    static_assert(WPT == 4 || (WPT == 8 && !HIST), "4 waves per tile, or 8 without the histogram");
-    constexpr int N = 4, NN = 16, NP = 8, TPB = 64 * WPT, NS = 16 / WPT, PS = NS / 2;  // PS: slots per pair
-    constexpr int GW = 16 * NS, BW = 64 * NS, TG = WPT * GW;  // groups / blocks per wave, groups per tile
+template <bool HIST>
+__global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void encode4p_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
+    constexpr int N = 4, NN = 16, NP = 8, NS = 4, PS = 2;  // slots per lane, slots per pair
+    constexpr int GW = 64, BW = 256, TG = 256;  // groups / blocks per wave, groups per tile
     constexpr int RW = 4 * BW;  // words per wave region
-    using ML = PMisc<WPT>;
+    using ML = PMisc;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int tid = threadIdx.x;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
     uint32_t* const reg = smem + wv * RW;  // this wave's pixels, later its slot images
-    uint32_t* const task = smem + WPT * RW + wv * kWTask;
+    uint32_t* const task = smem + 4 * RW + wv * kWTask;
     uint32_t* const res = task + 64;
-    uint32_t* const misc0 = smem + WPT * RW + WPT * kWTask;  // [2][ML::S]
-    uint32_t* const wl = misc0 + 2 * ML::S;  // [64][4]: the matrix-pipe A fragment of every lane
-    uint32_t* const hl = wl + kPWfrag;    // HIST: the tile's byte histogram
+    uint32_t* const misc = smem + 4 * RW + 4 * kWTask;  // [ML::S]
+    uint32_t* const wl = misc + ML::S;  // [64][4]: the matrix-pipe A fragment of every lane
+    uint32_t* const hl = wl + kPWfrag;  // HIST: the tile's byte histogram
     constexpr int HR = kWHistRep, HWORDS = 256 * HR;
     double* const srow = reinterpret_cast<double*>(hl + (HIST ? HWORDS : 0));
-    const int G = int(gridDim.x);
-
-    // The launch arguments are read through a pointer to the kernel-argument segment that is
-    // re-derived every tile: loop-invariant loads would otherwise be hoisted out of the tile loop
-    // and the ~40 argument words held in scalar registers for the kernel's whole life (spills).
+    const int t = int(blockIdx.x);
+    // The launch arguments are read through a pointer to the kernel-argument segment (constant
+    // address space): the geometry words in one scalar round trip (load_geo), the rest where used.
     using KArgs = const __attribute__((address_space(4))) EncArgs;
     KArgs* ka = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
-    // tile order: a grid of one workgroup per tile runs them in blockIdx order (dispatch order, as
-    // encode4w_kernel); a smaller (persistent) grid claims them (claim_resolve).  Ticket mode runs
-    // encode4w_kernel (launch_encode4w).
-    const bool dyn = IE_P_PERSIST && G < a_.ntiles;
-    const bool seg = a_.segmented != 0;
-    const int nch = seg ? a_.nframes : 1, tpc = seg ? a_.tiles_per_frame : a_.ntiles;
-    unsigned* const cnt = a_.claim;
-    int chain = int(blockIdx.x) % nch;  // the chain this workgroup claims from (wave 0's copy counts)
-    int t = int(blockIdx.x);
-    const GeoArgs ga0 = load_geo(ka);
-    if (dyn) {
-        if (wv == 0) {
-            unsigned k = 0;
-            if ((tid & 63) == 0) k = atomicAdd(&cnt[kClaimStride * chain], 1u);
-            const int tt = claim_resolve(cnt, nch, tpc, seg, &chain, k);
-            if (tid == 0) misc0[ML::C12] = uint32_t(tt);
-        }
-        lds_barrier();
-        t = __builtin_amdgcn_readfirstlane(int(misc0[ML::C12]));
-    }
-    // (every workgroup of a claiming grid counts its exit; the last one leaves the counters zero)
-    auto leave = [&]() {
-        if (dyn && tid == 0) {
-            const unsigned e = atomicAdd(&cnt[kClaimStride * nch], 1u);
-            if (e == unsigned(G) - 1u) {
-                for (int i = 0; i <= nch; i++) __hip_atomic_store(&cnt[kClaimStride * i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    };
-    if (t < 0 || t >= (IE_P_GEO ? ga0.ntiles : a_.ntiles)) {
-        leave();
-        return;
-    }
+    const GeoArgs ga = load_geo(ka);
+    if (t >= ga.ntiles) return;
+    // The lane id is re-derived at every phase (fresh_lane): a lane-derived VGPR held across the
+    // whole tile was spilled at higher occupancy.
+    int lane = fresh_lane();
     // (profiling: the workgroup's entry on the chip-wide clock, wave 0's word 13)
-    if (IE_PROFILE && a_.stamps && (tid & 63) == 0 && wv < 4) a_.stamps[size_t(t) * kStamps + wv * 16 + 13] = __builtin_amdgcn_s_memrealtime();
-    // each wave's pixel rows of tile tt into its own region (row r of the wave's block j at
-    // reg[r BW + j]: a lane's 16 bytes are its group's row)
-    auto issue_pixels = [&](const auto& a, int tt) {
-        const int l0 = tid & 63;
-        if (l0 >= GW) return;  // (8 waves per tile: a wave's 32 groups, one per lane)
-        const TileGeo gg = tile_geo<4, 4, TG>(a, tt, GW * wv + l0);
-        if (gg.nblk) {
-            const uint8_t* base = a.y + size_t(gg.frame) * a.frame_pitch + size_t(gg.byi) * N * a.stride + size_t(gg.bx0) * N;
+    if (IE_PROFILE && a_.stamps && lane == 0) a_.stamps[size_t(t) * kStamps + wv * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+    const TileGeo g = tile_geo<4, 4, TG>(ga, t, GW * wv + lane);
+    // the wave's pixel rows into its own region (row r of the wave's block j at reg[r BW + j]: a
+    // lane's 16 bytes are its group's row)
+    if (g.nblk) {
+        const uint8_t* base = ga.y + size_t(g.frame) * ga.frame_pitch + size_t(g.byi) * N * ga.stride + size_t(g.bx0) * N;
 #pragma unroll
-            for (int r = 0; r < N; r++)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
-                                                 (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, 0);
-        }
-    };
-    if (IE_P_GEO) issue_pixels(ga0, t);
-    else issue_pixels(*ka, t);
-    if (IE_PROFILE == 2 && a_.stamps && (tid & 63) == 0 && wv < 4) a_.stamps[size_t(t) * kStamps + wv * 16 + 1] = __builtin_amdgcn_s_memrealtime();
+        for (int r = 0; r < N; r++)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * ga.stride),
+                                             (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, 0);
+    }
+    if (IE_PROFILE == 2 && a_.stamps && lane == 0) a_.stamps[size_t(t) * kStamps + wv * 16 + 1] = __builtin_amdgcn_s_memrealtime();
     // the FP64 rows (waves 0-2: 2432 bytes) and the matrix-pipe A fragments (wave 3; read back per
-    // slot: a register copy held across the tile loop measured as spills) by DMA too: no register
-    // round trip, one wait for everything
+    // slot) by DMA too: no register round trip, one wait for everything
     {
-        const int lane0 = tid & 63;
         static_assert(kWRows * 8 == 2 * 1024 + 24 * 16, "rows: two full waves and 24 lanes of 16 bytes");
-        if (wv < 2 || (wv == 2 && lane0 < 24))
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->rows4[wv * 128 + 2 * lane0]),
+        if (wv < 2 || (wv == 2 && lane < 24))
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->rows4[wv * 128 + 2 * lane]),
                                              (__attribute__((address_space(3))) void*)(srow + wv * 128), 16, 0, 0);
         else if (wv == 3)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->mfma_w[lane0][0]),
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->mfma_w[lane][0]),
                                              (__attribute__((address_space(3))) void*)(wl), 16, 0, 0);
     }
     if constexpr (HIST)
-        for (int i = tid; i < HWORDS; i += TPB) hl[i] = 0u;
-    if ((tid & 63) == 0) {  // the waves' count flags of both misc copies
-        misc0[ML::F + wv] = 0u;
-        misc0[ML::S + ML::F + wv] = 0u;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA above and the first tile's pixels)
-    if (IE_PROFILE && a_.stamps && (tid & 63) == 0 && wv < 4) a_.stamps[size_t(t) * kStamps + wv * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+        for (int i = 64 * wv + lane; i < HWORDS; i += 256) hl[i] = 0u;
+    if (lane == 0) misc[ML::F + wv] = 0u;  // the waves' count flags
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA above and this wave's pixels)
+    if (IE_PROFILE && a_.stamps && lane == 0) a_.stamps[size_t(t) * kStamps + wv * 16 + 12] = __builtin_amdgcn_s_memrealtime();
     const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
     const bool deep = a_.deep_lb != 0;
-    lds_barrier();  // the rows, the A fragments (and the HIST bins) visible
-    if (IE_PROFILE && a_.stamps && (tid & 63) == 0 && wv < 4) a_.stamps[size_t(t) * kStamps + wv * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+    lds_barrier();  // every wave's pixels, the rows, the A fragments (and the HIST bins) visible
+    KArgs& a = *ka;
+    // (the tile's geometry is uniform: held in SGPRs, not in VGPRs the compiler would keep -- and
+    // spill -- across the tile)
+    const int frame = __builtin_amdgcn_readfirstlane(g.frame), tif = __builtin_amdgcn_readfirstlane(g.tif),
+              step = __builtin_amdgcn_readfirstlane(g.step), chain_pos = __builtin_amdgcn_readfirstlane(g.chain_pos);
+    const int ng = min(TG, ga.groups_per_frame - tif * TG);
+    const int nbw = __builtin_amdgcn_readfirstlane(4 * min(GW, max(0, ng - GW * wv)));  // blocks of this wave
+    const int wlast = (ng - 1) / GW;                    // the tile's last non-empty wave
+    WSTAMP(0);
+    WRTSTAMP(14);
+    if (IE_PROFILE != 2) WSTAMP(1);
+    asm volatile("; PHASE p1" ::: "memory");
 
-    for (int iter = 0;; iter++) {
-        asm volatile("" : "+s"(ka));
-        KArgs& a = *ka;
-        // lane-derived values re-derived every tile as well: addresses computed from them would
-        // otherwise be hoisted out of the tile loop and held (spilled) across it
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const int lane = tid & 63;
-        uint32_t* const misc = misc0 + (iter & 1) * ML::S;
-        const GeoArgs ga = load_geo(ka);
-        const TileGeo g = IE_P_GEO ? tile_geo<4, 4, TG>(ga, t, tid) : tile_geo<4, 4, TG>(a, t, tid);
-        const int frame = g.frame, tif = g.tif, step = g.step, chain_pos = g.chain_pos;
-        const int ng = min(TG, (IE_P_GEO ? ga.groups_per_frame : a.groups_per_frame) - tif * TG);
-        const int nbw = 4 * min(GW, max(0, ng - GW * wv));  // blocks of this wave
-        const int wlast = (ng - 1) / GW;                    // the tile's last non-empty wave
-        WSTAMP(0);
-        WRTSTAMP(14);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pixels landed
-        if (wv == 0 && lane == 0) misc[ML::CL] = 0u;  // the next tile's claim: not yet made (read after barrier 2)
-        if (IE_PROFILE != 2) WSTAMP(1);
-        asm volatile("; PHASE p1" ::: "memory");
-
-        // -------------------------------------------------------- transform + quantise, 4 slots
-        // (the table pointer is re-derived every tile so that the FP32 stage's 36 constants are
-        // loaded here, not hoisted out of the tile loop into scalar registers held for its whole life)
-        using KTab = const __attribute__((address_space(4))) EncTables;
-        KTab* tb = (KTab*)(tab);  // constant address space: scalar loads
-        asm volatile("" : "+s"(tb));
-        const bool dcx = IE_P_RHALF ? tb->dc_exact4h != 0 : tb->dc_exact4j != 0;
-        const float lim_s0 = tb->lim4j[Structural<4>::k[0]], lim_s1 = tb->lim4j[Structural<4>::k[1]],
-                    lim_s2 = tb->lim4j[Structural<4>::k[2]], lim_min = tb->lim_min4j;
-        constexpr int K0 = Structural<4>::k[0], K1 = Structural<4>::k[1], K2 = Structural<4>::k[2];
-        const HalfLims hl4{tb->dlo4h[K0], tb->dhi4h[K0], tb->dlo4h[K1], tb->dhi4h[K1],
-                           tb->dlo4h[K2], tb->dhi4h[K2], tb->dlo_max4h, tb->dhi_min4h};
-        uint32_t zp[NS][NP];
-        uint32_t flags = 0;  // 4 bits per slot: structural s (bits 0-2), whole block (bit 3)
-        auto slot_mfma = [&](int b) {
-            v4i32 px;
+    // ------------------------------------------------------------ transform + quantise, 4 slots
+    using KTab = const __attribute__((address_space(4))) EncTables;
+    KTab* tb = (KTab*)(tab);  // constant address space: scalar loads
+    const bool dcx = tb->dc_exact4j != 0;
+    const float lim_s0 = tb->lim4j[Structural<4>::k[0]], lim_s1 = tb->lim4j[Structural<4>::k[1]],
+                lim_s2 = tb->lim4j[Structural<4>::k[2]], lim_min = tb->lim_min4j;
+    uint32_t zp[NS][NP];
+    uint32_t flags = 0;  // 4 bits per slot: structural s (bits 0-2), whole block (bit 3)
 #pragma unroll
-            for (int r = 0; r < N; r++) px[r] = int(reg[r * BW + 64 * b + lane] ^ 0x80808080u);  // x - 128 as i8
-            const v4i32 wfrag = *reinterpret_cast<const v4i32*>(wl + 4 * lane);
-            return __builtin_amdgcn_mfma_i32_32x32x32_i8(wfrag, px, v16i32{}, 0, 0, 0);
-        };
+    for (int b = 0; b < NS; b++) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t sf;
+        float emax;
+        if (IE_P_ABL & 16) {  // (profiling) no transform: quotients = pixels / 64
+            float x[NN];
 #pragma unroll
-        for (int b = 0; b < NS; b++) {
-            __builtin_amdgcn_sched_barrier(0);
-            uint32_t sf;
-            float emax, lmin;
-            if (IE_P_ABL & 16) {  // (profiling) no transform: quotients = pixels / 64
-                float x[NN];
-#pragma unroll
-                for (int k = 0; k < NN; k++) x[k] = float((reg[(k >> 2) * BW + 64 * b + lane] >> (8 * (k & 3))) & 0xFFu) * 0.015625f;
-                emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
-                lmin = lim_min;
-            } else if (IE_P_MFMA && IE_P_RHALF) {
-                const v16i32 Jc = slot_mfma(b);
-                float Jf[16], x[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) Jf[k] = float(Jc[k]);
-                quot4j<true>(Jf, x, tb->plan4j, FloatOp());
-                emax = round_half4(x, zp[b], &sf, dcx, hl4) ? 1.0f : 0.0f;
-                lmin = 0.5f;
-            } else if (IE_P_MFMA) {
-                const v16i32 Jc = slot_mfma(b);
-                float Jf[16], x[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) Jf[k] = float(Jc[k]);
-                quot4j(Jf, x, tb->plan4j, FloatOp());
-                emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
-                lmin = lim_min;
-            } else {  // (A/B builds) the VALU transform of encode4w_kernel
-                uint32_t rows[N][1];
-#pragma unroll
-                for (int r = 0; r < N; r++) rows[r][0] = reg[r * BW + 64 * b + lane];
-                float x[NN];
-                block_pixels<N, 1>(rows, 0, x);
-                quotients<N>(tab, x);
-                emax = round_block_lean4(tab, x, zp[b], &sf);
-                lmin = tab->lim_min;
-            }
-            const uint32_t fb = (emax >= lmin) ? 8u : sf;
-            if (64 * b + lane < nbw) flags |= fb << (4 * b);
-#pragma unroll
-            for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
-            asm volatile("" : "+v"(flags));
-        }
-        WSTAMP(2);
-        asm volatile("; PHASE p2" ::: "memory");
-
-        // -------------------------------------------------------- FP64 fix-up (encode4w_kernel's)
-        auto block_px = [&](int b, int owner) {
-            BlockPx<N> px;
-#pragma unroll
-            for (int r = 0; r < N; r++) px.w[r] = reg[r * BW + 64 * b + owner];
-            return px;
-        };
-        if (!(IE_P_ABL & 1) && __ballot(flags != 0)) {
-            const uint32_t sf = flags & 0x7777u;
-            const uint32_t cnt = __popc(sf);
-            uint32_t pre, total;
-            if (IE_P_DPPFIX) {  // the lanes' request counts placed by one DPP wave scan
-                const uint32_t incl = wave_incl_scan_dpp(cnt);
-                pre = incl - cnt;
-                total = __builtin_amdgcn_readlane(incl, 63);
-            } else {  // (A/B builds) a 4-plane ballot prefix
-                pre = 0;
-                total = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {  // cnt <= 12
-                    const uint64_t bm = __ballot((cnt >> k) & 1u);
-                    pre += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
-                    total += uint32_t(__popcll(bm)) << k;
-                }
-            }
-            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
-                uint32_t m = sf, i = pre - r0;
-                while (m) {
-                    const int bit = __ffs(m) - 1;
-                    m &= m - 1;
-                    if (i < 64u) task[i] = (uint32_t(lane) << 4) | uint32_t(bit);
-                    i++;
-                }
-                wave_sync();
-                if (uint32_t(lane) < total - r0) {
-                    const uint32_t tk = task[lane];
-                    const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
-                    const BlockPx<N> px = block_px(b, owner);
-                    const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
-                    const int y = (IE_P_ABL & 32) ? int(px.w[0] & 1u)  // (profiling) no FP64 arithmetic (a small value: records stay in bound)
-                                                  : exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                                      srow[NN * NN + 2 * NN + k], px);
-                    res[lane] = uint32_t(y) & 0xFFFFu;
-                }
-                wave_sync();
-                i = pre - r0;
-#pragma unroll
-                for (int b = 0; b < NS; b++)
-#pragma unroll
-                    for (int ss = 0; ss < 3; ss++) {
-                        if ((sf >> (4 * b + ss)) & 1u) {
-                            const int zw = Structural<N>::zpos(ss) >> 1;
-                            if (i < 64u) zp[b][zw] = __builtin_amdgcn_perm(res[i], zp[b][zw], 0x05040100u);  // res low -> high half
-                            i++;
-                        }
-                    }
-                wave_sync();
-            }
-            const uint32_t wf = flags & 0x8888u;
-            if (__ballot(wf != 0)) {
-                const uint32_t nb = __popc(wf);
-                uint32_t pb = 0, tb = 0;
-#pragma unroll
-                for (int k = 0; k < 3; k++) {  // nb <= 4
-                    const uint64_t bm = __ballot((nb >> k) & 1u);
-                    pb += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
-                    tb += uint32_t(__popcll(bm)) << k;
-                }
-                for (uint32_t r0 = 0; r0 < tb; r0 += 4) {
-                    uint32_t m = wf, j = pb - r0;
-                    while (m) {
-                        const int b = (__ffs(m) - 1) >> 2;
-                        m &= m - 1;
-                        if (j < 4u) task[j] = (uint32_t(lane) << 4) | uint32_t(b);
-                        j++;
-                    }
-                    wave_sync();
-                    if (uint32_t(lane >> 4) < tb - r0) {
-                        const uint32_t tk = task[lane >> 4];
-                        const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
-                        const BlockPx<N> px = block_px(b, owner);
-                        const int y = exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
-                                                        srow[NN * NN + 2 * NN + k], px);
-                        res[lane] = uint32_t(y) & 0xFFFFu;
-                    }
-                    wave_sync();
-                    m = wf;
-                    j = pb - r0;
-                    while (m) {
-                        const int b = (__ffs(m) - 1) >> 2;
-                        m &= m - 1;
-                        if (j < 4u) {
-                            const uint32_t* rr = res + 16 * j;
-#pragma unroll
-                            for (int jj = 0; jj < NP; jj++) {
-                                const uint32_t w = rr[ZigZag<N>::idx[2 * jj]] | (rr[ZigZag<N>::idx[2 * jj + 1]] << 16);
-#pragma unroll
-                                for (int bb = 0; bb < NS; bb++) zp[bb][jj] = (b == bb) ? w : zp[bb][jj];
-                            }
-                        }
-                        j++;
-                    }
-                    wave_sync();
-                }
-            }
-        }
-        {  // statistics: FP64 requests of this wave (one store)
-            const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan_dpp(uint32_t(__popc(flags))), 63);
-            if (lane == 0) a.wave_fix[size_t(t) * (TPB / 64) + wv] = wsum;
-        }
-        WSTAMP(3);
-        asm volatile("; PHASE p3" ::: "memory");
-
-        // -------------------------------------------------------- sizing + the wave's offsets
-        uint32_t blw[NS], rb[NS];
-        const uint32_t k0 = uint32_t(tif * TG + GW * wv) * 4u;  // the wave's first block (frame raster order)
-#pragma unroll
-        for (int b = 0; b < NS; b++) {
-            const bool valid = 64 * b + lane < nbw;
-            if (a.coef && valid) {
-                int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + k0 + 64 * b + lane) * NN;
-#pragma unroll
-                for (int k = 0; k < NN; k++) {
-                    const int kz = ZigZagInv<N>::pos[k];
-                    dst[k] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            blw[b] = IE_P_SIZE4 ? size_block4(zp[b], a.rle, &rb[b]) : size_block<N>(zp[b], a.rle, &rb[b]);
-            rb[b] = valid ? rb[b] : 0u;
-            asm volatile("" : "+v"(blw[b]), "+v"(rb[b]));
-#pragma unroll
-            for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        uint32_t T[NS], off[NS];
-#pragma unroll
-        for (int h = 0; h < NS / 2; h++) {  // two slots per 32-bit scan (16-bit halves)
-            const uint32_t sv = rb[2 * h] | (rb[2 * h + 1] << 16);
-            const uint32_t iv = wave_incl_scan_dpp(sv);
-            const uint32_t tv = __builtin_amdgcn_readlane(iv, 63), ev = iv - sv;
-            T[2 * h] = tv & 0xFFFFu;
-            T[2 * h + 1] = tv >> 16;
-            off[2 * h] = ev & 0xFFFFu;
-            off[2 * h + 1] = ev >> 16;
-        }
-        uint32_t Sb[NS];  // slot starts in the wave image
-        Sb[0] = 0u;
-#pragma unroll
-        for (int b = 1; b < NS; b++) Sb[b] = Sb[b - 1] + T[b - 1];
-        const uint32_t Tw = Sb[NS - 1] + T[NS - 1];
-        const uint32_t S2 = NS == 4 ? Sb[2] : Sb[1];  // the end of slot pair 0 (8 waves: slot 0)
-        // The tile's bit count: wave 0 alone waits for the four waves' counts (their flags in
-        // misc[16..19], cleared before the tile) and publishes it; the other waves go on to their
-        // emission and learn their place in the tile after the position barrier.  (A launch too
-        // small to fill the chip -- deep look-back -- keeps a workgroup barrier here: all four
-        // waves read predecessor windows.)
-        if (lane == 0) {
-            misc[wv] = Tw;
-            __hip_atomic_store(&misc[ML::F + wv], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        WSTAMP(4);
-        asm volatile("; PHASE p4" ::: "memory");
-        if (deep || IE_P_CNTBAR) {
-            lds_barrier();
-        } else if (wv == 0) {
-            for (;;) {
-                uint32_t all = 1u;
-#pragma unroll
-                for (int q = 0; q < WPT / 4; q++) {
-                    const u32x4 f = *reinterpret_cast<const volatile u32x4*>(misc + ML::F + 4 * q);
-                    all &= f.x & f.y & f.z & f.w;
-                }
-                if (__builtin_amdgcn_readfirstlane(all)) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
-        WSTAMP(5);
-        asm volatile("; PHASE p5" ::: "memory");
-
-        uint32_t A = 0;  // (wave 0, or every wave in deep mode; the others after the position barrier)
-#pragma unroll
-        for (int w = 0; w < WPT; w++) A += __builtin_amdgcn_readfirstlane(misc[w]);
-        if (tid == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);
-        constexpr int DW = 2;
-        Probe pr[DW];
-#pragma unroll
-        for (int i = 0; i < DW; i++) pr[i] = Probe{0, 0, 0};
-        if (chain_pos != 0) {
-            if (deep) {
-#pragma unroll
-                for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
-            } else if (wv == 0 && !IE_P_LATEPROBE) {
-                pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
-            }
-        }
-
-        const uint32_t reg_bit0 = uint32_t(wv * RW) * 32u;
-        auto zero_img = [&](uint32_t bits) {
-            const uint32_t nq = (bits + 127u) >> 7;  // 16-byte groups
-            uint32_t z;
-            asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // (a zero vector hoisted out of the tile loop was spilled)
-            for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(reg + 4 * q) = u32x4{z, z, z, z};
-        };
-        // The wave's whole image fits its region (the last record's trailing zero fields reach at
-        // most rec_bits past its start, plus the 64-bit window): all four slots are emitted before
-        // the position barrier -- beside wave 0's look-back -- and stored in one pass after it.
-        // Otherwise slot pairs in turn (pair 1 after pair 0 is stored).
-        const bool whole = Tw + uint32_t(a.rec_bits) + 64u <= 32u * RW;
-        auto emit_slot = [&](int b) {  // slot b at its place in the (whole or pair) image
-            if (!(IE_P_ABL & 2) && rb[b]) {
-                const uint32_t p = reg_bit0 + (whole ? Sb[b] : Sb[b] - Sb[(b / PS) * PS]) + off[b];
-                if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
-                else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
-            }
-        };
-        zero_img(whole ? Tw : S2);
-        wave_sync();
-#pragma unroll
-        for (int b = 0; b < PS; b++) emit_slot(b);
-        // (A/B builds) the first probe issued half-way through the emission: predecessors that
-        // started just before this tile have had that much longer to publish their counts
-        if (IE_P_LATEPROBE && !deep && wv == 0 && chain_pos != 0) pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
-        if (whole) {
-#pragma unroll
-            for (int b = PS; b < NS; b++) emit_slot(b);
-        }
-        wave_sync();
-        WSTAMP(6);
-        asm volatile("; PHASE p6" ::: "memory");
-        if (lane == 0 && Tw) misc[ML::H + wv] = reg[0];  // the wave's first 32 bits
-
-        // -------------------------------------------------------- look-back (wave 0)
-        const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
-        uint32_t* const out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
-        if (deep && chain_pos != 0) {
-            uint64_t sm = 0;
-            bool found = false;
-            unsigned spins = 0;
-            for (;;) {
-                bool ready = true;
-                sm = 0;
-                found = false;
-#pragma unroll
-                for (int i = 0; i < DW; i++) {
-                    const WinSum r = window_sum(pr[i], chain_pos, 64 * (DW * wv + i), 64, a.tag);
-                    if (!found) {
-                        ready = ready && r.ready;
-                        sm += r.sum;
-                        found = r.found;
-                    }
-                }
-                if (ready) break;
-                if (++spins > kSpinLimit) {
-                    if (lane == 0) atomicAdd(&a.err[0], 1u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-                for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
-            }
-            if (lane == 0) {
-                misc[ML::D + 2 * wv] = uint32_t(sm);
-                misc[ML::D + 2 * wv + 1] = uint32_t(sm >> 32);
-                misc[ML::FD + wv] = found ? 1u : 0u;
-            }
-            lds_barrier();
-        }
-        if (wv == 0) {
-            uint64_t excl = 0;
-            uint32_t ptail = 0, pend = 0;
-            if (chain_pos == 0) {
-                const uint32_t s = uint32_t(start_bit & 31);
-                ptail = s ? (bswap32(out[start_bit >> 5]) >> (32 - s)) : 0u;
-            } else {
-                bool done = false;
-                if (deep) {
-#pragma unroll
-                    for (int w = 0; w < WPT; w++) {
-                        if (!done) {
-                            excl += uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::D + 2 * w]))) |
-                                    (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::D + 2 * w + 1]))) << 32);
-                            done = __builtin_amdgcn_readfirstlane(misc[ML::FD + w]) != 0;
-                        }
-                    }
-                    if (!done) excl = 0;
-                }
-                if (!done) {
-                    const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr[0];
-                    excl = (IE_P_ABL & 4) ? uint64_t(chain_pos) * 30000u
-                                          : lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
-                }
-                const bool have = (!IE_P_XCHG || deep) && uint32_t(pr[0].gt >> 56) == a.tag;
-                const bool split = ((start_bit + excl) & 31) != 0;
-                ptail = have ? uint32_t(pr[0].gt) : 0u;
-                pend = (!have && split) ? 1u : 0u;  // (IE_P_XCHG: the boundary word by exchange)
-            }
-            if (lane == 0) {
-                if (chain_pos != 0) publish(a.st, t, 1, a.tag, excl + A);
-                misc[ML::E] = uint32_t(excl);
-                misc[ML::E + 1] = uint32_t(excl >> 32);
-                misc[ML::PT] = ptail;
-                misc[ML::PD] = pend;
-                const uint64_t P = start_bit + excl;
-                if (tif == 0) a.frame_start[frame] = P;
-                if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
-            }
-        }
-        WSTAMP(7);
-        asm volatile("; PHASE p7" ::: "memory");
-        lds_barrier();  // ---- the tile's position
-        WSTAMP(8);
-        asm volatile("; PHASE p8" ::: "memory");
-        uint32_t W = 0;
-        A = 0;
-#pragma unroll
-        for (int w = 0; w < WPT; w++) {
-            const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
-            A += v;
-            W += (w < wv) ? v : 0u;
-        }
-        // every wave is past the previous tile: its count flags (the other copy) are free again
-        if (lane == 0) misc0[((iter + 1) & 1) * ML::S + ML::F + wv] = 0u;
-
-        // -------------------------------------------------------- store, slot pair by slot pair
-        // The next tile is claimed only now (wave 0: the atomic here, resolved after its first
-        // store, published in misc[13] with bit 31 set; the other waves read it when they have
-        // stored): a claim made a whole tile ahead let a tile start up to a tile's time after its
-        // successor had, whose look-back then waited for it (measured 2x slower).
-        unsigned kclaim = 0;
-        if (dyn && wv == 0 && lane == 0) kclaim = atomicAdd(&cnt[kClaimStride * chain], 1u);
-        bool claimed = !dyn || wv != 0;
-        auto resolve_claim = [&]() {
-            if (!claimed) {
-                const int tn = claim_resolve(cnt, nch, tpc, seg, &chain, kclaim);
-                if (lane == 0) misc[ML::CL] = 0x80000000u | uint32_t(tn);
-                claimed = true;
-            }
-        };
-        auto next_tile = [&]() -> int {
-            if (!dyn) return a.ntiles;
-            uint32_t v;
-            for (;;) {  // (wave 0 sets it right after its first store: a short wait at most)
-                v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&misc[ML::CL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (v & 0x80000000u) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            return v == 0xFFFFFFFFu ? -1 : int(v & 0x7FFFFFFFu);
-        };
-        int t_next = -1;
-        if (Tw) {
-            const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::E]))) |
-                                  (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::E + 1]))) << 32);
-            const uint64_t Xw = start_bit + excl + W;
-            const bool pend = __builtin_amdgcn_readfirstlane(misc[ML::PD]) != 0u;
-            const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
-            uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[ML::PT]) : 0u;
-            const HistCountT<HR> hc{hl, chain_last ? (start_bit + excl + A + 7) / 8 : ~0ull, uint32_t(lane % HR)};
-            auto count = [&](uint64_t gw, uint32_t v) {
-                if constexpr (HIST) hc(gw, v);
-            };
-            auto store_pair = [&](uint32_t S0, uint32_t n) {
-                if (!n || (IE_P_ABL & 8)) return;
-                const uint64_t Xb = Xw + S0;
-                const uint32_t nw = uint32_t(((Xb + n) >> 5) - (Xb >> 5));
-                if constexpr (HIST) store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane, hc);
-                else store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
-                prev = slot_tail32(reg, n, prev);
-            };
-            if constexpr (HIST) {
-                if (wv == 0 && chain_pos == 0)
-                    for (uint32_t i = lane; i < uint32_t(start_bit >> 5); i += 64) hc(i, out[i]);
-            }
-            const uint64_t E = Xw + Tw;
-            const uint32_t e = uint32_t(E) & 31u;
-            // (IE_P_XCHG) the tile's boundary words by exchange, issued before the stores so that
-            // their round trips overlap them: the first (wave 0, pend) and the last (wave wlast)
-            // (a launch too small to fill the chip -- deep -- keeps the published tails: its tiles end
-            // together, and the exchange's round trip would sit at every one's end)
-            const bool xs = IE_P_XCHG && !deep && wv == 0 && pend;
-            const bool xp = IE_P_XCHG && !deep && wv == wlast && e != 0u && !chain_last;
-            const uint32_t s0 = uint32_t(Xw) & 31u;
-            const uint32_t headS = xs ? (uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::H])) >> s0) : 0u;
-            uint64_t oldS = 0, oldP = 0;
-            if (xs && lane == 0) oldS = boundary_swap(a.st, t, a.tag, 2u, headS);
-            if (xp && whole) {
-                const uint32_t tw = slot_tail32(reg, Tw, prev);  // (= prev after the store)
-                if (lane == 0) oldP = boundary_swap(a.st, t + step, a.tag, 1u, tw << (32u - e));
-            }
-            store_pair(0u, whole ? Tw : S2);
-            resolve_claim();
-            WSTAMP(9);
-            asm volatile("; PHASE p9" ::: "memory");
-            if (!whole && Tw > S2) {
-                wave_sync();  // pair 0's image has been read
-                zero_img(Tw - S2);
-                wave_sync();
-#pragma unroll
-                for (int b = PS; b < NS; b++) emit_slot(b);
-                wave_sync();
-                store_pair(S2, Tw - S2);
-            }
-            if (xp && !whole && lane == 0) oldP = boundary_swap(a.st, t + step, a.tag, 1u, prev << (32u - e));
-            const uint32_t nexthead = (e && wv < wlast) ? misc[ML::H + wv + 1] : 0u;
-            // every read of this wave's region is complete (the stores consumed it): the next
-            // tile's pixels may land there now
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            t_next = next_tile();
-            if (t_next >= 0 && t_next < a.ntiles) issue_pixels(a, t_next);
-            if (lane == 0) {
-                if (e && (wv < wlast || chain_last)) {  // the wave's last, partial word
-                    const uint32_t v = bswap32((prev << (32u - e)) | (nexthead >> e));
-                    out[E >> 5] = v;
-                    count(E >> 5, v);
-                }
-                if ((!IE_P_XCHG || deep) && wv == wlast) publish(a.st, t, 2, a.tag, prev);  // the tile's last 32 bits
-                if ((!IE_P_XCHG || deep) && wv == 0 && pend) {  // the first word, with the predecessor's tail
-                    const uint32_t pt = wait_tail(a.st, t - step, a.tag, a.err);
-                    const uint32_t s = uint32_t(Xw) & 31u;
-                    const uint32_t v = bswap32((pt << (32u - s)) | (misc[ML::H] >> s));
-                    out[Xw >> 5] = v;
-                    count(Xw >> 5, v);
-                }
-                uint32_t v;
-                if (xs && boundary_second(oldS, a.tag, 2u, headS, &v)) {
-                    out[Xw >> 5] = v;
-                    count(Xw >> 5, v);
-                }
-                if (xp && boundary_second(oldP, a.tag, 1u, prev << (32u - e), &v)) {
-                    out[E >> 5] = v;
-                    count(E >> 5, v);
-                }
-            }
-            WSTAMP(10);
-            asm volatile("; PHASE p10" ::: "memory");
-            WRTSTAMP(15);
+            for (int k = 0; k < NN; k++) x[k] = float((reg[(k >> 2) * BW + 64 * b + lane] >> (8 * (k & 3))) & 0xFFu) * 0.015625f;
+            emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
         } else {
-            resolve_claim();
-            t_next = next_tile();
-            if (t_next >= 0 && t_next < a.ntiles) issue_pixels(a, t_next);
-        }
-        const bool more = t_next >= 0 && t_next < a.ntiles;
-        if constexpr (HIST) {
-            lds_barrier();  // every wave's bytes counted
-            uint32_t c = 0;
-#pragma unroll
-            for (int r = 0; r < HR; r++) c += hl[tid * HR + r];
-            if (c) atomicAdd(&a.hist[size_t(frame) * 256 + tid], c);
-            if (more) {  // (the next tile adds after two barriers; a zero vector held across the tile
-                         // loop was spilled: 16 B per lane stored per tile, ~30 MB per C5 launch)
-                uint32_t z;
-                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-#pragma unroll
-                for (int r = 0; r < HR; r++) hl[tid * HR + r] = z;
-            }
-        }
-        if (!more) break;
-        t = t_next;
-    }
-    leave();
-}
-
-// =============================================================================================
-// encode4q_kernel -- encode4p_kernel's tile, SOFTWARE-PIPELINED over a persistent grid.
-//   * Grid = the workgroups the chip holds at once (occupancy API, capped at IE_Q_PER_CU per CU);
-//     workgroup w takes tiles w, w + G, w + 2G, ... in that order (static: no claim atomics).  A
-//     tile's look-back waits only on tiles of earlier rounds or of earlier workgroups of its own
-//     round -- all resident -- so the order cannot deadlock.
-//   * Two pixel/image buffers per wave: tile k+1's pixels land by DMA while tile k is worked on.
-//   * Deferred back end: iteration k runs front(k) (transform, FP64 fix-up, sizing, the count),
-//     then back(k-1) (look-back, position barrier, store), then the DMA of tile k+1, then
-//     emit(k).  A tile's look-back thus runs a whole front stage after its predecessors
-//     published their counts (and after the round before published its inclusive prefixes), and
-//     the probe it evaluates (issued when the iteration starts) has had that long to return.
-//     Only a tile with a wave image too large for the buffer (slot pairs in turn) runs its back
-//     end at once.
-//   * Tile boundary word: the word holding a tile's first bits and its predecessor's last is
-//     written by whichever of the two reaches it second, found by ONE 64-bit exchange on the
-//     successor's granule 3 (atomics on one address are ordered: exactly one of the two sees the
-//     other's half) -- no tile waits for its predecessor's tail.
-// =============================================================================================
-#ifndef IE_ENC_Q
-#define IE_ENC_Q 1  // 0: (A/B builds) large 4x4 FAST batches on encode4p_kernel
-#endif
-#ifndef IE_Q_PER_CU
-#define IE_Q_PER_CU 4
-#endif
-#ifndef IE_Q_PROBE
-#define IE_Q_PROBE 64  // first look-back window of a deferred back end (predecessors)
-#endif
-constexpr int kQMisc = 3 * 32;  // three copies of encode4w_kernel's misc words (tile k: copy k % 3)
-constexpr int kQLdsBytes = (8 * kWReg + 4 * kWTask + kQMisc + kPWfrag) * 4 + kWRows * 8;
-
-__global__ __launch_bounds__(256, IE_Q_PER_CU) void encode4q_kernel(EncArgs a_, const EncTables* __restrict__ tab) {
-    constexpr int N = 4, NN = 16, NP = 8, TPB = 256, NS = 4;
-    constexpr int GW = 16 * NS, BW = 64 * NS, TG = 4 * GW;  // groups / blocks per wave, groups per tile
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int tid0 = threadIdx.x;
-    const int wv = __builtin_amdgcn_readfirstlane(tid0 >> 6);
-    uint32_t* const task = smem + 8 * kWReg + wv * kWTask;
-    uint32_t* const res = task + 64;
-    uint32_t* const misc0 = smem + 8 * kWReg + 4 * kWTask;  // [3][32]
-    uint32_t* const wl = misc0 + kQMisc;                    // [64][4]: the matrix-pipe A fragments
-    double* const srow = reinterpret_cast<double*>(wl + kPWfrag);
-    const int G = int(gridDim.x);
-    const int wg = int(blockIdx.x);
-    using KArgs = const __attribute__((address_space(4))) EncArgs;
-    KArgs* ka = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
-    // tiles by per-chain claims (encode4p_kernel's counters and claim_resolve), made two tiles
-    // ahead: tile k+2 is claimed when iteration k starts and resolved when tile k+1's pixels are
-    // requested; misc copy k % 3 word 13 holds tile k (-1: none)
-    const bool seg = a_.segmented != 0;
-    const int nch = seg ? a_.nframes : 1, tpc = seg ? a_.tiles_per_frame : a_.ntiles;
-    unsigned* const cnt = a_.claim;
-    int chain = wg % nch;  // (wave 0's copy counts)
-    bool claiming = true;
-    // wave wv's buffer par (0/1): pixels [4 rows][BW], then the tile's wave image
-    auto bufp = [&](int par) { return smem + (par * 4 + wv) * kWReg; };
-    auto issue_pixels = [&](KArgs& a, int tt, int par) {
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const TileGeo gg = tile_geo<4, 4, TG>(a, tt, tid);
-        if (gg.nblk) {
-            uint32_t* const reg = bufp(par);
-            const uint8_t* base = a.y + size_t(gg.frame) * a.frame_pitch + size_t(gg.byi) * N * a.stride + size_t(gg.bx0) * N;
-#pragma unroll
-            for (int r = 0; r < N; r++)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * a.stride),
-                                                 (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, 0);
-        }
-    };
-    {
-        const int lane0 = tid0 & 63;
-        static_assert(kWRows * 8 == 2 * 1024 + 24 * 16, "rows: two full waves and 24 lanes of 16 bytes");
-        if (wv < 2 || (wv == 2 && lane0 < 24))
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->rows4[wv * 128 + 2 * lane0]),
-                                             (__attribute__((address_space(3))) void*)(srow + wv * 128), 16, 0, 0);
-        else if (wv == 3)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(&tab->mfma_w[lane0][0]),
-                                             (__attribute__((address_space(3))) void*)(wl), 16, 0, 0);
-    }
-    if ((tid0 & 63) == 0) {  // the waves' count flags of the three misc copies
-#pragma unroll
-        for (int c = 0; c < 3; c++) misc0[32 * c + 16 + wv] = 0u;
-    }
-    if (wv == 0) {  // the first two tiles: two positions of the workgroup's chain by one atomic
-        unsigned k0 = 0;
-        if ((tid0 & 63) == 0) k0 = atomicAdd(&cnt[kClaimStride * chain], 2u);
-        const int k0u = __builtin_amdgcn_readfirstlane(int(k0));
-        int ta = -1, tb2 = -1;
-        if (k0u + 1 < tpc) {
-            ta = seg ? k0u * nch + chain : k0u;
-            tb2 = seg ? (k0u + 1) * nch + chain : k0u + 1;
-        } else {  // (the chain ends here: the next chains by claim_resolve)
-            ta = claim_resolve(cnt, nch, tpc, seg, &chain, k0);
-            if (ta >= 0) {
-                unsigned kn = 0;
-                if ((tid0 & 63) == 0) kn = atomicAdd(&cnt[kClaimStride * chain], 1u);
-                tb2 = claim_resolve(cnt, nch, tpc, seg, &chain, kn);
-            }
-        }
-        claiming = tb2 >= 0;
-        if ((tid0 & 63) == 0) {
-            misc0[13] = uint32_t(ta);
-            misc0[32 + 13] = uint32_t(tb2);
-        }
-    }
-    const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
-    lds_barrier();  // the first two tiles known
-    {
-        const int ta = __builtin_amdgcn_readfirstlane(int(misc0[13])), tb2 = __builtin_amdgcn_readfirstlane(int(misc0[32 + 13]));
-        if (ta >= 0) issue_pixels(*ka, ta, 0);
-        if (tb2 >= 0) issue_pixels(*ka, tb2, 1);
-    }
-    // (every workgroup counts its exit; the last one leaves the claim counters zero)
-    auto leave = [&]() {
-        if (tid0 == 0) {
-            const unsigned e = atomicAdd(&cnt[kClaimStride * nch], 1u);
-            if (e == unsigned(G) - 1u) {
-                for (int c = 0; c <= nch; c++) __hip_atomic_store(&cnt[kClaimStride * c], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    };
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();  // the rows, the A fragments visible
-
-    // the front stage's results (one tile at a time; function scope for back()'s slot-pair case)
-    uint32_t zp[NS][NP], blw[NS], rb[NS], off[NS];
-    uint32_t S2 = 0, S3 = 0;
-
-    // -------------------------------------------------------- the back end of tile tt
-    // (position: wave 0's look-back; every wave's store; the tile-boundary exchanges)
-    // now: the tile of this iteration (its image may be in slot pairs: zp of slots 2-3 live)
-    int qst = 0;  // (profiling builds) the tile whose stamp row this iteration fills
-#define QSTAMP(i)                                                                                         \
-    do {                                                                                                  \
-        if (IE_PROFILE && a.stamps && (threadIdx.x & 63) == 0) a.stamps[size_t(qst) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#define QRTSTAMP(i)                                                                                       \
-    do {                                                                                                  \
-        if (IE_PROFILE && a.stamps && (threadIdx.x & 63) == 0) a.stamps[size_t(qst) * kStamps + wv * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-    auto back = [&](int tt, int kk, bool now, const Probe& p0) {
-        asm volatile("" : "+s"(ka));
-        KArgs& a = *ka;
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const int lane = tid & 63;
-        const TileGeo gb = tile_geo<4, 4, TG>(a, tt, tid);
-        const int bframe = gb.frame, btif = gb.tif, bstep = gb.step, bpos = gb.chain_pos;
-        const int bng = min(TG, a.groups_per_frame - btif * TG);
-        const int wlast = (bng - 1) / GW;  // the tile's last non-empty wave
-        uint32_t* const bm = misc0 + (kk % 3) * 32;
-        uint32_t* const breg = bufp(kk & 1);
-        const bool chain_last = a.segmented ? (btif == a.tiles_per_frame - 1) : (tt == a.ntiles - 1);
-        uint32_t* const out = a.out + (a.segmented ? uint64_t(bframe) * a.out_pitch_words : 0ull);
-        if (wv == 0) {
-            uint32_t A = 0;
-#pragma unroll
-            for (int w = 0; w < 4; w++) A += __builtin_amdgcn_readfirstlane(bm[w]);
-            uint64_t excl = 0;
-            uint32_t ptail = 0, pend = 0;
-            if (bpos == 0) {
-                const uint32_t s = uint32_t(start_bit & 31);
-                ptail = s ? (bswap32(out[start_bit >> 5]) >> (32 - s)) : 0u;
-            } else {
-                const Probe q = now ? probe_issue(a.st, tt, bpos, bstep, 0, IE_Q_PROBE) : p0;
-                QSTAMP(12);
-                unsigned rounds = 0;
-                excl = lookback_wave<IE_W_AHEAD>(q, a.st, tt, bpos, bstep, a.tag, a.err, IE_PROFILE ? &rounds : nullptr, false, IE_Q_PROBE);
-                pend = ((start_bit + excl) & 31) != 0 ? 1u : 0u;  // the boundary word: exchanged
-                if (IE_PROFILE && a.stamps && lane == 0) a.stamps[size_t(qst) * kStamps + 13] = rounds;
-            }
-            QSTAMP(5);
-            if (lane == 0) {
-                if (bpos != 0) publish(a.st, tt, 1, a.tag, excl + A);
-                bm[8] = uint32_t(excl);
-                bm[9] = uint32_t(excl >> 32);
-                bm[10] = ptail;
-                bm[11] = pend;
-                const uint64_t P = start_bit + excl;
-                if (btif == 0) a.frame_start[bframe] = P;
-                if (chain_last) a.chain_end[a.segmented ? bframe : 0] = P + A;
-            }
-        }
-        lds_barrier();  // ---- the tile's position
-        QSTAMP(6);
-        uint32_t W = 0;
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const uint32_t v = __builtin_amdgcn_readfirstlane(bm[w]);
-            W += (w < wv) ? v : 0u;
-        }
-        const uint32_t bTw = __builtin_amdgcn_readfirstlane(bm[wv]);
-        if (!bTw) return;
-        const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(bm[8]))) |
-                              (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(bm[9]))) << 32);
-        const uint64_t Xw = start_bit + excl + W;
-        const bool pend = __builtin_amdgcn_readfirstlane(bm[11]) != 0u;
-        const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
-        uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(bm[10]) : 0u;
-        const bool whole = bTw + uint32_t(a.rec_bits) + 64u <= 32u * kWReg;
-        const uint64_t E = Xw + bTw;
-        const uint32_t e = uint32_t(E) & 31u;
-        // the boundary exchanges, issued before the stores (their round trip overlaps them)
-        const bool xs = wv == 0 && pend;                                 // this tile's first word
-        const bool xp = wv == wlast && e != 0u && !chain_last;           // its last word
-        const uint32_t s0 = uint32_t(Xw) & 31u;
-        const uint32_t head = __builtin_amdgcn_readfirstlane(bm[4 + wv]);
-        uint64_t oldS = 0, oldP = 0;
-        if (lane == 0 && xs) oldS = boundary_swap(a.st, tt, a.tag, 2u, head >> s0);
-        if (xp && whole) {
-            const uint32_t tw = slot_tail32(breg, bTw, prev);  // (= prev after the store)
-            if (lane == 0) oldP = boundary_swap(a.st, tt + bstep, a.tag, 1u, tw << (32u - e));
-        }
-        auto store_pair = [&](uint32_t S0, uint32_t n) {
-            if (!n) return;
-            const uint64_t Xb = Xw + S0;
-            const uint32_t nw = uint32_t(((Xb + n) >> 5) - (Xb >> 5));
-            store_slot(out, breg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
-            prev = slot_tail32(breg, n, prev);
-        };
-        if (whole) {
-            store_pair(0u, bTw);
-        } else if (now) {  // (slot pairs in turn: the zp of slots 2-3 are this iteration's)
-            store_pair(0u, S2);
-            if (bTw > S2) {
-                wave_sync();  // pair 0's image has been read
-                const uint32_t nq = (bTw - S2 + 127u) >> 7;
-                uint32_t z;
-                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-                for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(breg + 4 * q) = u32x4{z, z, z, z};
-                wave_sync();
-                const uint32_t reg_bit0 = uint32_t(((kk & 1) * 4 + wv) * kWReg) * 32u;
-#pragma unroll
-                for (int b = 2; b < 4; b++) {
-                    if (rb[b]) {
-                        const uint32_t p = reg_bit0 + (b == 2 ? 0u : (S3 - S2)) + off[b];
-                        if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
-                        else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
-                    }
-                }
-                wave_sync();
-                store_pair(S2, bTw - S2);
-            }
-            if (lane == 0 && xp) oldP = boundary_swap(a.st, tt + bstep, a.tag, 1u, prev << (32u - e));
-        }
-        const uint32_t nexthead = (e && wv < wlast) ? bm[4 + wv + 1] : 0u;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (every read of the buffer is done)
-        QSTAMP(7);
-        if (lane == 0) {
-            if (e && (wv < wlast || chain_last)) out[E >> 5] = bswap32((prev << (32u - e)) | (nexthead >> e));
-            if (xs) boundary_finish(out, Xw >> 5, oldS, a.tag, 2u, head >> s0);
-            if (xp) boundary_finish(out, E >> 5, oldP, a.tag, 1u, prev << (32u - e));
-        }
-    };
-
-    Probe prc{0, 0, 0};     // wave 0: the first look-back probe of the tile whose back end is deferred
-    bool deferred = false;  // the previous tile's back end is still to run
-    int t_prev = -1, klast = 0;
-    for (int k = 0;; k++) {
-        asm volatile("" : "+s"(ka));
-        KArgs& a = *ka;
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const int lane = tid & 63;
-        uint32_t* const misc = misc0 + (k % 3) * 32;
-        const int t = __builtin_amdgcn_readfirstlane(int(misc[13]));
-        if (t < 0) break;
-        uint32_t* const reg = bufp(k & 1);
-        unsigned kc = 0;  // wave 0: the claim of tile k + 2, resolved at tile k+1's pixel request
-        if (wv == 0 && claiming && lane == 0) kc = atomicAdd(&cnt[kClaimStride * chain], 1u);
-        const TileGeo g = tile_geo<4, 4, TG>(a, t, tid);
-        const int frame = g.frame, tif = g.tif, chain_pos = g.chain_pos;
-        const int ng = min(TG, a.groups_per_frame - tif * TG);
-        const int nbw = 4 * min(GW, max(0, ng - GW * wv));  // blocks of this wave
-        qst = t;
-        QRTSTAMP(14);
-        QSTAMP(11);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's pixels (and every older access)
-        QSTAMP(0);
-        // the deferred tile's first probe, in flight during this tile's front stage
-        if (deferred && wv == 0) {
-            const int tp = t_prev;
-            const TileGeo gp = tile_geo<4, 4, TG>(a, tp, tid);
-            if (gp.chain_pos != 0) prc = probe_issue(a.st, tp, gp.chain_pos, gp.step, 0, IE_Q_PROBE);
-        }
-
-        // -------------------------------------------------------- front: transform + quantise
-        using KTab = const __attribute__((address_space(4))) EncTables;
-        KTab* tb = (KTab*)(tab);
-        asm volatile("" : "+s"(tb));
-        const bool dcx = tb->dc_exact4j != 0;
-        const float lim_s0 = tb->lim4j[Structural<4>::k[0]], lim_s1 = tb->lim4j[Structural<4>::k[1]],
-                    lim_s2 = tb->lim4j[Structural<4>::k[2]], lim_min = tb->lim_min4j;
-        uint32_t flags = 0;  // 4 bits per slot: structural s (bits 0-2), whole block (bit 3)
-#pragma unroll
-        for (int b = 0; b < NS; b++) {
-            __builtin_amdgcn_sched_barrier(0);
-            uint32_t sf;
             v4i32 px;
 #pragma unroll
             for (int r = 0; r < N; r++) px[r] = int(reg[r * BW + 64 * b + lane] ^ 0x80808080u);  // x - 128 as i8
@@ -3104,312 +2108,404 @@ __global__ __launch_bounds__(256, IE_Q_PER_CU) void encode4q_kernel(EncArgs a_, 
             const v16i32 Jc = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfrag, px, v16i32{}, 0, 0, 0);
             float Jf[16], x[16];
 #pragma unroll
-            for (int kk = 0; kk < 16; kk++) Jf[kk] = float(Jc[kk]);
+            for (int k = 0; k < 16; k++) Jf[k] = float(Jc[k]);
             quot4j(Jf, x, tb->plan4j, FloatOp());
-            const float emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
-            const uint32_t fb = (emax >= lim_min) ? 8u : sf;
-            if (64 * b + lane < nbw) flags |= fb << (4 * b);
-#pragma unroll
-            for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
-            asm volatile("" : "+v"(flags));
+            emax = round_block_lean4j(x, zp[b], &sf, dcx, lim_s0, lim_s1, lim_s2);
         }
-
-        QSTAMP(1);
-        // -------------------------------------------------------- FP64 fix-up (encode4p_kernel's)
-        auto block_px = [&](int b, int owner) {
-            BlockPx<N> px;
+        const uint32_t fb = (emax >= lim_min) ? 8u : sf;
+        if (64 * b + lane < nbw) flags |= fb << (4 * b);
 #pragma unroll
-            for (int r = 0; r < N; r++) px.w[r] = reg[r * BW + 64 * b + owner];
-            return px;
-        };
-        if (__ballot(flags != 0)) {
-            const uint32_t sf = flags & 0x7777u;
-            const uint32_t cnt = __popc(sf);
-            const uint32_t incl = wave_incl_scan_dpp(cnt);
-            const uint32_t pre = incl - cnt, total = __builtin_amdgcn_readlane(incl, 63);
-            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
-                uint32_t m = sf, i = pre - r0;
+        for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
+        asm volatile("" : "+v"(flags));
+    }
+    WSTAMP(2);
+    asm volatile("; PHASE p2" ::: "memory");
+
+    // ------------------------------------------------------------ FP64 fix-up (encode4w_kernel's)
+    lane = fresh_lane();
+    auto block_px = [&](int b, int owner) {
+        BlockPx<N> px;
+#pragma unroll
+        for (int r = 0; r < N; r++) px.w[r] = reg[r * BW + 64 * b + owner];
+        return px;
+    };
+    if (!(IE_P_ABL & 1) && __ballot(flags != 0)) {
+        const uint32_t sf = flags & 0x7777u;
+        const uint32_t cnt = __popc(sf);
+        // the lanes' request counts placed by one DPP wave scan
+        const uint32_t incl = wave_incl_scan_dpp(cnt);
+        const uint32_t pre = incl - cnt;
+        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+            uint32_t m = sf, i = pre - r0;
+            while (m) {
+                const int bit = __ffs(m) - 1;
+                m &= m - 1;
+                if (i < 64u) task[i] = (uint32_t(lane) << 4) | uint32_t(bit);
+                i++;
+            }
+            wave_sync();
+            if (uint32_t(lane) < total - r0) {
+                const uint32_t tk = task[lane];
+                const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
+                const BlockPx<N> px = block_px(b, owner);
+                const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
+                const int y = (IE_P_ABL & 32) ? int(px.w[0] & 1u)  // (profiling) no FP64 arithmetic (a small value: records stay in bound)
+                                              : exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                                  srow[NN * NN + 2 * NN + k], px);
+                res[lane] = uint32_t(y) & 0xFFFFu;
+            }
+            wave_sync();
+            i = pre - r0;
+#pragma unroll
+            for (int b = 0; b < NS; b++)
+#pragma unroll
+                for (int ss = 0; ss < 3; ss++) {
+                    if ((sf >> (4 * b + ss)) & 1u) {
+                        const int zw = Structural<N>::zpos(ss) >> 1;
+                        if (i < 64u) zp[b][zw] = __builtin_amdgcn_perm(res[i], zp[b][zw], 0x05040100u);  // res low -> high half
+                        i++;
+                    }
+                }
+            wave_sync();
+        }
+        const uint32_t wf = flags & 0x8888u;
+        if (__ballot(wf != 0)) {
+            const uint32_t nb = __popc(wf);
+            uint32_t pb = 0, tb = 0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {  // nb <= 4
+                const uint64_t bm = __ballot((nb >> k) & 1u);
+                pb += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << k;
+                tb += uint32_t(__popcll(bm)) << k;
+            }
+            for (uint32_t r0 = 0; r0 < tb; r0 += 4) {
+                uint32_t m = wf, j = pb - r0;
                 while (m) {
-                    const int bit = __ffs(m) - 1;
+                    const int b = (__ffs(m) - 1) >> 2;
                     m &= m - 1;
-                    if (i < 64u) task[i] = (uint32_t(lane) << 4) | uint32_t(bit);
-                    i++;
+                    if (j < 4u) task[j] = (uint32_t(lane) << 4) | uint32_t(b);
+                    j++;
                 }
                 wave_sync();
-                if (uint32_t(lane) < total - r0) {
-                    const uint32_t tk = task[lane];
-                    const int s = int(tk & 3u), b = int((tk >> 2) & 3u), owner = int(tk >> 4);
+                if (uint32_t(lane >> 4) < tb - r0) {
+                    const uint32_t tk = task[lane >> 4];
+                    const int b = int(tk & 3u), owner = int(tk >> 4), k = lane & 15;
                     const BlockPx<N> px = block_px(b, owner);
-                    const int kc = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
-                    const int y = exact_coef_row<N>(srow + kc * NN, srow[NN * NN + kc], srow[NN * NN + NN + kc],
-                                                    srow[NN * NN + 2 * NN + kc], px);
+                    const int y = exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
+                                                    srow[NN * NN + 2 * NN + k], px);
                     res[lane] = uint32_t(y) & 0xFFFFu;
                 }
                 wave_sync();
-                i = pre - r0;
+                m = wf;
+                j = pb - r0;
+                while (m) {
+                    const int b = (__ffs(m) - 1) >> 2;
+                    m &= m - 1;
+                    if (j < 4u) {
+                        const uint32_t* rr = res + 16 * j;
 #pragma unroll
-                for (int b = 0; b < NS; b++)
+                        for (int jj = 0; jj < NP; jj++) {
+                            const uint32_t w = rr[ZigZag<N>::idx[2 * jj]] | (rr[ZigZag<N>::idx[2 * jj + 1]] << 16);
 #pragma unroll
-                    for (int ss = 0; ss < 3; ss++) {
-                        if ((sf >> (4 * b + ss)) & 1u) {
-                            const int zw = Structural<N>::zpos(ss) >> 1;
-                            if (i < 64u) zp[b][zw] = __builtin_amdgcn_perm(res[i], zp[b][zw], 0x05040100u);  // res low -> high half
-                            i++;
+                            for (int bb = 0; bb < NS; bb++) zp[bb][jj] = (b == bb) ? w : zp[bb][jj];
                         }
                     }
+                    j++;
+                }
                 wave_sync();
             }
-            const uint32_t wf = flags & 0x8888u;
-            if (__ballot(wf != 0)) {
-                const uint32_t nb = __popc(wf);
-                uint32_t pb = 0, tbk = 0;
-#pragma unroll
-                for (int kk = 0; kk < 3; kk++) {  // nb <= 4
-                    const uint64_t bm = __ballot((nb >> kk) & 1u);
-                    pb += __builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)) << kk;
-                    tbk += uint32_t(__popcll(bm)) << kk;
-                }
-                for (uint32_t r0 = 0; r0 < tbk; r0 += 4) {
-                    uint32_t m = wf, j = pb - r0;
-                    while (m) {
-                        const int b = (__ffs(m) - 1) >> 2;
-                        m &= m - 1;
-                        if (j < 4u) task[j] = (uint32_t(lane) << 4) | uint32_t(b);
-                        j++;
-                    }
-                    wave_sync();
-                    if (uint32_t(lane >> 4) < tbk - r0) {
-                        const uint32_t tk = task[lane >> 4];
-                        const int b = int(tk & 3u), owner = int(tk >> 4), kc = lane & 15;
-                        const BlockPx<N> px = block_px(b, owner);
-                        const int y = exact_coef_row<N>(srow + kc * NN, srow[NN * NN + kc], srow[NN * NN + NN + kc],
-                                                        srow[NN * NN + 2 * NN + kc], px);
-                        res[lane] = uint32_t(y) & 0xFFFFu;
-                    }
-                    wave_sync();
-                    m = wf;
-                    j = pb - r0;
-                    while (m) {
-                        const int b = (__ffs(m) - 1) >> 2;
-                        m &= m - 1;
-                        if (j < 4u) {
-                            const uint32_t* rr = res + 16 * j;
-#pragma unroll
-                            for (int jj = 0; jj < NP; jj++) {
-                                const uint32_t w = rr[ZigZag<N>::idx[2 * jj]] | (rr[ZigZag<N>::idx[2 * jj + 1]] << 16);
-#pragma unroll
-                                for (int bb = 0; bb < NS; bb++) zp[bb][jj] = (b == bb) ? w : zp[bb][jj];
-                            }
-                        }
-                        j++;
-                    }
-                    wave_sync();
-                }
-            }
         }
-        {  // statistics: FP64 requests of this wave (one store)
-            const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan_dpp(uint32_t(__popc(flags))), 63);
-            if (lane == 0) a.wave_fix[size_t(t) * (TPB / 64) + wv] = wsum;
-        }
+    }
+    {  // statistics: FP64 requests of this wave (one store)
+        const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan_dpp(uint32_t(__popc(flags))), 63);
+        if (lane == 0) a.wave_fix[size_t(t) * 4 + wv] = wsum;
+    }
+    WSTAMP(3);
+    asm volatile("; PHASE p3" ::: "memory");
 
-        QSTAMP(2);
-        // -------------------------------------------------------- sizing + the wave's offsets
-        const uint32_t k0 = uint32_t(tif * TG + GW * wv) * 4u;  // the wave's first block (frame raster order)
+    // ------------------------------------------------------------ sizing + the wave's offsets
+    lane = fresh_lane();
+    uint32_t blw[NS], rb[NS];
+    const uint32_t k0 = uint32_t(tif * TG + GW * wv) * 4u;  // the wave's first block (frame raster order)
 #pragma unroll
-        for (int b = 0; b < NS; b++) {
-            const bool valid = 64 * b + lane < nbw;
-            if (a.coef && valid) {
-                int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + k0 + 64 * b + lane) * NN;
+    for (int b = 0; b < NS; b++) {
+        const bool valid = 64 * b + lane < nbw;
+        if (a.coef && valid) {
+            int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + k0 + 64 * b + lane) * NN;
 #pragma unroll
-                for (int kk = 0; kk < NN; kk++) {
-                    const int kz = ZigZagInv<N>::pos[kk];
-                    dst[kk] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
+            for (int k = 0; k < NN; k++) {
+                const int kz = ZigZagInv<N>::pos[k];
+                dst[k] = int16_t(kz & 1 ? (zp[b][kz >> 1] >> 16) : (zp[b][kz >> 1] & 0xFFFFu));
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        blw[b] = size_block4(zp[b], a.rle, &rb[b]);
+        rb[b] = valid ? rb[b] : 0u;
+        asm volatile("" : "+v"(blw[b]), "+v"(rb[b]));
+#pragma unroll
+        for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t T[NS], off[NS];
+#pragma unroll
+    for (int h = 0; h < NS / 2; h++) {  // two slots per 32-bit scan (16-bit halves)
+        const uint32_t sv = rb[2 * h] | (rb[2 * h + 1] << 16);
+        const uint32_t iv = wave_incl_scan_dpp(sv);
+        const uint32_t tv = __builtin_amdgcn_readlane(iv, 63), ev = iv - sv;
+        T[2 * h] = tv & 0xFFFFu;
+        T[2 * h + 1] = tv >> 16;
+        off[2 * h] = ev & 0xFFFFu;
+        off[2 * h + 1] = ev >> 16;
+    }
+    uint32_t Sb[NS];  // slot starts in the wave image
+    Sb[0] = 0u;
+#pragma unroll
+    for (int b = 1; b < NS; b++) Sb[b] = Sb[b - 1] + T[b - 1];
+    const uint32_t Tw = Sb[NS - 1] + T[NS - 1];
+    const uint32_t S2 = Sb[2];  // the end of slot pair 0
+    // The tile's bit count: wave 0 alone waits for the four waves' counts (their flags, cleared
+    // before the tile) and publishes it; the other waves go on to their emission and learn their
+    // place in the tile after the position barrier.  (A launch too small to fill the chip -- deep
+    // look-back -- keeps a workgroup barrier here: all four waves read predecessor windows.)
+    if (lane == 0) {
+        misc[wv] = Tw;
+        __hip_atomic_store(&misc[ML::F + wv], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    WSTAMP(4);
+    asm volatile("; PHASE p4" ::: "memory");
+    if (deep) {
+        lds_barrier();
+    } else if (wv == 0) {
+        for (;;) {
+            const u32x4 f = *reinterpret_cast<const volatile u32x4*>(misc + ML::F);
+            if (__builtin_amdgcn_readfirstlane(f.x & f.y & f.z & f.w)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    WSTAMP(5);
+    asm volatile("; PHASE p5" ::: "memory");
+
+    lane = fresh_lane();
+    uint32_t A = 0;  // (wave 0, or every wave in deep mode; the others after the position barrier)
+#pragma unroll
+    for (int w = 0; w < 4; w++) A += __builtin_amdgcn_readfirstlane(misc[w]);
+    if (wv == 0 && lane == 0) chain_publish_count(a.st, t, chain_pos, a.tag, A);
+    constexpr int DW = 2;
+    Probe pr[DW];
+#pragma unroll
+    for (int i = 0; i < DW; i++) pr[i] = Probe{0, 0, 0};
+    if (chain_pos != 0) {
+        if (deep) {
+#pragma unroll
+            for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
+        } else if (wv == 0) {
+            pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
+        }
+    }
+
+    const uint32_t reg_bit0 = uint32_t(wv * RW) * 32u;
+    auto zero_img = [&](uint32_t bits) {
+        const uint32_t nq = (bits + 127u) >> 7;  // 16-byte groups
+        uint32_t z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // (a hoisted zero vector was spilled)
+        for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(reg + 4 * q) = u32x4{z, z, z, z};
+    };
+    // The wave's whole image fits its region (the last record's trailing zero fields reach at
+    // most rec_bits past its start, plus the 64-bit window): all four slots are emitted before
+    // the position barrier -- beside wave 0's look-back -- and stored in one pass after it.
+    // Otherwise slot pairs in turn (pair 1 after pair 0 is stored).
+    const bool whole = Tw + uint32_t(a.rec_bits) + 64u <= 32u * RW;
+    auto emit_slot = [&](int b) {  // slot b at its place in the (whole or pair) image
+        if (!(IE_P_ABL & 2) && rb[b]) {
+            const uint32_t p = reg_bit0 + (whole ? Sb[b] : Sb[b] - Sb[(b / PS) * PS]) + off[b];
+            if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
+            else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
+        }
+    };
+    zero_img(whole ? Tw : S2);
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < PS; b++) emit_slot(b);
+    if (whole) {
+#pragma unroll
+        for (int b = PS; b < NS; b++) emit_slot(b);
+    }
+    wave_sync();
+    WSTAMP(6);
+    asm volatile("; PHASE p6" ::: "memory");
+    if (lane == 0 && Tw) misc[ML::H + wv] = reg[0];  // the wave's first 32 bits
+
+    // ------------------------------------------------------------ look-back (wave 0)
+    lane = fresh_lane();
+    const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
+    uint32_t* const out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
+    if (deep && chain_pos != 0) {
+        uint64_t sm = 0;
+        bool found = false;
+        unsigned spins = 0;
+        for (;;) {
+            bool ready = true;
+            sm = 0;
+            found = false;
+#pragma unroll
+            for (int i = 0; i < DW; i++) {
+                const WinSum r = window_sum(pr[i], chain_pos, 64 * (DW * wv + i), 64, a.tag);
+                if (!found) {
+                    ready = ready && r.ready;
+                    sm += r.sum;
+                    found = r.found;
                 }
             }
-            __builtin_amdgcn_sched_barrier(0);
-            blw[b] = size_block4(zp[b], a.rle, &rb[b]);
-            rb[b] = valid ? rb[b] : 0u;
-            asm volatile("" : "+v"(blw[b]), "+v"(rb[b]));
+            if (ready) break;
+            if (++spins > kSpinLimit) {
+                if (lane == 0) atomicAdd(&a.err[0], 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-            for (int j = 0; j < NP; j++) asm volatile("" : "+v"(zp[b][j]));
-            __builtin_amdgcn_sched_barrier(0);
+            for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
         }
-        const uint32_t s01 = rb[0] | (rb[1] << 16), s23 = rb[2] | (rb[3] << 16);
-        const uint32_t i01 = wave_incl_scan_dpp(s01), i23 = wave_incl_scan_dpp(s23);
-        const uint32_t t01 = __builtin_amdgcn_readlane(i01, 63), t23 = __builtin_amdgcn_readlane(i23, 63);
-        const uint32_t e01 = i01 - s01, e23 = i23 - s23;
-        off[0] = e01 & 0xFFFFu;
-        off[1] = e01 >> 16;
-        off[2] = e23 & 0xFFFFu;
-        off[3] = e23 >> 16;
-        const uint32_t S1 = t01 & 0xFFFFu;
-        S2 = S1 + (t01 >> 16);
-        S3 = S2 + (t23 & 0xFFFFu);
-        const uint32_t Tw = S3 + (t23 >> 16);
-        QSTAMP(3);
-        // the tile's count: wave 0 waits for the four waves' (flag = k + 1 in this copy), publishes
-        // it, and decides whether every wave image fits its buffer (else the back end runs at once)
         if (lane == 0) {
-            misc[wv] = Tw;
-            __hip_atomic_store(&misc[16 + wv], uint32_t(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            misc[ML::D + 2 * wv] = uint32_t(sm);
+            misc[ML::D + 2 * wv + 1] = uint32_t(sm >> 32);
+            misc[ML::FD + wv] = found ? 1u : 0u;
         }
-        if (wv == 0) {
-            for (;;) {
-                const u32x4 f = *reinterpret_cast<const volatile u32x4*>(misc + 16);
-                const uint32_t want = uint32_t(k + 1);
-                if (__builtin_amdgcn_readfirstlane((f.x == want) & (f.y == want) & (f.z == want) & (f.w == want))) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            uint32_t A = 0, big = 0;
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
-                A += v;
-                big |= (v + uint32_t(a.rec_bits) + 64u > 32u * kWReg) ? 1u : 0u;
-            }
-            if (lane == 0) {
-                chain_publish_count(a.st, t, chain_pos, a.tag, A);
-                misc[12] = big;
-            }
-        }
-
-        QSTAMP(4);
-        if (k == 0) lds_barrier();  // (the decision below visible; later iterations: back()'s barrier)
-        else if (deferred) back(t_prev, k - 1, false, prc);
-        else lds_barrier();
-        const bool now = __builtin_amdgcn_readfirstlane(misc[12]) != 0u;
-        // the buffer of tile k-1 is free (its stores have read it): tile k+1's pixels into it;
-        // wave 0 resolves the claim of tile k+2
-        if (k >= 1) {
-            const int tn = __builtin_amdgcn_readfirstlane(int(misc0[((k + 1) % 3) * 32 + 13]));
-            if (tn >= 0) issue_pixels(a, tn, (k + 1) & 1);
-        }
-        if (wv == 0) {
-            int t2 = -1;
-            if (claiming) {
-                t2 = claim_resolve(cnt, nch, tpc, seg, &chain, kc);
-                claiming = t2 >= 0;
-            }
-            if (lane == 0) misc0[((k + 2) % 3) * 32 + 13] = uint32_t(t2);
-        }
-
-        // -------------------------------------------------------- emit (whole image, or slot pair 0)
-        const uint32_t reg_bit0 = uint32_t(((k & 1) * 4 + wv) * kWReg) * 32u;
-        const uint32_t Sb[NS] = {0u, S1, S2, S3};
-        const bool whole = Tw + uint32_t(a.rec_bits) + 64u <= 32u * kWReg;
-        {
-            const uint32_t nq = ((whole ? Tw : S2) + 127u) >> 7;  // 16-byte groups
-            uint32_t z;
-            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-            for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(reg + 4 * q) = u32x4{z, z, z, z};
-        }
-        wave_sync();
-        QSTAMP(8);
-#pragma unroll
-        for (int b = 0; b < NS; b++) {
-            if ((b < 2 || whole) && rb[b]) {
-                const uint32_t p = reg_bit0 + Sb[b] + off[b];
-                if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
-                else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
-            }
-        }
-        wave_sync();
-        if (lane == 0 && Tw) misc[4 + wv] = reg[0];  // the wave's first 32 bits
-        QSTAMP(9);
-        if (now) {
-            back(t, k, true, prc);
-            deferred = false;
+        lds_barrier();
+    }
+    if (wv == 0) {
+        uint64_t excl = 0;
+        uint32_t ptail = 0, pend = 0;
+        if (chain_pos == 0) {
+            const uint32_t s = uint32_t(start_bit & 31);
+            ptail = s ? (bswap32(out[start_bit >> 5]) >> (32 - s)) : 0u;
         } else {
-            deferred = true;
+            bool done = false;
+            if (deep) {
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    if (!done) {
+                        excl += uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::D + 2 * w]))) |
+                                (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::D + 2 * w + 1]))) << 32);
+                        done = __builtin_amdgcn_readfirstlane(misc[ML::FD + w]) != 0;
+                    }
+                }
+                if (!done) excl = 0;
+            }
+            if (!done) {
+                const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr[0];
+                excl = (IE_P_ABL & 4) ? uint64_t(chain_pos) * 30000u
+                                      : lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
+            }
+            const bool have = uint32_t(pr[0].gt >> 56) == a.tag;
+            const bool split = ((start_bit + excl) & 31) != 0;
+            ptail = have ? uint32_t(pr[0].gt) : 0u;
+            pend = (!have && split) ? 1u : 0u;
         }
-        t_prev = t;
-        klast = k;
-        QSTAMP(10);
-        QRTSTAMP(15);
-    }
-    if (deferred) {  // the last tile's back end (no front stage left to overlap its look-back)
-        if (wv == 0) {
-            const int tp = t_prev;
-            KArgs& a = *ka;
-            int tid = threadIdx.x;
-            asm volatile("" : "+v"(tid));
-            const TileGeo gp = tile_geo<4, 4, TG>(a, tp, tid);
-            if (gp.chain_pos != 0) prc = probe_issue(a.st, tp, gp.chain_pos, gp.step, 0, IE_Q_PROBE);
+        if (lane == 0) {
+            if (chain_pos != 0) publish(a.st, t, 1, a.tag, excl + A);
+            misc[ML::E] = uint32_t(excl);
+            misc[ML::E + 1] = uint32_t(excl >> 32);
+            misc[ML::PT] = ptail;
+            misc[ML::PD] = pend;
+            const uint64_t P = start_bit + excl;
+            if (tif == 0) a.frame_start[frame] = P;
+            if (chain_last) a.chain_end[a.segmented ? frame : 0] = P + A;
         }
-        back(t_prev, klast, false, prc);
     }
-    leave();
-#undef QSTAMP
-#undef QRTSTAMP
+    WSTAMP(7);
+    asm volatile("; PHASE p7" ::: "memory");
+    lds_barrier();  // ---- the tile's position
+    WSTAMP(8);
+    asm volatile("; PHASE p8" ::: "memory");
+    lane = fresh_lane();
+    uint32_t W = 0;
+    A = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(misc[w]);
+        A += v;
+        W += (w < wv) ? v : 0u;
+    }
+
+    // ------------------------------------------------------------ store, slot pair by slot pair
+    if (Tw) {
+        const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::E]))) |
+                              (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[ML::E + 1]))) << 32);
+        const uint64_t Xw = start_bit + excl + W;
+        const bool pend = __builtin_amdgcn_readfirstlane(misc[ML::PD]) != 0u;
+        const uint64_t skipw = ((Xw & 31) && (wv > 0 || pend)) ? (Xw >> 5) : ~0ull;
+        uint32_t prev = (wv == 0) ? __builtin_amdgcn_readfirstlane(misc[ML::PT]) : 0u;
+        const HistCountT<HR> hc{hl, chain_last ? (start_bit + excl + A + 7) / 8 : ~0ull, uint32_t(lane % HR)};
+        auto count = [&](uint64_t gw, uint32_t v) {
+            if constexpr (HIST) hc(gw, v);
+        };
+        auto store_pair = [&](uint32_t S0, uint32_t n) {
+            if (!n || (IE_P_ABL & 8)) return;
+            const uint64_t Xb = Xw + S0;
+            const uint32_t nw = uint32_t(((Xb + n) >> 5) - (Xb >> 5));
+            if constexpr (HIST) store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane, hc);
+            else store_slot(out, reg, Xb, nw, ((Xb >> 5) == skipw) ? 1u : 0u, prev, lane);
+            prev = slot_tail32(reg, n, prev);
+        };
+        if constexpr (HIST) {
+            if (wv == 0 && chain_pos == 0)
+                for (uint32_t i = lane; i < uint32_t(start_bit >> 5); i += 64) hc(i, out[i]);
+        }
+        const uint64_t E = Xw + Tw;
+        const uint32_t e = uint32_t(E) & 31u;
+        store_pair(0u, whole ? Tw : S2);
+        WSTAMP(9);
+        asm volatile("; PHASE p9" ::: "memory");
+        if (!whole && Tw > S2) {
+            wave_sync();  // pair 0's image has been read
+            zero_img(Tw - S2);
+            wave_sync();
+#pragma unroll
+            for (int b = PS; b < NS; b++) emit_slot(b);
+            wave_sync();
+            store_pair(S2, Tw - S2);
+        }
+        const uint32_t nexthead = (e && wv < wlast) ? misc[ML::H + wv + 1] : 0u;
+        if (lane == 0) {
+            if (e && (wv < wlast || chain_last)) {  // the wave's last, partial word
+                const uint32_t v = bswap32((prev << (32u - e)) | (nexthead >> e));
+                out[E >> 5] = v;
+                count(E >> 5, v);
+            }
+            if (wv == wlast) publish(a.st, t, 2, a.tag, prev);  // the tile's last 32 bits
+            if (wv == 0 && pend) {  // the first word, with the predecessor's tail
+                const uint32_t pt = wait_tail(a.st, t - step, a.tag, a.err);
+                const uint32_t s = uint32_t(Xw) & 31u;
+                const uint32_t v = bswap32((pt << (32u - s)) | (misc[ML::H] >> s));
+                out[Xw >> 5] = v;
+                count(Xw >> 5, v);
+            }
+        }
+        WSTAMP(10);
+        asm volatile("; PHASE p10" ::: "memory");
+        WRTSTAMP(15);
+    }
+    if constexpr (HIST) {
+        lds_barrier();  // every wave's bytes counted
+        uint32_t c = 0;
+        const int th = 64 * wv + fresh_lane();
+#pragma unroll
+        for (int r = 0; r < HR; r++) c += hl[th * HR + r];
+        if (c) atomicAdd(&a.hist[size_t(frame) * 256 + th], c);
+    }
 }
 
-#ifndef IE_ENC_P
-#define IE_ENC_P 1  // 0: 4x4 FAST batch launches run encode4w_kernel (A/B builds)
-#endif
-// Persistent workgroups per CU: the occupancy API's answer, capped at IE_P_PER_CU -- the number
-// tools/asmcheck.py (PERSIST) proves the SGPR admission rule lets in (the API can answer one more
-// than the hardware admits; a static-order grid with one workgroup not resident would stall).
-#ifndef IE_P_PER_CU
-#define IE_P_PER_CU 6
-#endif
-
-// Resident workgroups of encode4p_kernel<HIST> on this device (cached per process).
-static int encode4p_grid(bool hist, size_t lds) {
-    static int cached[2] = {0, 0};
-    int& c = cached[hist ? 1 : 0];
-    if (c) return c;
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hist) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4p_kernel<true, 4>, 256, lds);
-    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4p_kernel<false, 4>, 256, lds);
-    per = std::min(per, IE_P_PER_CU);
-    c = std::max(1, per) * std::max(1, cus);
-    return c;
-}
-
-// Resident workgroups of encode4q_kernel on this device (cached per process): the grid of its
-// static tile order, which must be resident at once.
-static int encode4q_grid() {
-    static int c = 0;
-    if (c) return c;
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, encode4q_kernel, 256, kQLdsBytes);
-    per = std::min(per, IE_Q_PER_CU);
-    c = std::max(1, per) * std::max(1, cus);
-    return c;
-}
-
-#ifndef IE_P_W8
-#define IE_P_W8 0  // 1: (A/B builds) launches too small to fill the chip run 8 waves per tile (one 4K frame: 16.9 against 16.3 us)
-#endif
 // Returns the FP64-statistics words per tile the launched kernel writes (its waves per tile).
 int launch_encode4w(const EncArgs& a, hipStream_t s) {
-    // large segmented launches without the histogram may run the pipelined persistent encoder (two
-    // or more tiles per workgroup; a smaller launch has nothing to overlap and keeps one tile per
-    // workgroup; one long chain -- a concatenated stream -- would make its deferred look-backs
-    // walk a whole round of the grid)
-    // (opt-in, IE_PIPELINED=1, read per launch: measured slower than encode4p_kernel)
-    const char* pe = getenv("IE_PIPELINED");
-    const bool pipelined = pe && atoi(pe) != 0;
-    if (IE_ENC_Q && pipelined && !a.ticket && !a.hist && !a.deep_lb && a.segmented && a.ntiles >= 2 * encode4q_grid()) {
-        hipLaunchKernelGGL(encode4q_kernel, dim3(encode4q_grid()), dim3(256), kQLdsBytes, s, a, a.tab);
+    if (!a.ticket) {  // dispatch order: encode4p_kernel, one workgroup per tile
+        const size_t lds = p_lds_bytes() + (a.hist ? 1024 * kWHistRep : 0);
+        if (a.hist) hipLaunchKernelGGL(encode4p_kernel<true>, dim3(a.ntiles), dim3(256), lds, s, a, a.tab);
+        else hipLaunchKernelGGL(encode4p_kernel<false>, dim3(a.ntiles), dim3(256), lds, s, a, a.tab);
         return 4;
     }
-    if (IE_ENC_P && IE_P_W8 && !a.ticket && !a.hist && a.deep_lb) {
-        hipLaunchKernelGGL((encode4p_kernel<false, 8>), dim3(a.ntiles), dim3(512), p_lds_bytes<8>(), s, a, a.tab);
-        return 8;
-    }
-    if (IE_ENC_P && !a.ticket) {
-        const size_t lds = p_lds_bytes<4>() + (a.hist ? 1024 * kWHistRep : 0);
-        const int grid = IE_P_PERSIST ? std::min(a.ntiles, encode4p_grid(a.hist != nullptr, lds)) : a.ntiles;
-        if (a.hist) hipLaunchKernelGGL((encode4p_kernel<true, 4>), dim3(grid), dim3(256), lds, s, a, a.tab);
-        else hipLaunchKernelGGL((encode4p_kernel<false, 4>), dim3(grid), dim3(256), lds, s, a, a.tab);
-        return 4;
-    }
+    // ticket mode (the host's redo after a look-back timeout): tiles in ticket order
     if (a.hist) hipLaunchKernelGGL(encode4w_kernel<true>, dim3(a.ntiles), dim3(256), kWLdsBytes + 1024 * kWHistRep, s, a, a.tab);
     else hipLaunchKernelGGL(encode4w_kernel<false>, dim3(a.ntiles), dim3(256), kWLdsBytes, s, a, a.tab);
     return 4;

@@ -73,3 +73,35 @@ def test_built_kernels_within_budget():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asmcheck.py")] + files,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_64bit_lds_atomic_fails(tmp_path):
+    """A 64-bit LDS atomic in any kernel (the round-5 fault: ds_or_b64 at a 4-byte aligned bit-image
+    address raised a memory violation that aborted the queue) fails the build check."""
+    r = _run(tmp_path, "\tds_or_b64 v2, v[4:5] offset:8\n\ts_endpgm\n")
+    assert r.returncode == 1 and "64-bit LDS atomic" in r.stderr
+    r = _run(tmp_path, "\tds_add_rtn_u64 v[6:7], v2, v[4:5]\n")
+    assert r.returncode == 1
+    assert _run(tmp_path, "\tds_or_b32 v2, v4\n\tds_or_b32 v2, v5 offset:4\n\tds_read_b64 v[4:5], v2\n").returncode == 0
+
+
+def test_wide_ds_in_inline_asm_fails(tmp_path):
+    """Hand-written inline asm may not name a 64/96/128-bit DS instruction (its address alignment is
+    beyond the compiler's checks); the 32-bit pair the emission uses passes."""
+    good = tmp_path / "good.hip"
+    good.write_text('asm volatile("ds_or_b32 %0, %1\\n\\tds_or_b32 %0, %2 offset:4" ::"v"(a), "v"(hi), "v"(lo));\n'
+                    "// a comment naming ds_or_b64 is not code\n")
+    bad = tmp_path / "bad.hip"
+    bad.write_text('asm volatile("ds_or_b64 %0, %1" ::"v"(a), "v"(x));\n')
+    tool = os.path.join(ROOT, "tools", "asmcheck.py")
+    assert subprocess.run([sys.executable, tool, str(good)], capture_output=True, text=True).returncode == 0
+    r = subprocess.run([sys.executable, tool, str(bad)], capture_output=True, text=True)
+    assert r.returncode == 1 and "bad.hip:1" in r.stderr
+
+
+def test_sources_have_no_wide_inline_ds():
+    import glob
+    srcs = [f for ext in ("hip", "h", "hpp") for f in glob.glob(os.path.join(ROOT, "imageencoder_amd", "csrc", f"*.{ext}"))]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asmcheck.py")] + srcs,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr

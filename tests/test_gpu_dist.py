@@ -103,7 +103,7 @@ def _worker_c4(rank, world, port, F, nchunks, steps, q_out):
     import torch
     import torch.distributed as dist
 
-    from imageencoder_amd import Codec, read_matrix, stream_bound, synth, write_header
+    from imageencoder_amd import MODE_EXACT, Codec, read_matrix, stream_bound, synth, write_header
     from imageencoder_amd import dist as D
     from tests import oracle_lib as O
 
@@ -151,7 +151,9 @@ def _worker_c4(rank, world, port, F, nchunks, steps, q_out):
             allf = synth.uniform_device(w, h, F, seed, dev, torch)
             ref = torch.zeros(stream_bound(w, h, n, F, hb) + 64, dtype=torch.uint8, device=dev)
             ref[: hdr.size].copy_(torch.from_numpy(hdr).to(dev))
-            _, end = enc.encode_frames(allf, w, h, ref, start_bit=hb, nframes=F)
+            # the reference launch in EXACT mode (encode_kernel<4, true>, FP64 everywhere, pinned to
+            # the oracle): independent of the ticket-mode FAST kernel the ranks ran
+            _, end = enc.encode_frames(allf, w, h, ref, start_bit=hb, nframes=F, mode=MODE_EXACT)
             q_out.put((res, (end, hashlib.md5(ref[: (end + 7) // 8].cpu().numpy().tobytes()).hexdigest()), counts))
         dist.barrier()
     finally:

@@ -463,6 +463,40 @@ def test_counted_encode_histogram(codec, w, h, f, start_bit, kind):
         assert int(f_pass[f_pass != np.uint64(2**64 - 1)].max()) >= 64 * 4096
 
 
+@pytest.mark.gpu
+def test_counted_encode_histogram_batch_sizes(codec):
+    """The counted encoder's histogram rows across batches of different sizes: a
+    counted batch of 8 that no fused pass reads, a batch of 4 that one does (clearing rows 0-3
+    only), then a batch of 8 again -- its rows 4-7 must not keep the first batch's counts.  Every
+    fused histogram equals a host bincount of the stream bytes."""
+    import torch
+    from imageencoder_amd import stream_bound
+    n, q = 4, O.read_matrix("matrix.txt", 4)
+    codec.set_quant(q, n)
+    w, h = 256, 128
+    pitch = (stream_bound(w, h, n, 1, 0) + 255) // 256 * 256
+    out = torch.zeros(pitch * 8, dtype=torch.uint8, device="cuda")
+
+    def check(f, seed, read):
+        y = torch.from_numpy(synth.frames("M", w, h, f, seed=seed)).cuda()
+        out.zero_()
+        codec.encode_images(y, w, h, out, out_pitch=pitch, nframes=f, count_bytes=True)
+        if not read:
+            return
+        hist, _ = codec.huffman_hist_after_encode(out, pitch, f)
+        ends = codec.encode_images(y, w, h, out, out_pitch=pitch, nframes=f)
+        host = out.cpu().numpy()
+        for k in range(f):
+            nb = (int(ends[k]) + 7) // 8
+            want = np.bincount(host[k * pitch: k * pitch + nb], minlength=256).astype(np.uint32)
+            np.testing.assert_array_equal(hist[k], want, err_msg=f"batch of {f}, image {k}")
+
+    check(8, 1, read=False)
+    check(4, 2, read=True)
+    check(8, 3, read=True)
+    check(8, 4, read=True)
+
+
 # ------------------------------------------------- multi-segment decode; one-launch path (opt-in)
 @pytest.mark.parametrize("huffman", [False, True])
 @pytest.mark.parametrize("n", [4, 8])

@@ -1,6 +1,8 @@
 """Interleaved A/B timing of libie_hip.so variants in ONE process (cdna_hip_programming.md rule 24).
 
-usage: python tools/ab.py [--n 4|8] [--frames 16] [--rounds 7] lib1.so lib2.so ...
+usage: python tools/ab.py [--n 4|8] [--frames 16] [--rounds 7] lib1.so lib2.so@ENV=VAL,ENV2=VAL ...
+A variant "path@ENV=VAL,..." runs that library with those environment variables set around each of
+its calls (knobs the library reads per launch, e.g. IE_P_GRID).
 Each variant gets its own ie_ctx on torch's current stream; every round times every variant
 (10 launches each, HIP events) in turn; prints the median / min us per launch, and whether the
 variant's output for the batch matches the first variant's byte for byte.
@@ -29,20 +31,45 @@ ap.add_argument("--op", default="encode", choices=["encode", "counted", "frames"
                      "--frames 64)")
 ap.add_argument("--w", type=int, default=3840)
 ap.add_argument("--h", type=int, default=2160)
+ap.add_argument("--rotate", type=int, default=1,
+                help="timed launches cycle over this many distinct input batches (4: 4 x 16 4K frames, "
+                     "more than the MALL holds -- the pixels come from HBM as in bench.py)")
 ap.add_argument("libs", nargs="+")
 args = ap.parse_args()
 
 n = args.n
 q = np.ascontiguousarray(np.asarray(O.read_matrix("matrix.txt" if n == 4 else "matrix8_1.txt", n), dtype=np.uint16).ravel())
 w, h, nf = args.w, args.h, args.frames
-y = (synth.uniform_device(w, h, nf, 3, "cuda", torch) if args.kind == "U"
-     else torch.from_numpy(synth.frames(args.kind, w, h, nf, seed=3)).cuda())
+y_all = (synth.uniform_device(w, h, nf * args.rotate, 3, "cuda", torch) if args.kind == "U"
+         else torch.from_numpy(synth.frames(args.kind, w, h, nf * args.rotate, seed=3)).cuda())
+y_rot = [y_all[i * nf:(i + 1) * nf] for i in range(args.rotate)]
+y = y_rot[0]
+rot = [0]
+
+
+def ybatch(sizes):
+    """The batch a launch reads: batch 0 for the checked launch, the next one in turn otherwise."""
+    if sizes:
+        return y_rot[0]
+    rot[0] = (rot[0] + 1) % args.rotate
+    return y_rot[rot[0]]
 stream = torch.cuda.Stream()  # a real stream handle (the default stream's handle is 0 = the ctx's own)
 torch.cuda.set_stream(stream)
 variants = []
 shared_out = None
-for path in args.libs:
-    L = C.CDLL(os.path.abspath(path), mode=C.RTLD_LOCAL)
+libs_loaded = {}
+for spec in args.libs:
+    path, _, envs = spec.partition("@")
+    env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
+    if path in libs_loaded:  # (the same library under several environments: one handle each)
+        import shutil
+        import tempfile
+        cp = os.path.join(tempfile.mkdtemp(), "libie_hip.so")
+        shutil.copy(path, cp)
+        L = C.CDLL(cp, mode=C.RTLD_LOCAL)
+    else:
+        L = C.CDLL(os.path.abspath(path), mode=C.RTLD_LOCAL)
+    libs_loaded[path] = L
     vp = C.c_void_p
     L.ie_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     L.ie_set_stream.argtypes = [vp, vp]
@@ -72,7 +99,20 @@ for path in args.libs:
         L.ie_encode_frames.argtypes = [vp, vp, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                        vp, C.c_size_t, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
 
-    def run(L=L, hnd=hnd, out=out, pitch=pitch, eb=eb, sizes=False):
+    def run(L=L, hnd=hnd, out=out, pitch=pitch, eb=eb, sizes=False, env=env):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            run1(L, hnd, out, pitch, eb, sizes)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    def run1(L, hnd, out, pitch, eb, sizes):
+        y = ybatch(sizes)
         if args.op == "frames":  # (eb[0] = the stream's end bit; compared over the whole stream)
             r = L.ie_encode_frames(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, nf, 1, 0, C.c_void_p(out.data_ptr()),
                                    pitch * nf, 165, None, eb.ctypes.data_as(C.POINTER(C.c_uint64)))
@@ -90,13 +130,13 @@ for path in args.libs:
         if r != 0:
             raise RuntimeError(L.ie_last_error(hnd))
 
-    print(f"running {path}", flush=True)  # (a fault names its variant)
+    print(f"running {spec}", flush=True)  # (a fault names its variant)
     run(sizes=True)
     torch.cuda.synchronize()
     fb = C.c_uint64(0)
     if hasattr(L, "ie_last_fallbacks") and L.ie_last_fallbacks(hnd, C.byref(fb)) == 0:
         print(f"{os.path.basename(os.path.dirname(path))}: FP64 fix-up requests per launch {fb.value}", flush=True)
-    variants.append({"name": os.path.basename(os.path.dirname(path)) or path, "run": run, "out": out.clone(),
+    variants.append({"name": (os.path.basename(os.path.dirname(path)) or path) + ("@" + envs if envs else ""), "run": run, "out": out.clone(),
                      "pitch": pitch, "eb": eb.copy(), "t": []})
 
 ref = variants[0]

@@ -8,12 +8,38 @@ rounding ties.  The kernels are built with -ffp-contract=off; this check proves 
 reports each kernel's VGPR count, scratch size and occupancy so register spills show up in the
 CPU build.
 
-    python3 tools/asmcheck.py build/asm/ie_encode.s [build/asm/ie_decode.s ...]
+    python3 tools/asmcheck.py build/asm/ie_encode.s [build/asm/ie_decode.s ...] [csrc/*.hip ...]
+
+It also rejects 64-bit LDS atomics in the ISA and 64/96/128-bit DS instructions in the inline asm
+of the given source files (DS_ATOMIC64 below).
 """
 import re
 import sys
 
 FORBIDDEN = ("v_fma_f64", "v_fmac_f64", "v_fma_mix", "v_pk_fma_f64")
+
+# LDS atomics on 64-bit data need an 8-byte aligned address; at a 4-byte aligned one the SQ raises a
+# memory violation and the whole queue aborts (round 5: one `ds_or_b64` at a word-aligned bit-image
+# address -- HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION on the first launch, twice; gone with the
+# same field as two `ds_or_b32`).  The kernels need none, so the rule is absolute: no 64-bit DS
+# atomic in any kernel's ISA, and no 64/96/128-bit DS mnemonic in hand-written inline asm, whose
+# addresses the compiler cannot check (compiler-generated wide DS reads/writes come from naturally
+# aligned types; a misaligned one is replayed, not faulted -- SQ_LDS_UNALIGNED_STALL, profiled).
+DS_ATOMIC64 = re.compile(r"^ds_(add|sub|rsub|inc|dec|min|max|and|or|xor|mskor|wrxchg|wrxchg2|wrxchg2st64|cmpst|"
+                         r"cmpswap|condxchg32|wrap|append|consume)(_rtn)?_(u64|i64|b64|f64)\b")
+DS_WIDE = re.compile(r"\bds_\w+_(b64|b96|b128|u64|i64|f64)\b")
+
+
+def inline_asm_wide_ds(paths):
+    """(file, line, text) of every inline-asm string in the given sources naming a 64/96/128-bit DS
+    instruction."""
+    hits = []
+    for path in paths:
+        for i, ln in enumerate(open(path), 1):
+            code = ln.split("//", 1)[0]
+            if "asm" in code and DS_WIDE.search(code):
+                hits.append((path, i, ln.strip()))
+    return hits
 
 
 def _regs(operands):
@@ -48,6 +74,8 @@ def scan(path):
             continue
         s = ln.strip()
         op = s.split(None, 1)[0] if s and not s.startswith((";", ".")) else ""
+        if op and DS_ATOMIC64.match(op):
+            bad.append((cur, "64-bit LDS atomic: " + s))
         args = s.split(None, 1)[1].split(",") if op and len(s.split(None, 1)) > 1 else []
         regs = _regs(args)
         fused = op in FORBIDDEN or any(op.startswith(f + "_") for f in FORBIDDEN)
@@ -99,42 +127,23 @@ BUDGETS = {
     "_ZN2ie13encode_kernelILi8ELb0ELb0ELi1EEEvNS_7EncArgsEPKNS_9EncTablesE": (4, 0),
     "_ZN2ie15encode4w_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
     "_ZN2ie15encode4w_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
-    "_ZN2ie15encode4p_kernelILb0ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
-    "_ZN2ie15encode4p_kernelILb1ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
-    "_ZN2ie15encode4p_kernelILb0ELi8EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
-    "_ZN2ie15encode4q_kernelENS_7EncArgsEPKNS_9EncTablesE": (4, 0),
+    "_ZN2ie15encode4p_kernelILb0EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
+    "_ZN2ie15encode4p_kernelILb1EEEvNS_7EncArgsEPKNS_9EncTablesE": (6, 0),
 }
-# Persistent kernels: the host sizes the grid as (workgroups per CU) x CUs with workgroups per CU
-# = min(occupancy API, PERSIST[name]); every one of them must be resident at once (static tile
-# order), so the SGPR admission rule (MI355X_MICROARCH.md, Residency: 256-thread blocks per CU <=
-# floor(800 / (ceil(sgpr / 16) * 16 + 16))) must admit at least that many.
-PERSIST = {
-    "_ZN2ie15encode4p_kernelILb0ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": 6,
-    "_ZN2ie15encode4p_kernelILb1ELi4EEEvNS_7EncArgsEPKNS_9EncTablesE": 6,
-    "_ZN2ie15encode4q_kernelENS_7EncArgsEPKNS_9EncTablesE": 4,
-}
-
-
-def sgpr_counts(path):
-    """{kernel: .sgpr_count} from the code object metadata."""
-    txt = open(path).read()
-    k = txt.find("amdhsa.kernels")
-    out = {}
-    for ent in txt[k:].split("\n  - ")[1:] if k >= 0 else []:
-        m = re.search(r"\.name:\s+(\S+)", ent)
-        g = re.search(r"\.sgpr_count:\s+(\d+)", ent)
-        if m and g:
-            out[m.group(1)] = int(g.group(1))
-    return out
-
-
 def main(paths):
     rc = 0
+    srcs = [a for a in paths if a.endswith((".hip", ".h", ".hpp", ".cpp"))]
+    paths = [a for a in paths if a not in srcs]
+    for f, i, t in inline_asm_wide_ds(srcs):
+        rc = 1
+        print(f"{f}:{i}: 64/96/128-bit DS instruction in inline asm (alignment unchecked): {t}", file=sys.stderr)
+    if srcs and rc == 0:
+        print(f"{len(srcs)} source files: no wide DS instruction in inline asm")
     for p in paths:
         # the encoder's bit image is addressed from LDS byte 0 (scatter_bits' inline ds_or): its
         # kernels must allocate no static LDS, so the dynamic area starts there
         for name, size in static_lds(p).items():
-            if ("encode_kernel" in name or "encode4w_kernel" in name or "encode4p_kernel" in name or "encode4q_kernel" in name) and size != 0:
+            if ("encode_kernel" in name or "encode4w_kernel" in name or "encode4p_kernel" in name) and size != 0:
                 rc = 1
                 print(f"{p}: {name} allocates {size} B of static LDS (scatter_bits assumes 0)", file=sys.stderr)
         bad, kernels = scan(p)
@@ -147,14 +156,6 @@ def main(paths):
                 rc = 1
                 print(f"{p}: {name[:60]} over budget: occupancy {info.get('Occupancy')} (>= {waves}), "
                       f"scratch {info.get('ScratchSize')} B (<= {scratch})", file=sys.stderr)
-        sg = sgpr_counts(p)
-        for name, per_cu in PERSIST.items():
-            if name in sg:
-                admit = 800 // ((sg[name] + 15) // 16 * 16 + 16)
-                if admit < per_cu:
-                    rc = 1
-                    print(f"{p}: {name[:60]} sgpr_count {sg[name]} admits {admit} workgroups per CU "
-                          f"< {per_cu} (the persistent grid would not be resident)", file=sys.stderr)
         for name, info in kernels.items():
             if info:
                 print(f"{p}: {name[:70]:70s} vgpr={info.get('NumVgprs')} scratch={info.get('ScratchSize')} "
@@ -162,8 +163,9 @@ def main(paths):
         if bad:
             rc = 1
             for k, s in bad[:20]:
-                print(f"{p}: FP64 FMA in {k}: {s}", file=sys.stderr)
-            print(f"{p}: {len(bad)} fused FP64 instructions (reference order violated)", file=sys.stderr)
+                print(f"{p}: {'' if s.startswith('64-bit LDS') else 'FP64 FMA '}in {k}: {s}", file=sys.stderr)
+            print(f"{p}: {len(bad)} forbidden instructions (fused FP64: reference order violated; 64-bit "
+                  f"LDS atomics: alignment faults)", file=sys.stderr)
         else:
             print(f"{p}: no fused FP64 instructions")
     return rc
