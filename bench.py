@@ -49,11 +49,11 @@ sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")  # data files (matrices, manifest of md5s)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROUND = "r05"  # profiles/<ROUND>_traffic_<workload>.json: this round's counter passes (tools/gpu_traffic.sh)
+ROUND = "r06"  # profiles/<ROUND>_traffic_<workload>.json: this round's counter passes (tools/gpu_traffic.sh)
 # the dominant kernel of each workload's timed launch (launch_encode: 4x4 FAST over whole 16-byte
 # groups runs encode4p_kernel; 8x8 runs encode_kernel<8>)
-KERNEL = {"c2": "encode4p_kernel<false, 4>", "c3": "encode_kernel<8,false>", "c4": "encode4p_kernel<false, 4>",
-          "c5": "encode4p_kernel<true, 4>"}
+KERNEL = {"c2": "encode4p_kernel<false>", "c3": "encode_kernel<8,false>", "c4": "encode4p_kernel<false>",
+          "c5": "encode4p_kernel<true>"}
 
 WORKLOADS = {
     "c2": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=False,
@@ -375,7 +375,7 @@ def main():
             t_cnt = g3 / args.steps
             # the roofline prices the launch the step runs (the counting encoder); the plain encoder
             # (same kernel without the byte counts) is reported beside it
-            extra["plain_encode"] = {"kernel": "encode4p_kernel<false, 4>", "launch_us": round(enc_s * 1e6, 2),
+            extra["plain_encode"] = {"kernel": "encode4p_kernel<false>", "launch_us": round(enc_s * 1e6, 2),
                                      "frac": round((B * w * h + out_bytes_per_launch) / enc_s / 1e9 / HBM_PEAK_GBS, 4)}
             enc_s = t_cnt
             extra["huffman_roofline"] = {

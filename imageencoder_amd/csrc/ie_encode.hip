@@ -50,6 +50,9 @@ template <> struct ZigZagInv<8> {
                                     21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 };
 
+#ifndef IE_PX_AUX8
+#define IE_PX_AUX8 2  // cache-policy bits of encode_kernel<8>'s pixel DMA: nt (HBM-resident C3 141.7 against 143.1 us)
+#endif
 #ifndef IE_PROFILE
 #define IE_PROFILE 0
 #endif
@@ -820,7 +823,7 @@ __global__ IE_ENC_BOUNDS(N, EXACT) void encode_kernel(EncArgs a, const EncTables
             for (int r = 0; r < N; r += 2)
                 if (live)
                     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + size_t(r + half) * a.stride),
-                                                     (__attribute__((address_space(3))) void*)(pwave + r * kRowW), 16, 0, 0);
+                                                     (__attribute__((address_space(3))) void*)(pwave + r * kRowW), 16, 0, IE_PX_AUX8);
         } else {  // odd bx / unaligned rows: through registers
             load_tile<N, WPR, BPT>(a, g, seg);
 #pragma unroll
@@ -2001,6 +2004,10 @@ __device__ __forceinline__ float round_block_lean4j(const float (&t)[16], uint32
     return emax;
 }
 
+#ifndef IE_P_PXAUX
+#define IE_P_PXAUX 2  // cache-policy bits of encode4p's pixel DMA: nt (pixels are read once; HBM-resident
+                      // frames 98.2 against 101.1 us per 16-frame launch, MALL-resident 97.9 against 92.8)
+#endif
 #ifndef IE_P_WAVES
 #define IE_P_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD)
 #endif
@@ -2047,7 +2054,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
 #pragma unroll
         for (int r = 0; r < N; r++)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + size_t(r) * ga.stride),
-                                             (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void*)(reg + r * BW), 16, 0, IE_P_PXAUX);
     }
     if (IE_PROFILE == 2 && a_.stamps && lane == 0) a_.stamps[size_t(t) * kStamps + wv * 16 + 1] = __builtin_amdgcn_s_memrealtime();
     // the FP64 rows (waves 0-2: 2432 bytes) and the matrix-pipe A fragments (wave 3; read back per

@@ -34,6 +34,7 @@ ap.add_argument("--h", type=int, default=2160)
 ap.add_argument("--rotate", type=int, default=1,
                 help="timed launches cycle over this many distinct input batches (4: 4 x 16 4K frames, "
                      "more than the MALL holds -- the pixels come from HBM as in bench.py)")
+ap.add_argument("--rotate-out", type=int, default=1, help="timed launches cycle over this many output buffers")
 ap.add_argument("libs", nargs="+")
 args = ap.parse_args()
 
@@ -45,6 +46,7 @@ y_all = (synth.uniform_device(w, h, nf * args.rotate, 3, "cuda", torch) if args.
 y_rot = [y_all[i * nf:(i + 1) * nf] for i in range(args.rotate)]
 y = y_rot[0]
 rot = [0]
+rot_o = [0]
 
 
 def ybatch(sizes):
@@ -85,9 +87,9 @@ for spec in args.libs:
     assert L.ie_set_stream(hnd, C.c_void_p(stream.cuda_stream)) == 0
     assert L.ie_set_quant(hnd, q.ctypes.data, n) == 0
     pitch = (int(L.ie_stream_bound(w, h, n, 1, 165)) + 255) // 256 * 256
-    if shared_out is None:  # one output buffer for every variant (placement effects cancel)
-        shared_out = torch.zeros(pitch * nf, dtype=torch.uint8, device="cuda")
-    out = shared_out
+    if shared_out is None:  # one output buffer set for every variant (placement effects cancel)
+        shared_out = [torch.zeros(pitch * nf, dtype=torch.uint8, device="cuda") for _ in range(args.rotate_out)]
+    out = shared_out[0]
     out.zero_()
     eb = np.zeros(nf, dtype=np.uint64)
 
@@ -113,6 +115,9 @@ for spec in args.libs:
 
     def run1(L, hnd, out, pitch, eb, sizes):
         y = ybatch(sizes)
+        if not sizes:  # (the checked launch writes buffer 0)
+            rot_o[0] = (rot_o[0] + 1) % args.rotate_out
+            out = shared_out[rot_o[0]]
         if args.op == "frames":  # (eb[0] = the stream's end bit; compared over the whole stream)
             r = L.ie_encode_frames(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, nf, 1, 0, C.c_void_p(out.data_ptr()),
                                    pitch * nf, 165, None, eb.ctypes.data_as(C.POINTER(C.c_uint64)))

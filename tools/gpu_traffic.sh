@@ -3,16 +3,16 @@
 # four workloads' bench runs -> gpurun_out/traffic/<ROUND>_traffic_<wl>.json + *_kernel_stats.csv.
 # Each GPU step has its own limit; a failing step ends the script.
 R=${GRAFT_REPO_ROOT:-/root/repo}
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 O=$R/gpurun_out/traffic; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 BOPT="--steps 6 --warmup 1 --no-cpu --no-single-frame --no-e2e --no-decode --no-gop --no-check"
 for wl in ${WLS:-c2 c3 c4 c5}; do
   case $wl in
     c3) K=encode_kernel; G="";;
-    c4) K="encode4p_kernel<false, 4>"; G=2080768;;  # the 64-frame launches: 64 x ceil(32400 groups / 256) tiles x 256 threads
-    c5) K="encode4p_kernel<true, 4>"; G="";;        # the counting encoder the C5 step runs
-    *)  K="encode4p_kernel<false, 4>"; G="";;
+    c4) K="encode4p_kernel<false>"; G=2080768;;  # the 64-frame launches: 64 x ceil(32400 groups / 256) tiles x 256 threads
+    c5) K="encode4p_kernel<true>"; G="";;        # the counting encoder the C5 step runs
+    *)  K="encode4p_kernel<false>"; G="";;
   esac
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${wl}_trace -o run -- python3 $R/bench.py --workload $wl $BOPT > $O/${wl}_trace.log 2>&1 || { echo "$wl trace failed"; tail -3 $O/${wl}_trace.log; exit 1; }
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/${wl}_fetch -o run -- python3 $R/bench.py --workload $wl $BOPT > $O/${wl}_fetch.log 2>&1 || { echo "$wl fetch failed"; tail -3 $O/${wl}_fetch.log; exit 1; }
