@@ -523,33 +523,20 @@ __device__ __forceinline__ uint32_t size_block(uint32_t (&zp)[N * N / 2], int rl
 }
 
 // OR the low `len` bits of v (MSB first) into the LDS bit image at bit p (len + p%32 <= 64).
-#ifndef IE_SCATTER
-#define IE_SCATTER 2  // 2: left-aligned field, funnel-shifted into the word pair (-2.7 % against 0, the 64-bit shift); 1: no LDS write (profiling)
-#endif
 __device__ __forceinline__ void scatter_bits(uint32_t* img, uint32_t p, uint32_t v, uint32_t len) {
     // The image is the dynamic LDS area at LDS byte address 0 (the encode kernels allocate no static
     // LDS; tools/asmcheck.py checks their group_segment_fixed_size): the word pair's byte address
-    // straight from p, the second word through the instruction's offset field.
+    // straight from p, the second word through the instruction's offset field.  The field is
+    // left-aligned once, then funnel-shifted into the pair (-2.7 % against a 64-bit shift).
     (void)img;
     const uint32_t a = (p >> 3) & ~3u;
     const uint32_t s = p & 31u;
-    uint32_t hi, lo;
-    if (IE_SCATTER >= 2) {
-        const uint32_t u = v << (32u - len);  // the field left-aligned (len <= 32)
-        hi = u >> s;
-        lo = __builtin_amdgcn_alignbit(u, 0u, s);  // u << (32 - s), 0 for s = 0
-    } else {
-        const uint64_t x = uint64_t(v) << (64u - len - s);
-        hi = uint32_t(x >> 32);
-        lo = uint32_t(x);
-    }
-    // (one ds_or_b64 at a 4-byte-aligned address -- no alignment requirement assumed -- faulted the
-    // GPU: the two words stay separate ds_or_b32)
-    if (IE_SCATTER == 1) {
-        asm volatile("" ::"v"(a), "v"(hi), "v"(lo) : "memory");
-    } else {
-        asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a), "v"(hi), "v"(lo) : "memory");
-    }
+    const uint32_t u = v << (32u - len);  // the field left-aligned (len <= 32)
+    const uint32_t hi = u >> s;
+    const uint32_t lo = __builtin_amdgcn_alignbit(u, 0u, s);  // u << (32 - s), 0 for s = 0
+    // (two ds_or_b32, never one ds_or_b64: the address is only 4-byte aligned, and a 64-bit LDS
+    // atomic there raises a memory violation -- tools/asmcheck.py rejects 64-bit DS atomics)
+    asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a), "v"(hi), "v"(lo) : "memory");
 }
 
 // Branch-free variant: every pair is written (past Lw the packed coefficients are zero, so
@@ -1343,12 +1330,6 @@ __device__ __forceinline__ float round_block_lean4(const EncTables* __restrict__
 // least 8 groups in every tile (groups_per_frame % 8 == 0: every wave segment >= 160 bits) and
 // slot images that fit half a region (rec_bits <= 252).
 // =============================================================================================
-#ifndef IE_ENC_W
-#define IE_ENC_W 1  // 0: every 4x4 FAST launch runs encode_kernel<4> (A/B builds)
-#endif
-#ifndef IE_W_DBG
-#define IE_W_DBG 0
-#endif
 #ifndef IE_W_AHEAD
 #define IE_W_AHEAD 2  // look-back windows per round trip (each holds 4 VGPRs live beside slots 2-3)
 #endif
@@ -1379,9 +1360,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     return v;
 }
 
-#ifndef IE_STORE2
-#define IE_STORE2 1  // 0: (A/B builds) the quad loop reads each word by itself (4-way LDS bank conflicts)
-#endif
 // One slot image I (bit 0 at absolute stream bit X) to the output words, by one wave: words
 // [r0, nw) counted from floor(X / 32), word r = alignbit(I[r - 1], I[r], X % 32) with I[-1] =
 // prev (the 32 bits before X); the partial word nw is left to whoever writes the next bits.
@@ -1396,54 +1374,39 @@ __device__ __forceinline__ void store_slot(uint32_t* __restrict__ out, const uin
         return bswap32(__builtin_amdgcn_alignbit(r ? am : prev, I[r], s));
     };
     uint32_t hd = min(nw - r0, uint32_t((4u - uint32_t((w0 + r0) & 3u)) & 3u));
-    if (IE_STORE2 && r0 + hd == 0u) hd = min(nw, 4u);  // (the quad loop needs I[r - 1]: word -1 is prev)
+    if (r0 + hd == 0u) hd = min(nw, 4u);  // (the quad loop needs I[r - 1]: word -1 is prev)
     if (uint32_t(lane) < hd) {
         const uint32_t v = word(r0 + lane);
         out[w0 + r0 + lane] = v;
         cnt(w0 + r0 + lane, v);
     }
     const uint32_t rq = r0 + hd, nq = (nw - rq) >> 2;
-    if (IE_STORE2) {
-        // output quad q = words rq + 4q .. +3 (16-byte aligned in out) needs I[rq + 4q - 1 ..
-        // rq + 4q + 3]: five words at offset d of the two 16-byte LDS quads from (rq - 1) / 4 + q,
-        // read whole (consecutive lanes, consecutive quads: no bank conflicts), d wave-uniform
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const uint32_t d = (rq - 1u) & 3u;
-        const v4u* I4 = reinterpret_cast<const v4u*>(I) + ((rq - 1u) >> 2);
-        uint32_t* const ob = out + (w0 + rq);
-        auto quads = [&](auto dc) {
-            constexpr uint32_t D = decltype(dc)::value;
-            for (uint32_t q = lane; q < nq; q += 64) {
-                const v4u A = I4[q], B = I4[q + 1];
-                const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-                const v4u v = {bswap32(__builtin_amdgcn_alignbit(W[D], W[D + 1], s)), bswap32(__builtin_amdgcn_alignbit(W[D + 1], W[D + 2], s)),
-                               bswap32(__builtin_amdgcn_alignbit(W[D + 2], W[D + 3], s)), bswap32(__builtin_amdgcn_alignbit(W[D + 3], W[D + 4], s))};
-                __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(ob + 4u * q));
-                cnt(w0 + rq + 4u * q, v.x);
-                cnt(w0 + rq + 4u * q + 1u, v.y);
-                cnt(w0 + rq + 4u * q + 2u, v.z);
-                cnt(w0 + rq + 4u * q + 3u, v.w);
-            }
-        };
-        if (d == 0u) quads(std::integral_constant<uint32_t, 0>{});
-        else if (d == 1u) quads(std::integral_constant<uint32_t, 1>{});
-        else if (d == 2u) quads(std::integral_constant<uint32_t, 2>{});
-        else quads(std::integral_constant<uint32_t, 3>{});
-    } else
-    for (uint32_t q = lane; q < nq; q += 64) {
-        const uint32_t r = rq + 4u * q;
-        const uint32_t am = I[max(r, 1u) - 1u];
-        const uint32_t a0 = r ? am : prev;
-        const uint32_t b0 = I[r], b1 = I[r + 1], b2 = I[r + 2], b3 = I[r + 3];
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const v4u v = {bswap32(__builtin_amdgcn_alignbit(a0, b0, s)), bswap32(__builtin_amdgcn_alignbit(b0, b1, s)),
-                       bswap32(__builtin_amdgcn_alignbit(b1, b2, s)), bswap32(__builtin_amdgcn_alignbit(b2, b3, s))};
-        __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(out + w0 + r));
-        cnt(w0 + r, v.x);
-        cnt(w0 + r + 1, v.y);
-        cnt(w0 + r + 2, v.z);
-        cnt(w0 + r + 3, v.w);
-    }
+    // output quad q = words rq + 4q .. +3 (16-byte aligned in out) needs I[rq + 4q - 1 ..
+    // rq + 4q + 3]: five words at offset d of the two 16-byte LDS quads from (rq - 1) / 4 + q,
+    // read whole (consecutive lanes, consecutive quads: no bank conflicts), d wave-uniform
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint32_t d = (rq - 1u) & 3u;
+    const v4u* I4 = reinterpret_cast<const v4u*>(I) + ((rq - 1u) >> 2);
+    uint32_t* const ob = out + (w0 + rq);
+    auto quads = [&](auto dc) {
+        constexpr uint32_t D = decltype(dc)::value;
+        for (uint32_t q = lane; q < nq; q += 64) {
+            const v4u A = I4[q], B = I4[q + 1];
+            const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+            const v4u v = {bswap32(__builtin_amdgcn_alignbit(W[D], W[D + 1], s)), bswap32(__builtin_amdgcn_alignbit(W[D + 1], W[D + 2], s)),
+                           bswap32(__builtin_amdgcn_alignbit(W[D + 2], W[D + 3], s)), bswap32(__builtin_amdgcn_alignbit(W[D + 3], W[D + 4], s))};
+            __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(ob + 4u * q));
+            cnt(w0 + rq + 4u * q, v.x);
+            cnt(w0 + rq + 4u * q + 1u, v.y);
+            cnt(w0 + rq + 4u * q + 2u, v.z);
+            cnt(w0 + rq + 4u * q + 3u, v.w);
+        }
+    };
+    if (d == 0u) quads(std::integral_constant<uint32_t, 0>{});
+    else if (d == 1u) quads(std::integral_constant<uint32_t, 1>{});
+    else if (d == 2u) quads(std::integral_constant<uint32_t, 2>{});
+    else quads(std::integral_constant<uint32_t, 3>{});
+
     const uint32_t rt = rq + 4u * nq;
     if (uint32_t(lane) < nw - rt) {
         const uint32_t v = word(rt + lane);
@@ -1517,7 +1480,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     const int ng = min(TG, a.groups_per_frame - tif * TG);
     const int nbw = 4 * min(GW, max(0, ng - GW * wv));  // blocks of this wave
     const int wlast = (ng - 1) / GW;                    // the tile's last non-empty wave
-    if (!(IE_W_DBG & 64) && g.nblk) {
+    if (g.nblk) {
         // pixel row r of the wave's block j at reg[r BW + j]: a lane's 16 bytes are its group's row
         const uint8_t* base = a.y + size_t(frame) * a.frame_pitch + size_t(g.byi) * N * a.stride + size_t(g.bx0) * N;
 #pragma unroll
@@ -1543,16 +1506,8 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         block_pixels<N, 1>(rows, 0, x);
         uint32_t sf;
         float emax;
-        if (IE_W_DBG & 32) {  // profiling: no transform (quotients = pixels / 64)
-#pragma unroll
-            for (int k = 0; k < NN; k++) x[k] *= 0.015625f;
-            emax = round_block_lean4(tab, x, zp[b], &sf);
-            sf = 0;
-            emax = 0.0f;
-        } else {
-            quotients<N>(tab, x);
-            emax = round_block_lean4(tab, x, zp[b], &sf);
-        }
+        quotients<N>(tab, x);
+        emax = round_block_lean4(tab, x, zp[b], &sf);
         const uint32_t fb = (emax >= tab->lim_min) ? 8u : sf;
         if (64 * b + lane < nbw) flags |= fb << (4 * b);
         // pin the packed words here: otherwise the packing sinks to its first use and the 16
@@ -1573,7 +1528,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         for (int r = 0; r < N; r++) px.w[r] = reg[r * BW + 64 * b + owner];
         return px;
     };
-    if (!(IE_W_DBG & 1) && __ballot(flags != 0)) {
+    if (__ballot(flags != 0)) {
         const uint32_t sf = flags & 0x7777u;
         const uint32_t cnt = __popc(sf);
         uint32_t pre = 0, total = 0;
@@ -1599,8 +1554,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
                 const int k = Structural<N>::k[0] * (s == 0) + Structural<N>::k[1] * (s == 1) + Structural<N>::k[2] * (s == 2);
                 const int y = exact_coef_row<N>(srow + k * NN, srow[NN * NN + k], srow[NN * NN + NN + k],
                                                 srow[NN * NN + 2 * NN + k], px);
-                res[lane] = (IE_W_DBG & 128) ? (px.w[0] & 0xFFFFu)  // profiling: no FP64 arithmetic
-                                             : uint32_t(y) & 0xFFFFu;
+                res[lane] = uint32_t(y) & 0xFFFFu;
             }
             wave_sync();
             // the owners take their results back: the flagged positions in bit order, each a
@@ -1683,7 +1637,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
 #pragma unroll
     for (int b = 0; b < NS; b++) {
         const bool valid = 64 * b + lane < nbw;
-        if (!(IE_W_DBG & 4) && a.coef && valid) {
+        if (a.coef && valid) {
             int16_t* dst = a.coef + (size_t(frame) * a.by * a.bx + k0 + 64 * b + lane) * NN;
 #pragma unroll
             for (int k = 0; k < NN; k++) {
@@ -1757,7 +1711,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
         for (uint32_t q = lane; q < nq; q += 64) *reinterpret_cast<u32x4*>(reg + 4 * q) = u32x4{0u, 0u, 0u, 0u};
     };
     auto emit_slot = [&](int b) {  // slot b at its place in its pair's image
-        if (!(IE_W_DBG & 8) && rb[b]) {
+        if (rb[b]) {
             const uint32_t p = reg_bit0 + (Sb[b] - Sb[b & 2]) + off[b];
             if (a.tri && a.rle) emit_block3(smem, p, zp[b], blw[b]);
             else emit_block2<N>(smem, p, zp[b], blw[b], a.rle);
@@ -1775,7 +1729,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     // ------------------------------------------------------------ look-back (wave 0)
     const bool chain_last = a.segmented ? (tif == a.tiles_per_frame - 1) : (t == a.ntiles - 1);
     uint32_t* const out = a.out + (a.segmented ? uint64_t(frame) * a.out_pitch_words : 0ull);
-    if (deep && chain_pos != 0 && !(IE_W_DBG & 16)) {
+    if (deep && chain_pos != 0) {
         // every wave sums its windows in order, up to the first with an inclusive prefix (read
         // again until every value it needs is published; its predecessors never wait on this
         // tile), for wave 0 to combine
@@ -1818,9 +1772,6 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
             // chain start: the bits before start_bit belong to the caller (header)
             const uint32_t s = uint32_t(start_bit & 31);
             ptail = s ? (bswap32(out[start_bit >> 5]) >> (32 - s)) : 0u;
-        } else if (IE_W_DBG & 16) {  // profiling: no look-back (every tile at a made-up offset)
-            excl = uint64_t(tif) * 110000u;
-            if (lane == 0) publish(a.st, t, 1, a.tag, excl + A);
         } else {
             bool done = false;
             if (deep) {  // the waves' sums in predecessor order, up to the first window with an inclusive prefix
@@ -1861,7 +1812,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
     asm volatile("; PHASE w8" ::: "memory");
 
     // ------------------------------------------------------------ store, slot by slot
-    if (!(IE_W_DBG & 2) && Tw) {
+    if (Tw) {
         // (readfirstlane returns int: zero-extend each half, or a prefix of 2^31 bits or more
         // would sign-extend into the high word)
         const uint64_t excl = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(misc[8]))) |
@@ -2076,6 +2027,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
     const uint64_t start_bit = a_.start_dev ? *a_.start_dev : a_.start_bit;
     const bool deep = a_.deep_lb != 0;
     lds_barrier();  // every wave's pixels, the rows, the A fragments (and the HIST bins) visible
+    if (IE_PROFILE && a_.stamps && lane == 0) a_.stamps[size_t(t) * kStamps + wv * 16 + 11] = __builtin_amdgcn_s_memrealtime();
     KArgs& a = *ka;
     // (the tile's geometry is uniform: held in SGPRs, not in VGPRs the compiler would keep -- and
     // spill -- across the tile)
@@ -2548,7 +2500,7 @@ int launch_encode4w(const EncArgs& a, hipStream_t s);
 int launch_encode(const EncArgs& a0, int n, bool exact, hipStream_t s, int bpt) {
     EncArgs a = a0;
     // 4x4 FAST over whole 16-byte groups: the wave-local encoders (encode4p_kernel)
-    if (IE_ENC_W && n == 4 && !exact && bpt == 4 && a.vec_ok && a.bx % 4 == 0 &&
+    if (n == 4 && !exact && bpt == 4 && a.vec_ok && a.bx % 4 == 0 &&
         a.groups_per_frame % 8 == 0 && a.rec_bits <= 252 && !a.ablate)
         return launch_encode4w(a, s);
     a.img_words = image_words_for(n, bpt, a.rec_bits);

@@ -120,7 +120,8 @@ for spec in args.libs:
             out = shared_out[rot_o[0]]
         if args.op == "frames":  # (eb[0] = the stream's end bit; compared over the whole stream)
             r = L.ie_encode_frames(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, nf, 1, 0, C.c_void_p(out.data_ptr()),
-                                   pitch * nf, 165, None, eb.ctypes.data_as(C.POINTER(C.c_uint64)))
+                                   pitch * nf, 165, None,
+                                   eb.ctypes.data_as(C.POINTER(C.c_uint64)) if sizes else None)  # (timed: async)
             if r != 0:
                 raise RuntimeError(L.ie_last_error(hnd))
             return
