@@ -64,7 +64,7 @@ WORKLOADS = {
     # GPU (one launch of 64 1080p frames, 8 128 tiles: 0.260 of HBM against 0.234 for two 32-frame
     # launches, round 4) and 2 above, where the first sub-batch's gather overlaps the second's encode
     # (rank 0's ingress of the other ranks' streams, not the encode, sets the multi-GPU step)
-    "c4": dict(w=1920, h=1080, n=4, matrix="matrix.txt", batch=64, resident=128, gen="U", huffman=False,
+    "c4": dict(w=1920, h=1080, n=4, matrix="matrix.txt", batch=64, resident=256, gen="U", huffman=False,
                chunks=None, golden="vidU1080x3_4x4"),
     "c5": dict(w=3840, h=2160, n=4, matrix="matrix.txt", batch=16, resident=64, gen="U", huffman=True,
                golden="synU4k_4x4_huff"),
