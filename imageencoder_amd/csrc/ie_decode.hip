@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kTPB) void huf_total_kernel(const uint32_t* wgsum, 
 //                      lanes decode the records: dequantise (Block.cpp:163-169), FP64 IDCT in the
 //                      reference's order (algo.cpp:343-363), +128, clamp, truncate
 //                      (Block.cpp:100-107).
-constexpr uint32_t kNoOwner = 0xFFFFu;
+
 constexpr uint32_t kRoot = 0x8000u;  // table pass: a walk result that is an exit, not an owner
 
 // bits [p, p+l) of the LDS stream copy L (MSB-first words), l <= 32, p relative to the copy
@@ -263,13 +263,13 @@ __device__ __forceinline__ uint32_t decode_record(const uint32_t* L, uint32_t p,
     }
     if (length > NN) length = NN;
     const int sh = 16 - bl;
+    double t[NN];
+#pragma unroll
+    for (int k = 0; k < NN; k++) t[k] = 0.0;
     // Block::processIDCTMulQ: Y *= q, then temp[ij] += R[uv][ij] * Y[uv] over uv ascending.  A
     // zero Y term adds +-0: it leaves every partial sum unchanged but possibly the sign of a zero,
     // which +128 and the clamp erase, so a term is skipped when it is zero in every lane (the
     // branch stays uniform and the R rows come through the scalar cache).
-    double t[NN];
-#pragma unroll
-    for (int k = 0; k < NN; k++) t[k] = 0.0;
 #pragma unroll
     for (int uv = 0; uv < NN; uv++) {
         const int kz = izz.r[uv];
@@ -667,6 +667,30 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
     {
         uint32_t nxt = 0, p = 0, id = 0, ce = 0, nsteps = 0, wsteps = 0, rsteps = 0;
         bool act = false;
+        // One step of an active walk at p (< ce, a valid position): the record's header, the claim
+        // and the next position.  The claim's result is read last, so the atomic's round trip
+        // overlaps the header read and the bitmap reads of the next position.  The claim table is
+        // direct-mapped and lossy: a slot another position holds is not probed on -- the walk goes
+        // on unclaimed there and meets its owner's claims further on.
+        auto walk_step = [&]() {
+            nsteps++;
+            wsteps++;
+            const uint32_t head = lbits(L, s0 + p, 20);
+            const uint32_t o = atomicCAS(&H[(p * 2654435761u) >> 16 & HM], 0xFFFFFFFFu, (p << 16) | id);
+            const uint32_t np = next_valid_sel(VB, NZ, p + rec_len_sel<N>(head, a.rle), ce);
+            if (o != 0xFFFFFFFFu && (o >> 16) == p) {  // an earlier walk was here: take its exit
+                res[id] = uint16_t(o & 0xFFFFu);
+                act = false;
+                wsteps = 0;
+            } else if (np >= ce) {  // left the chunk
+                res[id] = uint16_t(kRoot | (np - ce));
+                act = false;
+                rsteps += wsteps;  // (profiling: steps of walks that reached the chunk's end)
+                wsteps = 0;
+            } else {
+                p = np;
+            }
+        };
         // (a) while the list lasts: idle lanes take the next walks, every step claims its position
         // (claiming 4-16 steps longer measured equal or slower)
         while (nxt < nw) {  // (wave-uniform)
@@ -676,45 +700,27 @@ __global__ __launch_bounds__(64) void rec_table2_kernel(RecParseArgs a) {
                 if (r < nw) {
                     id = wl[r];
                     const uint32_t j = id / D1, d = id - j * D1;
-                    p = (d < uint32_t(D)) ? j * C + d : vst[j];
+                    p = (d < uint32_t(D)) ? j * C + d : vst[j];  // (< the chunk's end: d < min(D, C))
                     ce = (j + 1u) * C;
                     act = true;
                 }
             }
             nxt += uint32_t(__popcll(need));
-            if (act) {
-                nsteps++;
-                wsteps++;
-                if (p >= ce) {  // left the chunk
-                    res[id] = uint16_t(kRoot | (p - ce));
-                    act = false;
-                    rsteps += wsteps;  // (profiling: steps of walks that reached the chunk's end)
-                    wsteps = 0;
-                } else {
-                    // the record's header read before the claim (independent of it, so both LDS
-                    // round trips overlap)
-                    const uint32_t head = lbits(L, s0 + p, 20);
-                    const uint32_t key = (p << 16) | id;
-                    // direct-mapped and lossy: a slot another position holds is not probed on --
-                    // the walk goes on unclaimed here and meets its owner's claims further on
-                    const uint32_t o = atomicCAS(&H[(p * 2654435761u) >> 16 & HM], 0xFFFFFFFFu, key);
-                    const uint32_t own = (o != 0xFFFFFFFFu && (o >> 16) == p) ? (o & 0xFFFFu) : kNoOwner;
-                    if (own != kNoOwner) {
-                        res[id] = uint16_t(own);
-                        act = false;
-                        wsteps = 0;
-                    } else {
-                        // (p is valid: a record starts here)
-                        p = next_valid_sel(VB, NZ, p + rec_len_sel<N>(head, a.rle), ce);
-                    }
-                }
-            }
+            if (act) walk_step();
         }
-        // (b) the list is empty: the walks still going (a chunk's true path and the odd wrong-phase
-        // survivor, which would meet it later) run to their chunk's end without claims -- no new
-        // walk can merge into them, so a claim would only stop a survivor a few steps early, and
-        // each step is a third cheaper without one
-        if (act) {
+        // (b) the list is empty.  The walks still going are many (a lane per walk when the list ran
+        // out, most of them on the same few paths).  8x8: they keep claiming until every lane's walk
+        // has left its chunk or merged -- they merge into each other.  4x4: they run to the chunk's
+        // end unclaimed, a third cheaper per step.  Measured on one 4K noise frame (tools/ab.py --op
+        // decode, same process): claims to the end take the 4x4 walk from 575 to 222 lane-steps per
+        // chunk and 47.6 to 32.7 steps of the longest lane (tools/dec_stamps.py), yet the decode
+        // 132.0 -> 135.4 us; 8x8 210.3 -> 206.6 us.
+        constexpr bool kClaimToEnd = N == 8;
+        if (kClaimToEnd) {
+            while (__ballot(act)) {
+                if (act) walk_step();
+            }
+        } else if (act) {
             while (p < ce) {
                 nsteps++;
                 wsteps++;

@@ -25,10 +25,11 @@ ap.add_argument("--frames", type=int, default=16)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--kind", default="U")
-ap.add_argument("--op", default="encode", choices=["encode", "counted", "frames"],
+ap.add_argument("--op", default="encode", choices=["encode", "counted", "frames", "decode"],
                 help="counted: time ie_encode_images_counted (the encoder with the fused byte histogram); "
                      "frames: ie_encode_frames, one concatenated stream (the C4 shape with --w 1920 --h 1080 "
-                     "--frames 64)")
+                     "--frames 64); decode: ie_decode_frames of one frame's stream (--frames 1; encoded once "
+                     "by the first variant, 165 header bits before it)")
 ap.add_argument("--w", type=int, default=3840)
 ap.add_argument("--h", type=int, default=2160)
 ap.add_argument("--rotate", type=int, default=1,
@@ -59,6 +60,7 @@ stream = torch.cuda.Stream()  # a real stream handle (the default stream's handl
 torch.cuda.set_stream(stream)
 variants = []
 shared_out = None
+dec_stream = []
 libs_loaded = {}
 for spec in args.libs:
     path, _, envs = spec.partition("@")
@@ -101,6 +103,16 @@ for spec in args.libs:
         L.ie_encode_frames.argtypes = [vp, vp, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                        vp, C.c_size_t, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
 
+    if args.op == "decode":
+        L.ie_decode_frames.argtypes = [vp, vp, C.c_size_t, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, vp,
+                                       C.c_size_t, C.c_size_t, C.POINTER(C.c_uint64)]
+        if not dec_stream:
+            r = L.ie_encode_images(hnd, C.c_void_p(y.data_ptr()), w, h, w, w * h, 1, 1, 0, C.c_void_p(out.data_ptr()),
+                                   pitch, 165, eb.ctypes.data_as(C.POINTER(C.c_uint64)))
+            assert r == 0
+            dec_stream.append((out[: (int(eb[0]) + 7) // 8].clone(), (int(eb[0]) + 7) // 8))
+        out = torch.empty(h * w, dtype=torch.uint8, device="cuda")  # (this variant's pixels)
+
     def run(L=L, hnd=hnd, out=out, pitch=pitch, eb=eb, sizes=False, env=env):
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
@@ -114,6 +126,15 @@ for spec in args.libs:
                     os.environ[k] = v
 
     def run1(L, hnd, out, pitch, eb, sizes):
+        if args.op == "decode":
+            src, nbytes = dec_stream[0]
+            e = C.c_uint64(0)
+            r = L.ie_decode_frames(hnd, C.c_void_p(src.data_ptr()), nbytes, 165, w, h, 1, 1, C.c_void_p(out.data_ptr()),
+                                   w, w * h, C.byref(e))
+            if r != 0:
+                raise RuntimeError(L.ie_last_error(hnd))
+            eb[0] = e.value
+            return
         y = ybatch(sizes)
         if not sizes:  # (the checked launch writes buffer 0)
             rot_o[0] = (rot_o[0] + 1) % args.rotate_out
@@ -148,7 +169,9 @@ for spec in args.libs:
 ref = variants[0]
 for v in variants:
     ok = np.array_equal(v["eb"], ref["eb"])
-    if ok and args.op == "frames":
+    if args.op == "decode":
+        ok = ok and torch.equal(v["out"], ref["out"])
+    elif ok and args.op == "frames":
         nb = (int(v["eb"][0]) + 7) // 8
         ok = torch.equal(v["out"][:nb], ref["out"][:nb])
     elif ok:
