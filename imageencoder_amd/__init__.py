@@ -121,12 +121,17 @@ def load_library(path: str | None = None) -> C.CDLL:
     return L
 
 
-def load_host_library(path: str = HOST_LIB_PATH) -> C.CDLL:
-    """Load libie_host.so: the file-level encoders/decoders (include/ie_host.hpp)."""
+def load_host_library(path: str | None = None) -> C.CDLL:
+    """Load libie_host.so: the file-level encoders/decoders (include/ie_host.hpp).  With IE_LIB set
+    (an A/B build of libie_hip.so) the libie_host.so beside it is used, so that both libraries
+    are the same build."""
     global _host
     if _host is not None:
         return _host
     load_library()
+    if path is None:
+        alt = os.environ.get("IE_LIB")
+        path = os.path.join(os.path.dirname(alt), "libie_host.so") if alt else HOST_LIB_PATH
     if not os.path.exists(path):
         raise IEError(IE_EHIP, f"{path} not built -- run `make host` (or __graft_entry__.build())")
     H = C.CDLL(path)

@@ -150,12 +150,18 @@ __device__ __forceinline__ void st_state(uint64_t* p, uint64_t v) {
 // ---- tile chain protocol ------------------------------------------------------------------
 // A chain is a sequence of tiles whose bit images are concatenated; tile t sits at position
 // chain_pos of its chain and its d-th predecessor (d = 0, 1, ...) is tile t - step*(d+1).
-// Every tile publishes three 8-byte granules, each with ONE agent-scope store so the payload
+// Every tile publishes its state with agent-scope stores of single 8-byte words, so the payload
 // travels inside the atomic word and no fence is needed:
-//   st[3t+0] = {tag:8 | aggregate:56}   as soon as the tile's bit count is known (before emission)
-//   st[3t+1] = {tag:8 | inclusive:56}   once the look-back has resolved the exclusive prefix
-//   st[3t+2] = {tag:8 | tail:32}        the last 32 bits of the chain up to and including t
+//   st[kGran t + 0] = {tag:8 | 0:1 | aggregate:55}  as soon as the tile's bit count is known
+//                   = {tag:8 | 1:1 | inclusive:55}  once the look-back has resolved the prefix
+//   st[kGran t + 2] = {tag:8 | tail:32}            the last 32 bits of the chain up to and
+//                                                  including t
 // The early aggregate lets successors resolve their offsets while this tile is still emitting.
+// The inclusive value overwrites the aggregate in the same word (both stores come from the one
+// thread that publishes the tile, in that order), so a probe reads ONE word per predecessor:
+// whichever it sees is a correct term of the look-back sum.  (Round 5 kept them in two words and
+// read both: every probed predecessor cost two uncached loads -- C4's single chain reads 1.7 KB of
+// other XCDs' state lines per tile.)
 // granules per tile in the state array: 3 packed (24 B per tile) or IE_GRAN_STRIDE words apart
 // (16: each tile's state in a 128-B line of its own, no false sharing between tiles)
 #ifndef IE_GRAN_STRIDE
@@ -164,8 +170,16 @@ __device__ __forceinline__ void st_state(uint64_t* p, uint64_t v) {
 constexpr int kGran = IE_GRAN_STRIDE;
 static_assert(kGran >= 3 && kGran <= kStateWordsPerTile, "three granules per tile within the allocation");
 
+#ifndef IE_STATE_1W
+#define IE_STATE_1W 1  // 0: aggregate and inclusive in two words (round 5; A/B builds)
+#endif
+constexpr uint64_t kIncl = 1ull << 55, kMask55 = kIncl - 1;
+// g = 0: the aggregate, 1: the inclusive prefix, 2: the tail
 __device__ __forceinline__ void publish(uint64_t* st, int t, int g, uint32_t tag, uint64_t v) {
-    st_state(&st[kGran * t + g], (uint64_t(tag) << 56) | (v & kMask56));
+    if (IE_STATE_1W && g < 2)
+        st_state(&st[kGran * t], (uint64_t(tag) << 56) | (g == 1 ? kIncl : 0ull) | (v & kMask55));
+    else
+        st_state(&st[kGran * t + g], (uint64_t(tag) << 56) | (v & kMask56));
 }
 
 // A look-back probe: the states of the 64 chain predecessors d0 .. d0+63 of tile t (both
@@ -183,6 +197,21 @@ struct Probe {
 #endif
 constexpr int kProbe0 = IE_PROBE0;
 
+// One probed predecessor: *status 2 (inclusive prefix), 1 (aggregate) or 0 (nothing published in
+// this launch), *val its value.
+__device__ __forceinline__ void probe_status(const Probe& p, uint32_t tag, int* status, uint64_t* val) {
+    if (IE_STATE_1W) {
+        const bool mine = uint32_t(p.ga >> 56) == tag;
+        *status = mine ? ((p.ga & kIncl) ? 2 : 1) : 0;
+        *val = p.ga & kMask55;
+    } else if (uint32_t(p.gi >> 56) == tag) {
+        *val = p.gi & kMask56;
+    } else {
+        *status = (uint32_t(p.ga >> 56) == tag) ? 1 : 0;
+        *val = p.ga & kMask56;
+    }
+}
+
 __device__ __forceinline__ Probe probe_issue(const uint64_t* st, int t, int chain_pos, int step, int d0,
                                              int width) {
     Probe p;
@@ -191,8 +220,8 @@ __device__ __forceinline__ Probe probe_issue(const uint64_t* st, int t, int chai
     const int d = d0 + lane;
     if (lane < width && chain_pos - 1 - d >= 0) {
         const int idx = t - step * (d + 1);
-        p.gi = ld_state(&st[kGran * idx + 1]);
         p.ga = ld_state(&st[kGran * idx]);
+        p.gi = IE_STATE_1W ? 0ull : ld_state(&st[kGran * idx + 1]);
     }
     if (d0 == 0 && lane == 0 && chain_pos > 0) p.gt = ld_state(&st[kGran * (t - step) + 2]);
     return p;
@@ -213,13 +242,14 @@ constexpr int kLbAhead = IE_LB_AHEAD;
 // deep: the launch's tiles all reach their look-back at about the same time (a launch too small to
 // fill the chip), so a tile's nearest inclusive predecessor is far away: the windows after the
 // first probe are issued at once, before it is evaluated.
-template <int kLbAhead = ie::kLbAhead>
+template <int kLbAhead = ie::kLbAhead, int kLbW = 64>
 __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_pos, int step, uint32_t tag,
                                   unsigned* err, unsigned* rounds = nullptr, bool deep = false,
                                   int width0 = kProbe0) {
     const int lane = lane_id();
     uint64_t excl = 0;
     int d0 = 0, width = width0;  // (the first probe's width)
+    const int wl = deep ? 64 : kLbW;  // the later windows' width
     unsigned spins = 0;
     Probe ahead[kLbAhead];  // windows d0 + 64, d0 + 128, ... already in flight
     int nahead = 0;
@@ -236,12 +266,7 @@ __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_
         if (lane >= width) {
             status = 3;  // outside the window
         } else if (chain_pos - 1 - d >= 0) {
-            if (uint32_t(p.gi >> 56) == tag) {
-                val = p.gi & kMask56;
-            } else {
-                status = (uint32_t(p.ga >> 56) == tag) ? 1 : 0;
-                val = p.ga & kMask56;
-            }
+            probe_status(p, tag, &status, &val);
         }
         const uint64_t incl = __ballot(status == 2);
         const int dP = incl ? (__ffsll((unsigned long long)incl) - 1) : width;
@@ -259,10 +284,10 @@ __device__ uint64_t lookback_wave(Probe p, const uint64_t* st, int t, int chain_
         excl += wave_sum64((lane <= dP && lane < width) ? val : 0ull);
         if (dP < width) return excl;
         d0 += width;
-        width = 64;
+        width = wl;
         if (nahead == 0) {  // the next kLbAhead windows in one round trip
 #pragma unroll
-            for (int k = kLbAhead - 1; k >= 0; k--) ahead[k] = probe_issue(st, t, chain_pos, step, d0 + 64 * (kLbAhead - 1 - k), 64);
+            for (int k = kLbAhead - 1; k >= 0; k--) ahead[k] = probe_issue(st, t, chain_pos, step, d0 + wl * (kLbAhead - 1 - k), wl);
             nahead = kLbAhead;
             if (rounds) *rounds += 0x10000;
         }
@@ -290,12 +315,7 @@ __device__ __forceinline__ WinSum window_sum(const Probe& p, int chain_pos, int 
     if (lane >= width) {
         status = 3;
     } else if (chain_pos - 1 - d >= 0) {
-        if (uint32_t(p.gi >> 56) == tag) {
-            val = p.gi & kMask56;
-        } else {
-            status = (uint32_t(p.ga >> 56) == tag) ? 1 : 0;
-            val = p.ga & kMask56;
-        }
+        probe_status(p, tag, &status, &val);
     }
     const uint64_t incl = __ballot(status == 2);
     const int dP = incl ? (__ffsll((unsigned long long)incl) - 1) : width;

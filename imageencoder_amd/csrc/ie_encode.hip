@@ -1330,8 +1330,15 @@ __device__ __forceinline__ float round_block_lean4(const EncTables* __restrict__
 // least 8 groups in every tile (groups_per_frame % 8 == 0: every wave segment >= 160 bits) and
 // slot images that fit half a region (rec_bits <= 252).
 // =============================================================================================
+// Look-back windows after the first probe, for launches that fill the chip (one small window at a
+// time: the nearest inclusive prefix is seldom far, and each probed predecessor is an uncached
+// load -- C4's one 8 128-tile chain: 2 windows of 64 108.6 us, 1 of 64 102.4, 1 of 32 101.1, 1 of
+// 16 104.4 us per 64-frame launch; C2 and one 4K frame unchanged; tools/ab.py, round 6)
 #ifndef IE_W_AHEAD
-#define IE_W_AHEAD 2  // look-back windows per round trip (each holds 4 VGPRs live beside slots 2-3)
+#define IE_W_AHEAD 1  // windows per round trip (each holds 4 VGPRs live beside slots 2-3)
+#endif
+#ifndef IE_W_LBW
+#define IE_W_LBW 32  // predecessors per window
 #endif
 #ifndef IE_W_WAVES
 #define IE_W_WAVES 6  // __launch_bounds__ occupancy hint (waves per SIMD): 76 VGPRs, no scratch (7 spills)
@@ -1787,7 +1794,7 @@ __global__ __launch_bounds__(256, IE_W_WAVES) void encode4w_kernel(EncArgs a, co
             }
             if (!done) {
                 const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr[0];
-                excl = lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
+                excl = lookback_wave<IE_W_AHEAD, IE_W_LBW>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
             }
             const bool have = uint32_t(pr[0].gt >> 56) == a.tag;  // (lane 0's probe read the tail)
             const bool split = ((start_bit + excl) & 31) != 0;
@@ -2355,7 +2362,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
             if (!done) {
                 const Probe p0 = deep ? probe_issue(a.st, t, chain_pos, step, 0, kProbe0) : pr[0];
                 excl = (IE_P_ABL & 4) ? uint64_t(chain_pos) * 30000u
-                                      : lookback_wave<IE_W_AHEAD>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
+                                      : lookback_wave<IE_W_AHEAD, IE_W_LBW>(p0, a.st, t, chain_pos, step, a.tag, a.err, nullptr, deep);
             }
             const bool have = uint32_t(pr[0].gt >> 56) == a.tag;
             const bool split = ((start_bit + excl) & 31) != 0;

@@ -143,10 +143,15 @@ __device__ __forceinline__ void first_full_body(const uint8_t* __restrict__ in, 
     __shared__ unsigned long long f[256];
     __shared__ uint8_t miss[256];
     const int tid = threadIdx.x;
-    f[tid] = ~0ull;
-    miss[tid] = (hist[tid] != 0u && first[tid] == ~0ull) ? 1 : 0;
-    __syncthreads();
     const uint64_t from = uint64_t(kFirstScanChunks) * kHistTile;
+    f[tid] = ~0ull;
+    // Missing = not within the scanned prefix [0, from): the scan's positions are final, and this
+    // pass writes only positions >= from.  (Round 5 tested first == ~0: a workgroup of a later
+    // range that finished first had already lowered first[v], so a workgroup of an earlier range
+    // starting after it skipped v and the later position stood -- intermittently wrong
+    // dictionaries in the counted pipeline's late-values case.)
+    miss[tid] = (hist[tid] != 0u && first[tid] >= from) ? 1 : 0;
+    __syncthreads();
     for (uint64_t base = from + uint64_t(blockIdx.x) * kHistTile; base < n; base += uint64_t(gridDim.x) * kHistTile) {
         const uint64_t p = base + uint64_t(tid) * 16;
         for (int e = 0; e < 16; e++)

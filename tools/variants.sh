@@ -13,5 +13,8 @@ while [ $# -ge 2 ]; do
   wait
   L=imageencoder_amd/lib/var_$name; mkdir -p $L
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $d/*.o -o $L/libie_hip.so
+  # the host library beside it, bound to this build (rpath $ORIGIN; imageencoder_amd loads it
+  # when IE_LIB points here)
+  g++ -shared -fopenmp build/host/*.o -L$L -lie_hip -Wl,-rpath,'$ORIGIN' -o $L/libie_host.so
   echo "built $L/libie_hip.so ($flags)"
 done
