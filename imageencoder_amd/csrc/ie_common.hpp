@@ -350,6 +350,14 @@ __device__ __forceinline__ void chain_publish_count(uint64_t* st, int t, int cha
     if (chain_pos == 0) publish(st, t, 1, tag, A);
 }
 
+// chain_resolve's look-back windows after the first probe (encode_kernel, pack_kernel)
+#ifndef IE_CR_AHEAD
+#define IE_CR_AHEAD 1
+#endif
+#ifndef IE_CR_LBW
+#define IE_CR_LBW 32
+#endif
+
 // Phase B, after the LDS image is complete (all threads): tail publication, look-back from the
 // probe `pr` wave 0 issued after phase A, and the
 // values the store needs (wave 0 resolves; the others wait at the closing barrier).  out: the
@@ -378,7 +386,8 @@ __device__ __forceinline__ uint64_t chain_resolve(uint64_t* st, int t, int chain
     }
     if (chain_pos != 0 && tid < 64) {
         unsigned rounds = 0, polls = 0;
-        const uint64_t excl = lookback_wave(pr, st, t, chain_pos, step, tag, err, dbg ? &rounds : nullptr, deep);
+        const uint64_t excl = lookback_wave<IE_CR_AHEAD, IE_CR_LBW>(pr, st, t, chain_pos, step, tag, err,
+                                                                    dbg ? &rounds : nullptr, deep);
         if (tid == 0) {
             publish(st, t, 1, tag, excl + A);
             const bool have = uint32_t(pr.gt >> 56) == tag;
