@@ -352,6 +352,7 @@ def main():
             # themselves come from the counting encoder) and the pack; algorithmic bytes = the
             # payload bytes the pack reads + the Huffman bytes it writes
             th, tp, nin, nout = [], [], 0, 0
+            codec.set_stage_timing(True)  # (outside the timed region: the events cost the step time)
             for i in range(5):
                 slot = i % nslots
                 codec.encode_images(frames[slot * B:(slot + 1) * B], w, h, outs[0], out_pitch=pitch, nframes=B,
@@ -363,6 +364,7 @@ def main():
                 eb = ends_per_slot[slot]
                 nin += sum((int(e) + 7) // 8 for e in eb)
                 nout += sum(int(x) for x in hs)
+            codec.set_stage_timing(False)
             t_h, t_p = float(np.median(th)) / 1e3, float(np.median(tp)) / 1e3
             hbytes = (nin + nout) / 5
             # the counting encoder the step really runs (encode_kernel<4,HIST>: it also counts the

@@ -61,6 +61,7 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.ie_set_quant.argtypes = [vp, u16p, C.c_int]
     L.ie_cos_table.argtypes = [vp, vp]
     L.ie_last_stage_ms.argtypes = [vp, C.c_int, C.POINTER(C.c_float)]
+    L.ie_set_stage_timing.argtypes = [vp, C.c_int]
     L.ie_stream_bound.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
     L.ie_stream_bound.restype = C.c_size_t
     L.ie_encode_frames.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
@@ -326,6 +327,11 @@ class Codec:
         assert q.size == n * n
         self._chk(self.L.ie_set_quant(self.h, q.ctypes.data, n))
         self.n = n
+
+    def set_stage_timing(self, on: bool) -> None:
+        """Record HIP events around the batched Huffman stages (for :meth:`last_stage_ms`; off by
+        default, the events delay the pipelined launches)."""
+        self._chk(self.L.ie_set_stage_timing(self.h, int(bool(on))))
 
     def last_stage_ms(self, stage: int) -> float:
         """Device time (ms) of the last batched Huffman histogram (0) or pack (1) (ie_last_stage_ms)."""

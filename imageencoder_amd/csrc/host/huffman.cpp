@@ -212,8 +212,15 @@ static int trees_and_pack(ie_ctx* c, const uint8_t* din, size_t in_pitch, const 
     };
     // one tree per string on OpenMP's persistent thread team (no thread start-up per call)
     const int T = int(std::min<size_t>(K, size_t(std::max(1, std::min(16, omp_get_max_threads())))));
+#ifdef IE_HOST_PROFILE
+    const auto b0 = std::chrono::steady_clock::now();
+#endif
 #pragma omp parallel for schedule(dynamic, 1) num_threads(T) if (T > 1)
     for (int k = 0; k < int(K); k++) build(size_t(k));
+#ifdef IE_HOST_PROFILE
+    fprintf(stderr, "[finish] %d trees on %d threads %.1f us\n", count, T,
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - b0).count());
+#endif
     for (size_t k = 0; k < K; k++)
         if (!ok[k]) return (err = errs[k], IE_EINVAL);
     size_t pp = 4;
@@ -268,6 +275,9 @@ int huffman_device_batch(ie_ctx* c, const uint8_t* din, size_t in_pitch, const u
 // ie_huffman_hist_batch_ends_async(slot) -- waits for that slot's histograms, then trees + pack.
 int huffman_device_batch_finish(ie_ctx* c, const uint8_t* din, size_t in_pitch, int count, int slot, uint8_t* dout,
                                 size_t out_pitch, int64_t* bytes, std::string& err) {
+#ifdef IE_HOST_PROFILE  // (profiling builds: host time of the wait and of the trees + pack issue)
+    const auto h0 = std::chrono::steady_clock::now();
+#endif
     const size_t K = size_t(count);
     std::vector<uint32_t> hist(256 * K);
     std::vector<uint64_t> first(256 * K);
@@ -276,7 +286,16 @@ int huffman_device_batch_finish(ie_ctx* c, const uint8_t* din, size_t in_pitch, 
     std::vector<uint64_t> n(K, 0);
     for (size_t k = 0; k < K; k++)
         for (int b = 0; b < 256; b++) n[k] += hist[256 * k + b];
+#ifdef IE_HOST_PROFILE
+    const auto h1 = std::chrono::steady_clock::now();
+    r = trees_and_pack(c, din, in_pitch, n.data(), count, hist.data(), first.data(), dout, out_pitch, bytes, err);
+    const auto h2 = std::chrono::steady_clock::now();
+    fprintf(stderr, "[finish] wait %.1f us, trees + pack %.1f us\n",
+            std::chrono::duration<double, std::micro>(h1 - h0).count(), std::chrono::duration<double, std::micro>(h2 - h1).count());
+    return r;
+#else
     return trees_and_pack(c, din, in_pitch, n.data(), count, hist.data(), first.data(), dout, out_pitch, bytes, err);
+#endif
 }
 
 int Huffman::encode(ie_ctx* c, const uint8_t* in, size_t n, std::vector<uint8_t>& out) {

@@ -49,6 +49,7 @@ struct ie_ctx {
     bool use_ticket = false;            // order tiles with an atomic ticket (after a timeout)
     hipEvent_t stage_ev[4] = {};        // timing events around the last batched histogram [0,1] / pack [2,3]
     bool stage_rec[2] = {false, false};
+    bool stage_timing = false;          // ie_set_stage_timing
     int fake_timeouts = 0;              // debug (IE_FAKE_TIMEOUTS): report this many look-back timeouts
     bool fake_fired = false;            // a faked timeout was reported (the redo paths dirty the output first)
     // Asynchronous launches (no read-back) since the last error read: a look-back timeout found
@@ -507,6 +508,7 @@ int prepare_state(ie_ctx* c, int ntiles, int nframes) {
 // reports the increments since the previous read.
 // Timing marks around the batched Huffman stages (ie_last_stage_ms): event i on the context's stream.
 int stage_mark(ie_ctx* c, int i) {
+    if (!c->stage_timing) return IE_OK;  // (ie_set_stage_timing: off by default)
     if (!c->stage_ev[i]) HIPCHK(c, hipEventCreate(&c->stage_ev[i]));
     HIPCHK(c, hipEventRecord(c->stage_ev[i], c->stream));
     if (i & 1) c->stage_rec[i >> 1] = true;
@@ -1665,6 +1667,13 @@ int ie_set_quant(ie_ctx* c, const uint16_t* q, int n) {
     HIPCHK(c, hipMemcpy(c->d_tab, c->h_tab, sizeof(ie::EncTables), hipMemcpyHostToDevice));
     c->n = n;
     std::memcpy(c->q, q, sizeof(uint16_t) * n * n);
+    return IE_OK;
+}
+
+int ie_set_stage_timing(ie_ctx* c, int on) {
+    if (!c) return IE_EINVAL;
+    c->stage_timing = on != 0;
+    if (!c->stage_timing) c->stage_rec[0] = c->stage_rec[1] = false;  // (stale marks are not reported)
     return IE_OK;
 }
 

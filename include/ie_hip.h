@@ -240,9 +240,11 @@ int ie_huffman_pack_batch(ie_ctx* ctx, const uint8_t* in, size_t in_pitch, const
 /* Device time of the last batched Huffman stage on the context's stream (HIP events around its
  * launches): stage 0 = the histogram / first-occurrence kernels of ie_huffman_hist_batch_ends_async,
  * stage 1 = the pack kernel of ie_huffman_pack_batch.  Only those two batched calls record the
- * events (two hipEventRecord each); the single-string ie_huffman_hist / ie_huffman_pack do not.
- * Waits for the stage to finish. */
+ * events (two hipEventRecord each), and only while ie_set_stage_timing(ctx, 1) is in effect (off by
+ * default: the timing events cost the pipelined C5 step about 15 us of device idle time); the
+ * single-string ie_huffman_hist / ie_huffman_pack never do.  Waits for the stage to finish. */
 int ie_last_stage_ms(ie_ctx* ctx, int stage, float* ms);
+int ie_set_stage_timing(ie_ctx* ctx, int on);
 
 /* Copy n bytes into out starting at bit start_bit, i.e. shifted by start_bit % 8 (the "no gain"
  * path of Huffman.cpp:329-341 writes '0' + the input: start_bit = 1).  Device input and output:
