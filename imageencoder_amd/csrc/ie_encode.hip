@@ -2266,7 +2266,7 @@ __global__ __launch_bounds__(256, HIST ? IE_P_WAVES_HIST : IE_P_WAVES) void enco
         if (deep) {
 #pragma unroll
             for (int i = 0; i < DW; i++) pr[i] = probe_issue(a.st, t, chain_pos, step, 64 * (DW * wv + i), 64);
-        } else if (wv == 0) {
+        } else if (wv == 0 && !(IE_P_ABL & 4)) {  // (look-back left out: no probe either)
             pr[0] = probe_issue(a.st, t, chain_pos, step, 0, kProbe0);
         }
     }
