@@ -497,6 +497,37 @@ def test_counted_encode_histogram_batch_sizes(codec):
     check(8, 4, read=True)
 
 
+@pytest.mark.gpu
+def test_stage_timing_opt_in(codec):
+    """ie_last_stage_ms reports the batched Huffman stages only while ie_set_stage_timing is on
+    (off by default: the events idle the pipelined step); the outputs do not depend on it."""
+    import torch
+    from imageencoder_amd import IEError, stream_bound, write_header
+    n, q, w, h, f = 4, O.read_matrix("matrix.txt", 4), 256, 128, 3
+    codec.set_quant(q, n)
+    hdr, hb = write_header(n, q, True, w, h, huffman=True)
+    pitch = (stream_bound(w, h, n, 1, hb) + 255) // 256 * 256
+    y = torch.from_numpy(synth.frames("U", w, h, f, seed=9)).cuda()
+    out = torch.zeros(pitch * f, dtype=torch.uint8, device="cuda")
+    hout = torch.zeros(2 * pitch * f, dtype=torch.uint8, device="cuda")
+    results = []
+    for on in (False, True):
+        codec.set_stage_timing(on)
+        codec.encode_images(y, w, h, out, out_pitch=pitch, nframes=f, start_bit=hb, want_sizes=False)
+        codec.huffman_begin_after_encode(out, pitch, f, 0)  # (the batched calls that record the events)
+        sizes = codec.huffman_finish_after_encode(out, pitch, f, 0, hout, 2 * pitch)
+        codec.sync()
+        torch.cuda.synchronize()
+        results.append((sizes, hout.clone()))
+        if on:
+            assert codec.last_stage_ms(0) > 0.0 and codec.last_stage_ms(1) > 0.0
+        else:
+            with pytest.raises(IEError):
+                codec.last_stage_ms(1)
+    codec.set_stage_timing(False)
+    assert results[0][0] == results[1][0] and torch.equal(results[0][1], results[1][1])
+
+
 # ------------------------------------------------- multi-segment decode; one-launch path (opt-in)
 @pytest.mark.parametrize("huffman", [False, True])
 @pytest.mark.parametrize("n", [4, 8])
